@@ -1,0 +1,514 @@
+// C-ABI implementation (include/rtgpu.h): scene ingest, device upload, render.
+#include <hip/hip_runtime.h>
+
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "host_assets.hpp"
+#include "host_scene.hpp"
+#include "rtg_device.hpp"
+#include "rtg_kernels.hpp"
+#include "rtgpu.h"
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const char* fmt, ...) {
+    char buf[1024];
+    va_list ap;
+    va_start(ap, fmt);
+    std::vsnprintf(buf, sizeof(buf), fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIP_TRY(expr)                                                                              \
+    do {                                                                                           \
+        hipError_t e_ = (expr);                                                                    \
+        if (e_ != hipSuccess) return set_err(RTG_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_)); \
+    } while (0)
+
+// Ken Perlin's reference permutation ("Improving Noise", SIGGRAPH 2002), duplicated to
+// 512 entries, and the 12 cube-edge gradients -- the tables perlinTexture.cpp:5-37 uses.
+const int kPerm256[256] = {
+    151, 160, 137, 91,  90,  15,  131, 13,  201, 95,  96,  53,  194, 233, 7,   225, 140, 36,  103, 30,  69,  142,
+    8,   99,  37,  240, 21,  10,  23,  190, 6,   148, 247, 120, 234, 75,  0,   26,  197, 62,  94,  252, 219, 203,
+    117, 35,  11,  32,  57,  177, 33,  88,  237, 149, 56,  87,  174, 20,  125, 136, 171, 168, 68,  175, 74,  165,
+    71,  134, 139, 48,  27,  166, 77,  146, 158, 231, 83,  111, 229, 122, 60,  211, 133, 230, 220, 105, 92,  41,
+    55,  46,  245, 40,  244, 102, 143, 54,  65,  25,  63,  161, 1,   216, 80,  73,  209, 76,  132, 187, 208, 89,
+    18,  169, 200, 196, 135, 130, 116, 188, 159, 86,  164, 100, 109, 198, 173, 186, 3,   64,  52,  217, 226, 250,
+    124, 123, 5,   202, 38,  147, 118, 126, 255, 82,  85,  212, 207, 206, 59,  227, 47,  16,  58,  17,  182, 189,
+    28,  42,  223, 183, 170, 213, 119, 248, 152, 2,   44,  154, 163, 70,  221, 153, 101, 155, 167, 43,  172, 9,
+    129, 22,  39,  253, 19,  98,  108, 110, 79,  113, 224, 232, 178, 185, 112, 104, 218, 246, 97,  228, 251, 34,
+    242, 193, 238, 210, 144, 12,  191, 179, 162, 241, 81,  51,  145, 235, 249, 14,  239, 107, 49,  192, 214, 31,
+    181, 199, 106, 157, 184, 84,  204, 176, 115, 121, 50,  45,  127, 4,   150, 254, 138, 236, 205, 93,  222, 114,
+    67,  29,  24,  72,  243, 141, 128, 195, 78,  66,  215, 61,  156, 180};
+const float kGrad[36] = {1, 1, 0, -1, 1, 0, 1, -1, 0, -1, -1, 0, 1, 0, 1, -1, 0, 1,
+                         1, 0, -1, -1, 0, -1, 0, 1, 1, 0, -1, 1, 0, 1, -1, 0, -1, -1};
+
+template <typename T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t n = 0;
+    ~DevBuf() { if (p) (void)hipFree(p); }
+    hipError_t upload(const std::vector<T>& v) {
+        n = v.size();
+        if (n == 0) return hipSuccess;
+        hipError_t e = hipMalloc(&p, n * sizeof(T));
+        if (e != hipSuccess) return e;
+        return hipMemcpy(p, v.data(), n * sizeof(T), hipMemcpyHostToDevice);
+    }
+};
+
+void f4(float* dst, const rtg_float3& v, float w = 0.f) { dst[0] = v.x; dst[1] = v.y; dst[2] = v.z; dst[3] = w; }
+
+}  // namespace
+
+struct rtg_scene {
+    int device = 0;
+    rtg::DevScene ds;
+    std::vector<rtg_camera> cameras;
+    int max_depth = 0;
+    DevBuf<float4> node_a, node_b, tri_v0, tri_e1, tri_e2, face_n;
+    DevBuf<int> node_cnt, env_images;
+    DevBuf<float2> face_uv;
+    DevBuf<rtg::DevObject> objects;
+    DevBuf<rtg::DevMaterial> materials;
+    DevBuf<rtg::DevBrdf> brdfs;
+    DevBuf<rtg::DevTexture> textures;
+    DevBuf<rtg::DevImage> images;
+    DevBuf<float> texels;
+    DevBuf<rtg::DevPointLight> point_lights;
+    DevBuf<rtg::DevAreaLight> area_lights;
+    DevBuf<rtg::DevDirLight> dir_lights;
+    DevBuf<rtg::DevSpotLight> spot_lights;
+    DevBuf<rtg::DevCounters> counters;
+    // scratch for the host-buffer entry point
+    float* d_hdr = nullptr;
+    unsigned char* d_ldr = nullptr;
+    size_t d_pixels = 0;
+    ~rtg_scene() {
+        if (d_hdr) (void)hipFree(d_hdr);
+        if (d_ldr) (void)hipFree(d_ldr);
+    }
+};
+
+extern "C" {
+
+const char* rtg_last_error(void) { return g_err.c_str(); }
+int rtg_abi_version(void) { return RTG_ABI_VERSION; }
+
+int rtg_host_scene_load_xml(const char* xml_path, rtg_host_scene** out) {
+    if (!xml_path || !out) return set_err(RTG_ERR_INVALID, "null argument");
+    *out = nullptr;
+    std::unique_ptr<rtg_host_scene> hs(new (std::nothrow) rtg_host_scene);
+    if (!hs) return set_err(RTG_ERR_NOMEM, "out of memory");
+    std::string err;
+    int rc = hs->s.load(xml_path, err);
+    if (rc != RTG_OK) return set_err(rc, "%s: %s", xml_path, err.c_str());
+    *out = hs.release();
+    return RTG_OK;
+}
+
+const rtg_scene_desc* rtg_host_scene_desc(const rtg_host_scene* hs) { return hs ? &hs->s.desc : nullptr; }
+void rtg_host_scene_free(rtg_host_scene* hs) { delete hs; }
+
+int rtg_desc_camera_info(const rtg_scene_desc* d, int camera, int32_t* width, int32_t* height, int32_t* spp,
+                         int32_t* has_tonemapper) {
+    if (!d || camera < 0 || camera >= d->num_cameras) return set_err(RTG_ERR_INVALID, "bad camera index %d", camera);
+    const rtg_camera& c = d->cameras[camera];
+    if (width) *width = c.width;
+    if (height) *height = c.height;
+    if (spp) *spp = c.spp;
+    if (has_tonemapper) *has_tonemapper = c.has_tonemapper;
+    return RTG_OK;
+}
+
+int rtg_desc_counts(const rtg_scene_desc* d, int64_t* num_objects, int64_t* num_faces, int64_t* num_nodes,
+                    int64_t* num_lights) {
+    if (!d) return set_err(RTG_ERR_INVALID, "null desc");
+    if (num_objects) *num_objects = d->num_objects;
+    if (num_faces) *num_faces = d->num_faces;
+    if (num_nodes) *num_nodes = d->num_nodes;
+    if (num_lights)
+        *num_lights = (int64_t)d->num_point_lights + d->num_area_lights + d->num_dir_lights + d->num_spot_lights +
+                      d->num_env_lights + d->num_mesh_lights;
+    return RTG_OK;
+}
+
+int rtg_device_count(int32_t* count) {
+    if (!count) return set_err(RTG_ERR_INVALID, "null argument");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    *count = e == hipSuccess ? n : 0;
+    return RTG_OK;
+}
+
+int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
+    if (!d || !out) return set_err(RTG_ERR_INVALID, "null argument");
+    *out = nullptr;
+    if (d->num_mesh_lights > 0)
+        return set_err(RTG_ERR_UNSUPPORTED, "LightMesh (mesh light sampling) is not implemented on the GPU path yet");
+    if (d->max_recursion_depth > rtg::max_supported_depth())
+        return set_err(RTG_ERR_UNSUPPORTED, "MaxRecursionDepth %d > %d", d->max_recursion_depth, rtg::max_supported_depth());
+    for (int i = 0; i < d->num_objects; ++i) {
+        const rtg_object& o = d->objects[i];
+        if (o.tex_normal >= 0 || o.tex_bump >= 0)
+            return set_err(RTG_ERR_UNSUPPORTED, "normal / bump mapping is not implemented on the GPU path yet");
+        if (o.material < 0 || o.material >= d->num_materials) return set_err(RTG_ERR_INVALID, "object %d: bad material", i);
+        if (o.kind != RTG_OBJ_SPHERE && (o.mesh < 0 || o.mesh >= d->num_meshes))
+            return set_err(RTG_ERR_INVALID, "object %d: bad mesh", i);
+    }
+    for (int i = 0; i < d->num_images; ++i)
+        if (d->images[i].channels < 1 || !d->images[i].texels) return set_err(RTG_ERR_INVALID, "image %d: no texels", i);
+
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return set_err(RTG_ERR_HIP, "no HIP device available");
+    if (device < 0 || device >= ndev) return set_err(RTG_ERR_INVALID, "device %d out of range (%d devices)", device, ndev);
+    HIP_TRY(hipSetDevice(device));
+
+    std::unique_ptr<rtg_scene> sc(new (std::nothrow) rtg_scene);
+    if (!sc) return set_err(RTG_ERR_NOMEM, "out of memory");
+    sc->device = device;
+    sc->max_depth = d->max_recursion_depth;
+    sc->cameras.assign(d->cameras, d->cameras + d->num_cameras);
+
+    // ---- BVH: reference topology -> pre-order with skip links (rtg_device.hpp)
+    std::vector<float4> na, nb;
+    std::vector<int> ncnt;
+    na.reserve(d->num_nodes); nb.reserve(d->num_nodes); ncnt.reserve(d->num_nodes);
+    std::vector<int> meshBegin(d->num_meshes), meshEnd(d->num_meshes);
+    for (int m = 0; m < d->num_meshes; ++m) {
+        const rtg_mesh& M = d->meshes[m];
+        const rtg_bvh_node* N = d->nodes + M.node_offset;
+        const int base = (int)na.size();
+        meshBegin[m] = base;
+        // pre-order, recording each node's subtree end for the skip link
+        std::vector<int> order;
+        order.reserve(M.node_count);
+        std::vector<int> stack{0};
+        while (!stack.empty()) {
+            int k = stack.back();
+            stack.pop_back();
+            if (k < 0 || k >= M.node_count) return set_err(RTG_ERR_INVALID, "mesh %d: corrupt BVH", m);
+            order.push_back(k);
+            if (N[k].left >= 0) { stack.push_back(N[k].left + 1); stack.push_back(N[k].left); }
+        }
+        std::vector<int> pos(M.node_count, -1);
+        for (size_t i = 0; i < order.size(); ++i) pos[order[i]] = (int)i;
+        std::vector<int> size(M.node_count, 1);
+        for (int i = (int)order.size() - 1; i >= 0; --i) {
+            int k = order[i];
+            if (N[k].left >= 0) size[k] = 1 + size[N[k].left] + size[N[k].left + 1];
+        }
+        for (int k : order) {
+            const rtg_bvh_node& n = N[k];
+            int skip = base + pos[k] + size[k];
+            int first = n.left >= 0 ? -1 : M.face_offset + n.first;
+            float4 a, b;
+            a.x = n.bmin[0]; a.y = n.bmin[1]; a.z = n.bmin[2]; a.w = n.bmax[0];
+            b.x = n.bmax[1]; b.y = n.bmax[2];
+            std::memcpy(&b.z, &skip, 4);
+            std::memcpy(&b.w, &first, 4);
+            na.push_back(a); nb.push_back(b);
+            ncnt.push_back(n.left >= 0 ? 0 : n.count);
+        }
+        meshEnd[m] = (int)na.size();
+    }
+
+    // ---- faces (already BVH-permuted)
+    std::vector<float4> v0(d->num_faces), e1(d->num_faces), e2(d->num_faces), fn(d->num_faces);
+    bool anyUV = false;
+    for (int m = 0; m < d->num_meshes; ++m) anyUV |= d->meshes[m].has_uv != 0;
+    std::vector<float2> fuv(anyUV ? 3 * d->num_faces : 0);
+    for (int64_t f = 0; f < d->num_faces; ++f) {
+        const rtg_face& F = d->faces[f];
+        v0[f] = make_float4(F.v0.x, F.v0.y, F.v0.z, 0.f);
+        e1[f] = make_float4(F.v0.x - F.v1.x, F.v0.y - F.v1.y, F.v0.z - F.v1.z, 0.f);
+        e2[f] = make_float4(F.v0.x - F.v2.x, F.v0.y - F.v2.y, F.v0.z - F.v2.z, 0.f);
+        fn[f] = make_float4(F.n.x, F.n.y, F.n.z, 0.f);
+        if (anyUV) {
+            fuv[3 * f] = make_float2(F.uv0[0], F.uv0[1]);
+            fuv[3 * f + 1] = make_float2(F.uv1[0], F.uv1[1]);
+            fuv[3 * f + 2] = make_float2(F.uv2[0], F.uv2[1]);
+        }
+    }
+
+    // ---- objects
+    std::vector<rtg::DevObject> objs(d->num_objects);
+    for (int i = 0; i < d->num_objects; ++i) {
+        const rtg_object& o = d->objects[i];
+        rtg::DevObject& D = objs[i];
+        std::memset(&D, 0, sizeof(D));
+        D.kind = o.kind;
+        D.material = o.material;
+        D.flags = o.flags;
+        if (o.kind != RTG_OBJ_SPHERE) {
+            D.node_begin = meshBegin[o.mesh];
+            D.node_end = meshEnd[o.mesh];
+            if (d->meshes[o.mesh].has_uv) D.flags |= rtg::OBJF_HAS_UV;
+        }
+        D.tex_diffuse = o.tex_diffuse;
+        D.tex_specular = o.tex_specular;
+        D.tex_replace_all = o.tex_replace_all;
+        for (int k = 0; k < 3; ++k) { D.bmin[k] = o.bbox_min[k]; D.bmax[k] = o.bbox_max[k]; }
+        f4(D.mbv, o.motion_blur);
+        f4(D.center, o.center, o.radius);
+        for (int k = 0; k < 12; ++k) {
+            D.inv[k] = o.inv_transform[k];
+            D.invT[k] = o.inv_transpose[k];
+            D.baseInvT[k] = o.base_inv_transpose[k];
+        }
+    }
+    std::vector<rtg::DevMaterial> mats(d->num_materials);
+    for (int i = 0; i < d->num_materials; ++i) {
+        const rtg_material& m = d->materials[i];
+        rtg::DevMaterial& D = mats[i];
+        std::memset(&D, 0, sizeof(D));
+        D.type = m.type;
+        D.brdf = m.brdf;
+        f4(D.ambient, m.ambient); f4(D.diffuse, m.diffuse); f4(D.specular, m.specular); f4(D.mirror, m.mirror);
+        f4(D.absorption, m.absorption); f4(D.radiance, m.radiance);
+        D.phong_exponent = m.phong_exponent;
+        D.refractive_index = m.refractive_index;
+        D.absorption_index = m.absorption_index;
+        D.roughness = m.roughness;
+    }
+    std::vector<rtg::DevBrdf> brdfs(d->num_brdfs);
+    for (int i = 0; i < d->num_brdfs; ++i) {
+        std::memset(&brdfs[i], 0, sizeof(brdfs[i]));
+        brdfs[i].type = d->brdfs[i].type;
+        brdfs[i].energy_conserving = d->brdfs[i].energy_conserving;
+        brdfs[i].kd_fresnel = d->brdfs[i].kd_fresnel;
+        brdfs[i].exponent = d->brdfs[i].exponent;
+    }
+    std::vector<rtg::DevTexture> texs(d->num_textures);
+    for (int i = 0; i < d->num_textures; ++i) {
+        const rtg_texture& t = d->textures[i];
+        std::memset(&texs[i], 0, sizeof(texs[i]));
+        texs[i].kind = t.kind;
+        texs[i].blend = t.blend;
+        texs[i].image = t.image;
+        texs[i].nearest = t.nearest;
+        texs[i].noise_scale = t.noise_scale;
+        texs[i].bump_factor = t.bump_factor;
+        texs[i].normalizer = t.normalizer;
+        texs[i].noise_abs = t.noise_abs;
+    }
+    // texel pool; each image padded with one extra row + 4 floats so the reference's
+    // edge reads (bilinear p+1, 1-channel RGB reads) stay inside the allocation
+    std::vector<rtg::DevImage> imgs(d->num_images);
+    std::vector<float> pool;
+    for (int i = 0; i < d->num_images; ++i) {
+        const rtg_image& im = d->images[i];
+        imgs[i].width = im.width; imgs[i].height = im.height; imgs[i].channels = im.channels;
+        imgs[i].offset = (long long)pool.size();
+        size_t n = (size_t)im.width * im.height * im.channels;
+        pool.insert(pool.end(), im.texels, im.texels + n);
+        pool.insert(pool.end(), (size_t)im.width * im.channels + 4, 0.f);
+    }
+    std::vector<rtg::DevPointLight> pls(d->num_point_lights);
+    for (int i = 0; i < d->num_point_lights; ++i) {
+        f4(pls[i].pos, d->point_lights[i].position);
+        f4(pls[i].intensity, d->point_lights[i].intensity);
+    }
+    std::vector<rtg::DevAreaLight> als(d->num_area_lights);
+    for (int i = 0; i < d->num_area_lights; ++i) {
+        const rtg_area_light& a = d->area_lights[i];
+        std::memset(&als[i], 0, sizeof(als[i]));
+        f4(als[i].pos, a.position); f4(als[i].normal, a.normal); f4(als[i].radiance, a.radiance);
+        f4(als[i].u, a.u); f4(als[i].v, a.v);
+        als[i].extent = a.extent; als[i].area = a.area;
+    }
+    std::vector<rtg::DevDirLight> dls(d->num_dir_lights);
+    for (int i = 0; i < d->num_dir_lights; ++i) {
+        f4(dls[i].dir, d->dir_lights[i].dir);
+        f4(dls[i].radiance, d->dir_lights[i].radiance);
+    }
+    std::vector<rtg::DevSpotLight> sls(d->num_spot_lights);
+    for (int i = 0; i < d->num_spot_lights; ++i) {
+        const rtg_spot_light& s = d->spot_lights[i];
+        std::memset(&sls[i], 0, sizeof(sls[i]));
+        f4(sls[i].pos, s.position); f4(sls[i].dir, s.dir); f4(sls[i].intensity, s.intensity);
+        sls[i].coverage_deg = s.coverage_deg; sls[i].falloff_deg = s.falloff_deg;
+        sls[i].cos_half_coverage = s.cos_half_coverage; sls[i].cos_half_falloff = s.cos_half_falloff;
+    }
+    std::vector<int> envs(d->num_env_lights);
+    for (int i = 0; i < d->num_env_lights; ++i) {
+        envs[i] = d->env_lights[i].image;
+        if (envs[i] < 0 || envs[i] >= d->num_images) return set_err(RTG_ERR_INVALID, "env light %d: bad image", i);
+    }
+
+    HIP_TRY(sc->node_a.upload(na)); HIP_TRY(sc->node_b.upload(nb)); HIP_TRY(sc->node_cnt.upload(ncnt));
+    HIP_TRY(sc->tri_v0.upload(v0)); HIP_TRY(sc->tri_e1.upload(e1)); HIP_TRY(sc->tri_e2.upload(e2));
+    HIP_TRY(sc->face_n.upload(fn)); HIP_TRY(sc->face_uv.upload(fuv));
+    HIP_TRY(sc->objects.upload(objs)); HIP_TRY(sc->materials.upload(mats)); HIP_TRY(sc->brdfs.upload(brdfs));
+    HIP_TRY(sc->textures.upload(texs)); HIP_TRY(sc->images.upload(imgs)); HIP_TRY(sc->texels.upload(pool));
+    HIP_TRY(sc->point_lights.upload(pls)); HIP_TRY(sc->area_lights.upload(als)); HIP_TRY(sc->dir_lights.upload(dls));
+    HIP_TRY(sc->spot_lights.upload(sls)); HIP_TRY(sc->env_images.upload(envs));
+    std::vector<rtg::DevCounters> zero(1);
+    std::memset(zero.data(), 0, sizeof(rtg::DevCounters));
+    HIP_TRY(sc->counters.upload(zero));
+    {
+        int perm[512];
+        for (int i = 0; i < 512; ++i) perm[i] = kPerm256[i & 255];
+        if (rtg::upload_perlin_tables(perm, kGrad) != 0) return set_err(RTG_ERR_HIP, "perlin table upload failed");
+    }
+
+    rtg::DevScene& S = sc->ds;
+    std::memset(&S, 0, sizeof(S));
+    S.node_a = sc->node_a.p; S.node_b = sc->node_b.p; S.node_cnt = sc->node_cnt.p;
+    S.tri_v0 = sc->tri_v0.p; S.tri_e1 = sc->tri_e1.p; S.tri_e2 = sc->tri_e2.p; S.face_n = sc->face_n.p;
+    S.face_uv = sc->face_uv.p;
+    S.objects = sc->objects.p; S.materials = sc->materials.p; S.brdfs = sc->brdfs.p;
+    S.textures = sc->textures.p; S.images = sc->images.p; S.texels = sc->texels.p;
+    S.point_lights = sc->point_lights.p; S.area_lights = sc->area_lights.p; S.dir_lights = sc->dir_lights.p;
+    S.spot_lights = sc->spot_lights.p; S.env_images = sc->env_images.p;
+    S.num_objects = d->num_objects; S.num_point = d->num_point_lights; S.num_area = d->num_area_lights;
+    S.num_dir = d->num_dir_lights; S.num_spot = d->num_spot_lights; S.num_env = d->num_env_lights;
+    S.max_depth = d->max_recursion_depth;
+    S.bg_texture = d->bg_texture;
+    S.eps = d->shadow_epsilon;
+    S.ambient[0] = d->ambient_light.x; S.ambient[1] = d->ambient_light.y; S.ambient[2] = d->ambient_light.z;
+    for (int k = 0; k < 3; ++k) S.background[k] = d->background[k];
+    HIP_TRY(hipDeviceSynchronize());
+    *out = sc.release();
+    return RTG_OK;
+}
+
+void rtg_scene_destroy(rtg_scene* s) {
+    if (!s) return;
+    (void)hipSetDevice(s->device);
+    delete s;
+}
+
+static int prepare(rtg_scene* s, const rtg_render_opts* o, rtg::DevCamera& C, rtg::RenderParams& P) {
+    if (!s || !o) return set_err(RTG_ERR_INVALID, "null argument");
+    if (o->camera < 0 || o->camera >= (int)s->cameras.size()) return set_err(RTG_ERR_INVALID, "bad camera %d", o->camera);
+    const rtg_camera& c = s->cameras[o->camera];
+    if (c.path_tracing) return set_err(RTG_ERR_UNSUPPORTED, "path tracing (<Renderer>PathTracing) is not implemented yet");
+    if (c.width <= 0 || c.height <= 0) return set_err(RTG_ERR_INVALID, "camera %d has an empty image", o->camera);
+    std::memset(&C, 0, sizeof(C));
+    auto cp = [](float* d, const rtg_float3& v) { d[0] = v.x; d[1] = v.y; d[2] = v.z; };
+    cp(C.pos, c.position); cp(C.gaze, c.gaze); cp(C.up, c.up); cp(C.right, c.right); cp(C.q, c.q);
+    C.left = c.left; C.right_ext = c.right_ext; C.bottom = c.bottom; C.top = c.top;
+    C.focus_distance = c.focus_distance; C.aperture = c.aperture;
+    C.width = c.width; C.height = c.height; C.spp = c.spp < 1 ? 1 : c.spp;
+    std::memset(&P, 0, sizeof(P));
+    P.row_begin = o->row_begin < 0 ? 0 : o->row_begin;
+    P.row_end = (o->row_end <= 0 || o->row_end > c.height) ? c.height : o->row_end;
+    if (P.row_begin >= P.row_end) return set_err(RTG_ERR_INVALID, "empty row range");
+    P.sample_begin = o->sample_begin < 0 ? 0 : o->sample_begin;
+    P.sample_count = o->sample_count < 0 ? C.spp : o->sample_count;
+    P.accum_only = (o->flags & RTG_RENDER_ACCUM_ONLY) ? 1 : 0;
+    if (!P.accum_only && (P.sample_begin != 0 || P.sample_count != C.spp))
+        return set_err(RTG_ERR_INVALID, "a partial sample range requires RTG_RENDER_ACCUM_ONLY");
+    P.tiles_x = (c.width + 15) / 16;
+    P.tiles_y = (P.row_end - P.row_begin + 15) / 16;
+    P.num_tiles = P.tiles_x * P.tiles_y;
+    P.seed = o->seed;
+    return RTG_OK;
+}
+
+int rtg_render_device(rtg_scene* s, const rtg_render_opts* o, float* d_hdr, uint8_t* d_ldr, float* d_accum,
+                      void* stream) {
+    rtg::DevCamera C;
+    rtg::RenderParams P;
+    int rc = prepare(s, o, C, P);
+    if (rc) return rc;
+    if (P.accum_only && !d_accum) return set_err(RTG_ERR_INVALID, "RTG_RENDER_ACCUM_ONLY needs an accumulation buffer");
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(rtg::launch_render(s->ds, C, P, d_hdr, d_ldr, d_accum, s->counters.p, (o->flags & RTG_RENDER_COUNT_STATS) != 0,
+                               (hipStream_t)stream));
+    return RTG_OK;
+}
+
+int rtg_render(rtg_scene* s, const rtg_render_opts* o, float* hdr_rgb, uint8_t* ldr_rgb) {
+    rtg::DevCamera C;
+    rtg::RenderParams P;
+    int rc = prepare(s, o, C, P);
+    if (rc) return rc;
+    if (P.accum_only) return set_err(RTG_ERR_INVALID, "use rtg_render_device for RTG_RENDER_ACCUM_ONLY");
+    HIP_TRY(hipSetDevice(s->device));
+    const size_t pixels = (size_t)C.width * C.height;
+    if (s->d_pixels < pixels) {
+        if (s->d_hdr) { (void)hipFree(s->d_hdr); s->d_hdr = nullptr; }
+        if (s->d_ldr) { (void)hipFree(s->d_ldr); s->d_ldr = nullptr; }
+        s->d_pixels = 0;
+        HIP_TRY(hipMalloc(&s->d_hdr, pixels * 3 * sizeof(float)));
+        HIP_TRY(hipMalloc(&s->d_ldr, pixels * 3));
+        s->d_pixels = pixels;
+    }
+    HIP_TRY(hipMemset(s->d_hdr, 0, pixels * 3 * sizeof(float)));
+    HIP_TRY(hipMemset(s->d_ldr, 0, pixels * 3));
+    HIP_TRY(rtg::launch_render(s->ds, C, P, s->d_hdr, s->d_ldr, nullptr, s->counters.p,
+                               (o->flags & RTG_RENDER_COUNT_STATS) != 0, nullptr));
+    HIP_TRY(hipDeviceSynchronize());
+    // rows outside [row_begin, row_end) are left untouched in the caller's buffers
+    const size_t off = (size_t)P.row_begin * C.width * 3, n = (size_t)(P.row_end - P.row_begin) * C.width * 3;
+    if (hdr_rgb) HIP_TRY(hipMemcpy(hdr_rgb + off, s->d_hdr + off, n * sizeof(float), hipMemcpyDeviceToHost));
+    if (ldr_rgb) HIP_TRY(hipMemcpy(ldr_rgb + off, s->d_ldr + off, n, hipMemcpyDeviceToHost));
+    return RTG_OK;
+}
+
+int rtg_resolve_accum(const float* accum, int32_t w, int32_t h, float* hdr, uint8_t* ldr) {
+    if (!accum || w <= 0 || h <= 0) return set_err(RTG_ERR_INVALID, "bad accumulation buffer");
+    for (size_t p = 0; p < (size_t)w * h; ++p) {
+        const float* a = accum + 4 * p;
+        for (int k = 0; k < 3; ++k) {
+            float c = a[k] / a[3];
+            if (hdr) hdr[3 * p + k] = c;
+            if (ldr) {
+                int i = (c > -2147483904.0f && c < 2147483648.0f) ? (int)c : (int)0x80000000;
+                ldr[3 * p + k] = (uint8_t)(i < 0 ? 0 : (i > 255 ? 255 : i));
+            }
+        }
+    }
+    return RTG_OK;
+}
+
+int rtg_scene_stats(rtg_scene* s, rtg_stats* out) {
+    if (!s || !out) return set_err(RTG_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(s->device));
+    rtg::DevCounters c;
+    HIP_TRY(hipDeviceSynchronize());
+    HIP_TRY(hipMemcpy(&c, s->counters.p, sizeof(c), hipMemcpyDeviceToHost));
+    out->camera_rays = c.camera_rays;
+    out->secondary_rays = c.secondary_rays;
+    out->shadow_rays = c.shadow_rays;
+    out->node_visits = c.node_visits;
+    out->tri_tests = c.tri_tests;
+    out->sphere_tests = c.sphere_tests;
+    out->object_tests = c.object_tests;
+    out->pad0 = 0;
+    return RTG_OK;
+}
+
+int rtg_scene_reset_stats(rtg_scene* s) {
+    if (!s) return set_err(RTG_ERR_INVALID, "null argument");
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipMemset(s->counters.p, 0, sizeof(rtg::DevCounters)));
+    return RTG_OK;
+}
+
+int rtg_write_png(const char* path, int32_t w, int32_t h, const uint8_t* rgb) {
+    std::string err;
+    if (!path || !rgb || w <= 0 || h <= 0) return set_err(RTG_ERR_INVALID, "bad arguments");
+    if (!rtg::write_png(path, w, h, rgb, err)) return set_err(RTG_ERR_IO, "%s", err.c_str());
+    return RTG_OK;
+}
+
+int rtg_write_hdr(const char* path, int32_t w, int32_t h, const float* rgb) {
+    std::string err;
+    if (!path || !rgb || w <= 0 || h <= 0) return set_err(RTG_ERR_INVALID, "bad arguments");
+    if (!rtg::write_hdr(path, w, h, rgb, err)) return set_err(RTG_ERR_IO, "%s", err.c_str());
+    return RTG_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,120 @@
+// Device-side data layout for the gfx950 render path.
+//
+// HBM layout (one replica per GPU, built by rtg_scene_create):
+//   node_a[i]  float4 {min.x, min.y, min.z, max.x}                      16 B
+//   node_b[i]  float4 {max.y, max.z, skip (int bits), first (int bits)} 16 B
+//   node_cnt[i] int  leaf face count (read only at leaves)               4 B
+//     Nodes are the reference's BVH (mesh.cpp:23-156) re-laid in pre-order
+//     (left subtree before right) with a miss/skip link, so a stackless walk
+//     "hit -> i+1, miss or leaf done -> skip" visits boxes and faces in exactly the
+//     order of BVH::IntersectBVH's recursion (bvh.cpp:5-30).  first < 0 marks
+//     an inner node.
+//   tri_v0[f]  float4 {v0.xyz, 0}                                        16 B
+//   tri_e1[f]  float4 {v0-v1, 0}   (matrixA column 0, mesh.cpp:208-210)  16 B
+//   tri_e2[f]  float4 {v0-v2, 0}   (matrixA column 1)                    16 B
+//   face_n[f]  float4 {n.xyz, 0}   (read once per hit)
+//   face_uv[f] 3 x float2 (meshes with UVs only)
+// Faces are in the BVH-permuted order, so a leaf is a contiguous, coalescable
+// range.  Objects, materials, BRDFs, lights, textures are small tables.
+#pragma once
+
+#include <stdint.h>
+
+namespace rtg {
+
+enum { OBJ_MESH = 0, OBJ_INSTANCE = 1, OBJ_SPHERE = 2 };
+enum { OBJF_SHADOW_SKIP = 1, OBJF_NORMAL_TWICE = 2, OBJF_MOTION_BLUR = 4, OBJF_HAS_UV = 8 };
+
+struct DevObject {
+    int kind, material, flags, pad0;
+    int node_begin, node_end;       // global node range of the (base) mesh's BVH
+    int tex_diffuse, tex_specular, tex_replace_all, pad1;
+    float bmin[4], bmax[4];         // mesh: local bbox, instance: world bbox
+    float mbv[4];                   // motion blur vector
+    float center[4];                // sphere center (xyz) + radius (w)
+    double inv[12];                 // rows 0..2 of inverseTransform
+    double invT[12];                // rows 0..2 of inverseTransposeTransform
+    double baseInvT[12];            // base mesh's inverseTransposeTransform
+};
+
+struct DevMaterial {
+    int type, brdf, pad0, pad1;
+    float ambient[4], diffuse[4], specular[4], mirror[4], absorption[4], radiance[4];
+    float phong_exponent, refractive_index, absorption_index, roughness;
+};
+
+struct DevBrdf {
+    int type, energy_conserving, kd_fresnel, pad0;
+    float exponent, pad1, pad2, pad3;
+};
+
+struct DevTexture {
+    int kind, blend, image, nearest;
+    float noise_scale, bump_factor, normalizer, pad0;
+    int noise_abs, pad1, pad2, pad3;
+};
+
+struct DevImage {
+    int width, height, channels, pad0;
+    long long offset;               // into the texel pool (floats)
+};
+
+struct DevPointLight { float pos[4], intensity[4]; };
+struct DevAreaLight { float pos[4], normal[4], radiance[4], u[4], v[4]; float extent, area, pad0, pad1; };
+struct DevDirLight { float dir[4], radiance[4]; };
+struct DevSpotLight {
+    float pos[4], dir[4], intensity[4];
+    float coverage_deg, falloff_deg, pad0, pad1;
+    double cos_half_coverage, cos_half_falloff;
+};
+
+struct DevScene {
+    const float4* __restrict__ node_a;
+    const float4* __restrict__ node_b;
+    const int* __restrict__ node_cnt;
+    const float4* __restrict__ tri_v0;
+    const float4* __restrict__ tri_e1;
+    const float4* __restrict__ tri_e2;
+    const float4* __restrict__ face_n;
+    const float2* __restrict__ face_uv;
+    const DevObject* __restrict__ objects;
+    const DevMaterial* __restrict__ materials;
+    const DevBrdf* __restrict__ brdfs;
+    const DevTexture* __restrict__ textures;
+    const DevImage* __restrict__ images;
+    const float* __restrict__ texels;
+    const DevPointLight* __restrict__ point_lights;
+    const DevAreaLight* __restrict__ area_lights;
+    const DevDirLight* __restrict__ dir_lights;
+    const DevSpotLight* __restrict__ spot_lights;
+    const int* __restrict__ env_images;
+    int num_objects, num_point, num_area, num_dir, num_spot, num_env;
+    int max_depth, bg_texture;
+    float eps;
+    float ambient[3];
+    int background[3];
+};
+
+struct DevCamera {
+    float pos[3], gaze[3], up[3], right[3], q[3];
+    float left, right_ext, bottom, top;
+    float focus_distance, aperture;
+    int width, height, spp;
+    int path_tracing, next_event;
+};
+
+struct RenderParams {
+    int row_begin, row_end;
+    int sample_begin, sample_count;
+    int accum_only;
+    int tiles_x, tiles_y, num_tiles;
+    unsigned long long seed;
+};
+
+// Per-launch ray/traversal counters (RTG_RENDER_COUNT_STATS).
+struct DevCounters {
+    unsigned long long camera_rays, secondary_rays, shadow_rays, node_visits, tri_tests, sphere_tests,
+        object_tests, pad0;
+};
+
+}  // namespace rtg

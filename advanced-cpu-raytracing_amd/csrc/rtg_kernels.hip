@@ -1,0 +1,1025 @@
+// gfx950 render path: camera rays, threaded BVH traversal, Cramer's-rule triangle
+// and analytic sphere tests, Whitted shading with the five BRDFs, shadow rays, and
+// mirror / dielectric / conductor secondaries.
+//
+// Numerics: this file is compiled with -ffp-contract=off and IEEE div/sqrt, and every
+// expression keeps the reference's association and float/double choices, so the
+// only differences from the CPU path are the last-ulp results of transcendental
+// library calls (powf, acosf, expf, atan2f, double pow/cos).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "rtg_device.hpp"
+#include "rtg_kernels.hpp"
+
+namespace rtg {
+
+#define DEV __device__ __forceinline__
+
+// ---------------------------------------------------------------------------
+// helperMath.cpp
+// ---------------------------------------------------------------------------
+struct f3 { float x, y, z; };
+DEV f3 mk(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
+DEV f3 ld3(const float* p) { return mk(p[0], p[1], p[2]); }
+DEV f3 add(f3 a, f3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
+DEV f3 sub(f3 a, f3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
+DEV f3 mulv(f3 a, f3 b) { return mk(a.x * b.x, a.y * b.y, a.z * b.z); }
+DEV f3 muls(f3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
+DEV f3 divs(f3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
+DEV f3 neg(f3 a) { return mk(a.x * -1.0f, a.y * -1.0f, a.z * -1.0f); }
+DEV float dot(f3 a, f3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+DEV f3 cross(f3 a, f3 b) { return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+DEV float len(f3 a) { return sqrtf((a.x * a.x) + (a.y * a.y) + (a.z * a.z)); }
+DEV f3 makeUnit(f3 a) { float l = len(a); return mk(a.x / l, a.y / l, a.z / l); }
+DEV float fmax0(float v) { return (0.0f < v) ? v : 0.0f; }          // std::max(0.0f, v)
+
+DEV void onb(f3 r, f3& u, f3& v) {                                     // helperMath.cpp:59-85
+    float ax = fabsf(r.x), ay = fabsf(r.y), az = fabsf(r.z);
+    f3 rp = r;
+    if (ax < ay) { if (ax < az) rp.x = 1.0f; else rp.z = 1.0f; }
+    else { if (ay < az) rp.y = 1.0f; else rp.z = 1.0f; }
+    u = makeUnit(cross(rp, r));
+    v = makeUnit(cross(r, u));
+}
+
+#define RT_PI 3.14159265358979323846
+DEV double angleBetween(f3 a, f3 b) {                                  // helperMath.cpp:154-157
+    float d = dot(a, b);
+    float c = (-1.0f < d) ? d : -1.0f;      // std::max(-1.0f, d)
+    c = (c < 1.0f) ? c : 1.0f;              // std::min(1.0f, c)
+    return (double)acosf(c) * (double)(180.0f / RT_PI);
+}
+DEV double cosDeg(double a) { return cos(a * (RT_PI / 180.0f)); }      // helperMath.cpp:158-161
+
+// matrix.hpp:56-81 (double accumulation, w column included)
+DEV f3 xform(const double* m, f3 v, float w) {
+    return mk((float)(m[0] * v.x + m[1] * v.y + m[2] * v.z + m[3] * w),
+              (float)(m[4] * v.x + m[5] * v.y + m[6] * v.z + m[7] * w),
+              (float)(m[8] * v.x + m[9] * v.y + m[10] * v.z + m[11] * w));
+}
+
+// counter-based RNG (replaces the shared mt19937 streams; keyed by pixel, sample and
+// ray-tree node so results do not depend on thread / GPU count)
+DEV uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+DEV float rnd(uint64_t key, uint32_t purpose, uint32_t idx) {
+    uint64_t h = mix64(key ^ mix64(((uint64_t)purpose << 32) | idx));
+    return (float)(h >> 40) * (1.0f / 16777216.0f);
+}
+DEV uint64_t child_key(uint64_t key, int slot) { return mix64(key + 0x632BE59BD9B4E019ULL * (uint64_t)(slot + 1)); }
+DEV uint64_t root_key(uint64_t seed, int pixel, int sample) {
+    return mix64(mix64(seed ^ 0xD1B54A32D192ED03ULL) ^ ((uint64_t)(uint32_t)pixel * 0x9E3779B97F4A7C15ULL) ^
+                 ((uint64_t)(uint32_t)sample << 1));
+}
+enum { RP_MOTION = 1, RP_DOF = 2, RP_JITTER = 3, RP_AREA = 4, RP_ENV = 5, RP_ROUGH_REFL = 6, RP_ROUGH_REFR = 7 };
+
+// ---------------------------------------------------------------------------
+// Counters
+// ---------------------------------------------------------------------------
+template <bool STATS> struct Cnt {
+    DEV void node() {} DEV void tri() {} DEV void sph() {} DEV void obj() {}
+    DEV void cam() {} DEV void sec() {} DEV void shd() {}
+};
+template <> struct Cnt<true> {
+    uint32_t nodes = 0, tris = 0, sphs = 0, objs = 0, cams = 0, secs = 0, shds = 0;
+    DEV void node() { ++nodes; } DEV void tri() { ++tris; } DEV void sph() { ++sphs; } DEV void obj() { ++objs; }
+    DEV void cam() { ++cams; } DEV void sec() { ++secs; } DEV void shd() { ++shds; }
+};
+
+// ---------------------------------------------------------------------------
+// Geometry
+// ---------------------------------------------------------------------------
+struct Ray {
+    f3 o, d;
+};
+
+// BoundingBox::doesIntersectWith (shape.hpp:78-100): true divisions, x-slab by
+// comparison, y/z by fmin/fmax (NaN-ignoring), accept iff tmax>0 && tmax>=tmin && tmin<minT.
+DEV bool box_hit(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, const Ray& r, float minT) {
+    float tx1 = (mnx - r.o.x) / r.d.x;
+    float tx2 = (mxx - r.o.x) / r.d.x;
+    float tmin = tx1, tmax = tx2;
+    if (tx1 > tx2) { tmin = tx2; tmax = tx1; }
+    float ty1 = (mny - r.o.y) / r.d.y;
+    float ty2 = (mxy - r.o.y) / r.d.y;
+    tmin = fmaxf(tmin, fminf(ty1, ty2));
+    tmax = fminf(tmax, fmaxf(ty1, ty2));
+    float tz1 = (mnz - r.o.z) / r.d.z;
+    float tz2 = (mxz - r.o.z) / r.d.z;
+    tmin = fmaxf(tmin, fminf(tz1, tz2));
+    tmax = fminf(tmax, fmaxf(tz1, tz2));
+    return tmax > 0 && tmax >= tmin && tmin < minT;
+}
+
+// determinant (helperMath.cpp:132-138)
+DEV float det3(float m00, float m01, float m02, float m10, float m11, float m12, float m20, float m21, float m22) {
+    float first = m00 * (m11 * m22 - m12 * m21);
+    float second = m10 * (m02 * m21 - m01 * m22);
+    float third = m20 * (m01 * m12 - m11 * m02);
+    return first + second + third;
+}
+
+// Mesh::IntersectFace (mesh.cpp:201-240): Cramer's rule, early outs in the same order.
+// Returns t (or a value failing 0<t<minT) and beta/gamma.
+DEV bool tri_test(const DevScene& S, int f, const Ray& r, float minT, float& tout, float* bg = nullptr) {
+    const float4 A = S.tri_v0[f], E1 = S.tri_e1[f], E2 = S.tri_e2[f];
+    const float dx = r.d.x, dy = r.d.y, dz = r.d.z;
+    float detA = det3(E1.x, E2.x, dx, E1.y, E2.y, dy, E1.z, E2.z, dz);
+    if (detA == 0) return false;
+    const float sx = A.x - r.o.x, sy = A.y - r.o.y, sz = A.z - r.o.z;
+    float beta = det3(sx, E2.x, dx, sy, E2.y, dy, sz, E2.z, dz) / detA;
+    if (beta < 0) return false;
+    float gama = det3(E1.x, sx, dx, E1.y, sy, dy, E1.z, sz, dz) / detA;
+    if (gama < 0 || gama + beta > 1) return false;
+    float t = det3(E1.x, E2.x, sx, E1.y, E2.y, sy, E1.z, E2.z, sz) / detA;
+    if (bg) { bg[0] = beta; bg[1] = gama; }
+    tout = t;
+    return t > 0.0f && t < minT;
+}
+
+// BVH::IntersectBVH (bvh.cpp:5-30) as a stackless pre-order walk (rtg_device.hpp).
+// ANY: stop at the first accepted face with t < limit (CastShadowRay semantics).
+template <bool ANY, bool STATS>
+DEV bool walk_bvh(const DevScene& S, int i, const int end, const Ray& r, float& minT, int& hitFace, float limit,
+                  Cnt<STATS>& c) {
+    bool hit = false;
+    while (i < end) {
+        const float4 a = S.node_a[i];
+        const float4 b = S.node_b[i];
+        c.node();
+        const int skip = __float_as_int(b.z);
+        if (box_hit(a.x, a.y, a.z, a.w, b.x, b.y, r, minT)) {
+            const int first = __float_as_int(b.w);
+            if (first >= 0) {
+                const int cnt = S.node_cnt[i];
+                for (int f = first; f < first + cnt; ++f) {
+                    c.tri();
+                    float t;
+                    if (tri_test(S, f, r, minT, t)) {
+                        minT = t;
+                        hitFace = f;
+                        hit = true;
+                        if (ANY && t < limit) return true;
+                    }
+                }
+                i = skip;
+            } else {
+                i = i + 1;
+            }
+        } else {
+            i = skip;
+        }
+    }
+    return hit;
+}
+
+// Sphere::Intersect (sphere.cpp:13-78): root selection and acceptance; lo/ld local ray.
+DEV bool sphere_t(const DevObject& ob, const Ray& lr, float minT, float& tout) {
+    const f3 center = mk(ob.center[0], ob.center[1], ob.center[2]);
+    const float radius = ob.center[3];
+    f3 oc = sub(lr.o, center);
+    float c = dot(oc, oc) - (radius * radius);
+    float b = 2 * dot(lr.d, oc);
+    float a = dot(lr.d, lr.d);
+    float delta = b * b - (4 * a * c);
+    if (delta < 0.0f) return false;
+    delta = sqrtf(delta);
+    a = (float)(2.0 * a);
+    float t1 = (-b + delta) / a;
+    float t2 = (-b - delta) / a;
+    float t = t1 < t2 ? t1 : t2;
+    if (t1 < t2) { t = (t1 > 0.0f) ? t1 : t2; }
+    else if (t2 < t1) { t = (t2 > 0.0f) ? t2 : t1; }
+    tout = t;
+    return t < minT && t > 0.0f;
+}
+
+DEV Ray local_ray(const DevObject& ob, const Ray& r, float mbTime) {
+    Ray lr;
+    lr.o = xform(ob.inv, r.o, 1.0f);
+    lr.d = xform(ob.inv, r.d, 0.0f);
+    if (ob.flags & OBJF_MOTION_BLUR) lr.o = add(lr.o, muls(ld3(ob.mbv), mbTime));
+    return lr;
+}
+
+struct Hit {
+    float t;
+    int obj, face;     // face < 0: sphere
+    f3 o;              // world ray origin when the hit was accepted (normal/uv are computed then)
+};
+
+// IntersectObjects (raytracer.cpp:625-643) / CastShadowRay (raytracer.cpp:585-623).
+// Closest hit: shared minT across objects, earlier object wins ties (strict <).
+// Any hit (ANY): skip emissive meshes, true as soon as a hit with t < limit exists.
+// The ray is updated in place like the reference's: an instance with motion blur whose
+// bbox test fails leaves its offset on the ray origin (instancedMesh.cpp:18-60).
+template <bool ANY, bool STATS>
+DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit, Hit& h, Cnt<STATS>& c) {
+    h.t = minT;
+    h.obj = -1;
+    h.face = -1;
+    for (int k = 0; k < S.num_objects; ++k) {
+        const DevObject& ob = S.objects[k];
+        c.obj();
+        if (ob.kind == OBJ_SPHERE) {
+            c.sph();
+            Ray lr = local_ray(ob, r, mbTime);
+            float t;
+            if (sphere_t(ob, lr, h.t, t)) {
+                h.t = t; h.obj = k; h.face = -1; h.o = r.o;
+                if (ANY && t < limit) return true;
+            }
+            continue;
+        }
+        if (ANY && (ob.flags & OBJF_SHADOW_SKIP)) continue;
+        if (ob.kind == OBJ_INSTANCE) {
+            // InstancedMesh::Intersect (instancedMesh.cpp:16-66): world bbox first
+            Ray wr = r;
+            if (ob.flags & OBJF_MOTION_BLUR) wr.o = add(wr.o, muls(ld3(ob.mbv), mbTime));
+            if (!box_hit(ob.bmin[0], ob.bmin[1], ob.bmin[2], ob.bmax[0], ob.bmax[1], ob.bmax[2], wr, h.t)) {
+                r.o = wr.o;
+                continue;
+            }
+        }
+        // Mesh::Intersect (mesh.cpp:158-188); the mesh bbox test equals the root-node test
+        Ray lr = local_ray(ob, r, mbTime);
+        int face = -1;
+        float t = h.t;
+        if (walk_bvh<ANY, STATS>(S, ob.node_begin, ob.node_end, lr, t, face, limit, c)) {
+            h.t = t; h.obj = k; h.face = face; h.o = r.o;
+            if (ANY && t < limit) return true;
+        }
+    }
+    return !ANY && h.obj >= 0;
+}
+
+// ---------------------------------------------------------------------------
+// Hit reconstruction: normal / uv of the winning primitive
+// ---------------------------------------------------------------------------
+DEV float tiledUV(float x) {                                           // mesh.cpp:382-389
+    if (x > 1.0001f) {
+        x = x - floorf(x);
+        if (x < 0.0001) x = 1.0f;
+    }
+    return x;
+}
+
+struct Surf {
+    f3 p, n;
+    float u, v;
+};
+
+template <bool STATS>
+DEV Surf surface(const DevScene& S, const Ray& r, float mbTime, const Hit& h, Cnt<STATS>& c) {
+    const DevObject& ob = S.objects[h.obj];
+    Surf s;
+    s.p = add(r.o, muls(r.d, h.t));                                    // raytracer.cpp:69
+    s.u = s.v = 0.f;
+    Ray hr;
+    hr.o = h.o;
+    hr.d = r.d;
+    Ray lr = local_ray(ob, hr, mbTime);
+    if (h.face < 0) {                                                  // sphere.cpp:71-175
+        const f3 center = mk(ob.center[0], ob.center[1], ob.center[2]);
+        f3 lp = add(lr.o, muls(lr.d, h.t));
+        f3 p = sub(lp, center);
+        float phi = atan2f(p.z, p.x);
+        float theta = acosf(p.y / ob.center[3]);
+        s.u = (float)((-phi + RT_PI) / (2.0f * RT_PI));
+        s.v = (float)(theta / RT_PI);
+        f3 n = makeUnit(sub(lp, center));
+        s.n = makeUnit(xform(ob.invT, n, 0.0f));
+        return s;
+    }
+    f3 n = ld3(&S.face_n[h.face].x);
+    if (ob.flags & OBJF_NORMAL_TWICE) n = makeUnit(xform(ob.baseInvT, n, 0.0f));   // mesh.cpp:363
+    s.n = makeUnit(xform(ob.invT, n, 0.0f));                                          // mesh.cpp:179 / instancedMesh.cpp:57
+    if (ob.flags & OBJF_HAS_UV) {                                                     // mesh.cpp:245-262
+        float bg[2], t;
+        tri_test(S, h.face, lr, INFINITY, t, bg);
+        const float2 a = S.face_uv[3 * h.face], b = S.face_uv[3 * h.face + 1], cc = S.face_uv[3 * h.face + 2];
+        float u = a.x + bg[0] * (b.x - a.x) + bg[1] * (cc.x - a.x);
+        float v = a.y + bg[0] * (b.y - a.y) + bg[1] * (cc.y - a.y);
+        s.u = tiledUV(u);
+        s.v = tiledUV(v);
+    }
+    return s;
+}
+
+// ---------------------------------------------------------------------------
+// Textures (imageTexture.h, perlinTexture.h) and environment light
+// ---------------------------------------------------------------------------
+DEV f3 texel(const DevScene& S, const DevImage& im, int i, int j) {     // LDRImage.h:16-26
+    const long long idx = (long long)im.channels * ((long long)i + (long long)j * im.width);
+    const long long n = (long long)im.width * im.height * im.channels;
+    const float* t = S.texels + im.offset;
+    // linear indexing as in the reference (an x+1 read at the last column takes the next
+    // row's first texel); reads outside the image, undefined in the reference, give 0
+    return mk((idx >= 0 && idx < n) ? t[idx] : 0.f, (idx + 1 >= 0 && idx + 1 < n) ? t[idx + 1] : 0.f,
+              (idx + 2 >= 0 && idx + 2 < n) ? t[idx + 2] : 0.f);
+}
+
+DEV f3 image_rgb(const DevScene& S, const DevTexture& tx, float u, float v) {   // imageTexture.h:60-73,111-133
+    const DevImage im = S.images[tx.image];
+    if (tx.nearest) {
+        int i = (int)(u * im.width);
+        int j = (int)(v * im.height);
+        i = (im.width - 1 < i) ? im.width - 1 : i;
+        j = (im.height - 1 < j) ? im.height - 1 : j;
+        return texel(S, im, i, j);
+    }
+    float fi = u * im.width, fj = v * im.height;
+    float hiw = (float)(im.width - 1), hih = (float)(im.height - 1);
+    fi = (hiw < fi) ? hiw : fi; fi = (fi < 0.0f) ? 0.0f : fi;          // std::max(lower, std::min(n, upper))
+    fj = (hih < fj) ? hih : fj; fj = (fj < 0.0f) ? 0.0f : fj;
+    float p = floorf(fi), q = floorf(fj);
+    float dx = fi - p, dy = fj - q;
+    float w1 = (1 - dx) * (1 - dy), w2 = dx * (1 - dy), w3 = (1 - dx) * dy, w4 = dx * dy;
+    int ip = (int)p, iq = (int)q;
+    return add(add(add(muls(texel(S, im, ip, iq), w1), muls(texel(S, im, ip + 1, iq), w2)),
+                   muls(texel(S, im, ip, iq + 1), w3)), muls(texel(S, im, ip + 1, iq + 1), w4));
+}
+
+__constant__ int c_perm[512];
+__constant__ float c_grad[36];
+
+DEV double perlin_f(float x) {                                          // perlinTexture.h:153-160
+    x = fabsf(x);
+    if (x > 1) return 0;
+    float xSqr = x * x;
+    float xCube = xSqr * x;
+    return (-6 * xCube * xSqr) + 15 * xCube * x - 10 * xCube + 1;
+}
+DEV float gdot(int g, float x, float y, float z) {
+    return c_grad[3 * g] * x + c_grad[3 * g + 1] * y + c_grad[3 * g + 2] * z;
+}
+DEV float perlin(const DevTexture& tx, float x, float y, float z) {     // perlinTexture.h:57-123
+    x *= tx.noise_scale; y *= tx.noise_scale; z *= tx.noise_scale;
+    int X = (int)floorf(x), Y = (int)floorf(y), Z = (int)floorf(z);
+    float dx = x - X, dy = y - Y, dz = z - Z;
+    X = X & 255; Y = Y & 255; Z = Z & 255;
+    const int* p = c_perm;
+    int ind0 = p[X + p[Y + p[Z]]] % 12;
+    int ind1 = p[X + p[Y + p[Z + 1]]] % 12;
+    int ind2 = p[X + p[Y + 1 + p[Z]]] % 12;
+    int ind3 = p[X + p[Y + 1 + p[Z + 1]]] % 12;
+    int ind4 = p[X + 1 + p[Y + p[Z]]] % 12;
+    int ind5 = p[X + 1 + p[Y + p[Z + 1]]] % 12;
+    int ind6 = p[X + 1 + p[Y + 1 + p[Z]]] % 12;
+    int ind7 = p[X + 1 + p[Y + 1 + p[Z + 1]]] % 12;
+    double c0 = gdot(ind0, dx, dy, dz), c1 = gdot(ind4, dx - 1, dy, dz), c2 = gdot(ind2, dx, dy - 1, dz),
+           c3 = gdot(ind6, dx - 1, dy - 1, dz), c4 = gdot(ind1, dx, dy, dz - 1), c5 = gdot(ind5, dx - 1, dy, dz - 1),
+           c6 = gdot(ind3, dx, dy - 1, dz - 1), c7 = gdot(ind7, dx - 1, dy - 1, dz - 1);
+    double fdx = perlin_f(dx), fdy = perlin_f(dy), fdz = perlin_f(dz);
+    double fdx1 = perlin_f(dx - 1), fdy1 = perlin_f(dy - 1), fdz1 = perlin_f(dz - 1);
+    double w0 = fdx * fdy * fdz, w1 = fdx1 * fdy * fdz, w2 = fdx * fdy1 * fdz, w3 = fdx1 * fdy1 * fdz;
+    double w4 = fdx * fdy * fdz1, w5 = fdx1 * fdy * fdz1, w6 = fdx * fdy1 * fdz1, w7 = fdx1 * fdy1 * fdz1;
+    double total = w0 * c0 + w1 * c1 + w2 * c2 + w3 * c3 + w4 * c4 + w5 * c5 + w6 * c6 + w7 * c7;
+    if (!tx.noise_abs) return (float)((total + 1) / 2.0f);
+    return (float)fabs(total);
+}
+
+DEV f3 tex_rgb(const DevScene& S, const DevTexture& tx, float u, float v) {
+    if (tx.kind == 1) return mk(180.f, 30.f, 180.f);                    // PerlinTexture::GetRGBSample
+    return image_rgb(S, tx, u, v);
+}
+
+// SphericalEnvironmentLight::GetSample (sphericalEnvironmentLight.h:22-34)
+DEV f3 env_sample(const DevScene& S, int e, f3 dir) {
+    const DevImage im = S.images[S.env_images[e]];
+    float u = (float)((1 + (atan2f(dir.x, -dir.z) / RT_PI)) / 2.0f);
+    float v = (float)(acosf(dir.y) / RT_PI);
+    int i = (int)(im.width * u);
+    int j = (int)(im.height * v);
+    return muls(muls(texel(S, im, i, j), (float)2), (float)RT_PI);
+}
+
+// GetDirection (sphericalEnvironmentLight.h:36-61): rejection sampling, returns the
+// un-normalised candidate.  The reference spins forever on a NaN normal; bounded here.
+DEV f3 env_direction(f3 surfaceNormal, uint64_t key, int e) {
+    f3 n = makeUnit(surfaceNormal);
+    f3 cand = mk(0, 0, 0);
+    for (uint32_t k = 0; k < 4096; ++k) {
+        uint32_t base = (uint32_t)e * 16384u + 3u * k;
+        cand.x = 2.0f * rnd(key, RP_ENV, base) - 1.0f;
+        cand.y = 2.0f * rnd(key, RP_ENV, base + 1) - 1.0f;
+        cand.z = 2.0f * rnd(key, RP_ENV, base + 2) - 1.0f;
+        float length = len(cand);
+        if (length <= 1.0f && dot(n, cand) > 0.0f) break;
+    }
+    return cand;
+}
+
+// ---------------------------------------------------------------------------
+// BRDFs (brdf*.cpp) and Shade (raytracer.cpp:192-206, 478-554)
+// ---------------------------------------------------------------------------
+DEV f3 brdf_apply(const DevBrdf& B, float refrIdx, f3 kd, f3 ks, f3 w_i, f3 w_o, f3 normal) {
+    const float th = (float)angleBetween(w_i, normal);
+    const double ex = (double)B.exponent;
+    switch (B.type) {
+        case 0: {                                                       // brdfPhong.cpp:11-20
+            if (th >= 90.0f || th < 0) return mk(0, 0, 0);
+            f3 r = makeUnit(sub(muls(muls(normal, 2.0f), dot(normal, w_i)), w_i));
+            double angleR = angleBetween(r, w_o);
+            return add(kd, muls(ks, (float)(pow(cosDeg(angleR), ex) / cosDeg(th))));
+        }
+        case 1: {                                                       // brdfBlinnPhong.cpp:11-20
+            if (th >= 90.0f) return mk(0, 0, 0);
+            f3 half = divs(add(w_i, w_o), len(add(w_i, w_o)));
+            double a = angleBetween(half, normal);
+            return add(kd, muls(ks, (float)(pow(cosDeg(a), ex) / cosDeg(th))));
+        }
+        case 2: {                                                       // brdfModifiedPhong.cpp:14-33
+            if (th >= 90.0f || th < 0) return mk(0, 0, 0);
+            f3 r = makeUnit(sub(muls(muls(normal, 2.0f), dot(normal, w_i)), w_i));
+            double angleR = angleBetween(r, w_o);
+            if (B.energy_conserving) {
+                f3 kdTerm = muls(kd, (float)(1.0f / RT_PI));
+                double ksCons = (B.exponent + 2) / (2 * RT_PI);
+                double cosTerm = pow(cosDeg(angleR), ex);
+                return add(kdTerm, muls(ks, (float)(ksCons * cosTerm)));
+            }
+            return add(kd, muls(ks, (float)pow(cosDeg(angleR), ex)));
+        }
+        case 3: {                                                       // brdfModifiedBlinnPhong.cpp:11-29
+            if (th >= 90.0f) return mk(0, 0, 0);
+            f3 half = divs(add(w_i, w_o), len(add(w_i, w_o)));
+            double a = angleBetween(half, normal);
+            if (B.energy_conserving) {
+                f3 kdTerm = muls(kd, (float)(1.0f / RT_PI));
+                double ksCons = (B.exponent + 8) / (8 * RT_PI);
+                double cosTerm = pow(cosDeg(a), ex);
+                return add(kdTerm, muls(ks, (float)(ksCons * cosTerm)));
+            }
+            return add(kd, muls(ks, (float)pow(cosDeg(a), ex)));
+        }
+        default: {                                                      // brdfTorranceSparrow.cpp:15-59
+            if (th >= 90.0f) return mk(0, 0, 0);
+            f3 half = divs(add(w_i, w_o), len(add(w_i, w_o)));
+            double cosAlpha = dot(half, normal);
+            double d = (ex + 2) * pow(cosAlpha, ex) / (2 * RT_PI);
+            double cosbeta = dot(half, w_o), n = refrIdx;
+            double r0 = pow(n - 1, 2.0) / pow(n + 1, 2.0);
+            double f = r0 + (1.0 - r0) * pow((1.0 - cosbeta), 5.0);
+            double ndoth = dot(normal, half), ndotwo = dot(normal, w_o), ndotwi = dot(normal, w_i), wodoth = dot(w_o, half);
+            double ga = 2.0f * ndoth * ndotwo / wodoth, gb = 2.0 * ndoth * ndotwi / wodoth;
+            double gm = (gb < ga) ? gb : ga;
+            double g = (gm < 1.0) ? gm : 1.0;
+            double kdCoeff = (1.0f / RT_PI);
+            if (B.kd_fresnel) kdCoeff *= (1 - f);
+            f3 kdTerm = muls(kd, (float)kdCoeff);
+            double costheta = dot(normal, w_i), cosphi = dot(normal, w_o);
+            f3 ksTerm = muls(ks, (float)((d * f * g) / (4 * costheta * cosphi)));
+            return add(kdTerm, ksTerm);
+        }
+    }
+}
+
+struct ShadeCtx {
+    const DevObject* ob;
+    const DevMaterial* mat;
+    Surf s;
+};
+
+DEV f3 kd_coeff(const DevScene& S, const ShadeCtx& c) {                // raytracer.cpp:478-508
+    f3 refl = ld3(c.mat->diffuse);
+    if (c.ob->tex_diffuse >= 0) {
+        const DevTexture tx = S.textures[c.ob->tex_diffuse];
+        f3 t;
+        if (tx.kind == 1) { float p = perlin(tx, c.s.p.x, c.s.p.y, c.s.p.z); t = mk(p, p, p); }
+        else t = divs(image_rgb(S, tx, c.s.u, c.s.v), 255.0f);
+        refl = tx.blend ? divs(add(t, ld3(c.mat->diffuse)), 2.0f) : t;
+    }
+    return refl;
+}
+DEV f3 ks_coeff(const DevScene& S, const ShadeCtx& c) {                // raytracer.cpp:509-539 (reads diffuseTex)
+    f3 refl = ld3(c.mat->specular);
+    if (c.ob->tex_specular >= 0 && c.ob->tex_diffuse >= 0) {
+        const DevTexture tx = S.textures[c.ob->tex_diffuse];
+        f3 t;
+        if (tx.kind == 1) { float p = perlin(tx, c.s.p.x, c.s.p.y, c.s.p.z); t = mk(p, p, p); }
+        else t = divs(image_rgb(S, tx, c.s.u, c.s.v), 255.0f);
+        refl = tx.blend ? divs(add(t, ld3(c.mat->diffuse)), 2.0f) : t;
+    }
+    return refl;
+}
+
+DEV f3 shade(const DevScene& S, const ShadeCtx& c, f3 w_i, f3 w_o, f3 Li) {
+    if (c.mat->brdf >= 0) {
+        float costheta_i = fmax0(dot(w_i, c.s.n));
+        f3 kd = kd_coeff(S, c), ks = ks_coeff(S, c);
+        f3 res = brdf_apply(S.brdfs[c.mat->brdf], c.mat->refractive_index, kd, ks, w_i, w_o, c.s.n);
+        return muls(mulv(res, Li), costheta_i);
+    }
+    f3 kd = kd_coeff(S, c);                                             // GetDiffuse
+    float costheta = fmax0(dot(w_i, c.s.n));
+    f3 diff = muls(mulv(kd, Li), costheta);
+    f3 ks = ks_coeff(S, c);                                             // GetSpecular
+    f3 half = divs(add(w_i, w_o), len(add(w_i, w_o)));
+    float cosAlpha = fmax0(dot(c.s.n, half));
+    f3 spec = muls(mulv(ks, Li), powf(cosAlpha, c.mat->phong_exponent));
+    return add(diff, spec);
+}
+
+// IsInShadow (raytracer.cpp:567-584); IsInShadowDirectional (:555-566)
+template <bool STATS>
+DEV bool in_shadow(const DevScene& S, f3 p, f3 n, f3 lightPos, float mbTime, Cnt<STATS>& c) {
+    f3 dir = sub(lightPos, p);
+    float lightT = len(dir);
+    Ray sr;
+    sr.d = divs(dir, lightT);
+    sr.o = add(p, muls(n, S.eps));
+    Hit h;
+    c.shd();
+    return trace<true, STATS>(S, sr, mbTime, lightT + 0.01f, lightT, h, c);
+}
+template <bool STATS>
+DEV bool in_shadow_dir(const DevScene& S, f3 p, f3 n, f3 lightDir, float mbTime, Cnt<STATS>& c) {
+    Ray sr;
+    sr.d = neg(lightDir);
+    sr.o = add(p, muls(n, S.eps));
+    Hit h;
+    c.shd();
+    return trace<true, STATS>(S, sr, mbTime, INFINITY, INFINITY, h, c);
+}
+
+// SampleDirectLighting (raytracer.cpp:701-805): type order point, area, env, dir, spot
+template <bool STATS>
+DEV f3 direct(const DevScene& S, const ShadeCtx& c, f3 w_o, float mbTime, uint64_t key, Cnt<STATS>& cn) {
+    f3 color = mk(0, 0, 0);
+    const f3 p = c.s.p, n = c.s.n;
+    for (int i = 0; i < S.num_point; ++i) {
+        const f3 lp = ld3(S.point_lights[i].pos);
+        if (in_shadow<STATS>(S, p, n, lp, mbTime, cn)) continue;
+        f3 w_i = makeUnit(sub(lp, p));
+        float dist = len(sub(lp, p));
+        f3 E = divs(ld3(S.point_lights[i].intensity), dist * dist);
+        color = add(color, shade(S, c, w_i, w_o, E));
+    }
+    for (int i = 0; i < S.num_area; ++i) {
+        const DevAreaLight& L = S.area_lights[i];
+        float offU = rnd(key, RP_AREA, 2 * i) - 0.5f;                     // areaLight.h:34-41
+        float offV = rnd(key, RP_AREA, 2 * i + 1) - 0.5f;
+        f3 sp = add(add(ld3(L.pos), muls(ld3(L.u), L.extent * offU)), muls(ld3(L.v), L.extent * offV));
+        if (in_shadow<STATS>(S, p, n, sp, mbTime, cn)) continue;
+        f3 w_i = sub(sp, p);
+        float dist = len(w_i);
+        float dSqr = dist * dist;
+        w_i = divs(w_i, dist);
+        float lc = dot(ld3(L.normal), neg(w_i));
+        if (lc < 0) lc = dot(ld3(L.normal), w_i);
+        f3 E = muls(ld3(L.radiance), L.area * lc / dSqr);
+        color = add(color, shade(S, c, w_i, w_o, E));
+    }
+    for (int i = 0; i < S.num_env; ++i) {
+        f3 sd = env_direction(n, key, i);
+        f3 E = env_sample(S, i, sd);
+        color = add(color, shade(S, c, n, w_o, E));
+    }
+    for (int i = 0; i < S.num_dir; ++i) {
+        const f3 ldir = ld3(S.dir_lights[i].dir);
+        if (in_shadow_dir<STATS>(S, p, n, ldir, mbTime, cn)) continue;
+        color = add(color, shade(S, c, neg(ldir), w_o, ld3(S.dir_lights[i].radiance)));
+    }
+    for (int i = 0; i < S.num_spot; ++i) {
+        const DevSpotLight& L = S.spot_lights[i];
+        const f3 lp = ld3(L.pos);
+        if (in_shadow<STATS>(S, p, n, lp, mbTime, cn)) continue;
+        f3 w_i = makeUnit(sub(lp, p));
+        // SpotLight::GetIrradiance (spotLight.h:33-57)
+        float distToPoint = len(sub(p, lp));
+        f3 toPoint = divs(sub(p, lp), distToPoint);
+        double alpha = angleBetween(ld3(L.dir), toPoint);
+        f3 E;
+        if (alpha <= 0 || alpha > (L.coverage_deg / 2.0f)) {
+            E = mk(0, 0, 0);
+        } else {
+            float distSqr = distToPoint * distToPoint;
+            E = divs(ld3(L.intensity), distSqr);
+            if (alpha > (L.falloff_deg / 2.0f)) {
+                double cosAlpha = cos(alpha * (RT_PI / 180.0f));
+                double s = pow((cosAlpha - L.cos_half_coverage) / (L.cos_half_falloff - L.cos_half_coverage), (double)4.0f);
+                E = muls(E, (float)s);
+            }
+        }
+        color = add(color, shade(S, c, w_i, w_o, E));
+    }
+    return color;
+}
+
+// Raytracer::Reflect (raytracer.cpp:424-440)
+DEV f3 reflect(f3 normal, f3 w_o, float roughness, uint64_t key, uint32_t purpose) {
+    f3 r = makeUnit(sub(muls(muls(normal, 2.0f), dot(normal, w_o)), w_o));
+    if (roughness > 0.001) {
+        f3 u, v;
+        onb(r, u, v);
+        float psi1 = rnd(key, purpose, 0) - 0.5f;
+        float psi2 = rnd(key, purpose, 1) - 0.5f;
+        return makeUnit(add(r, muls(add(muls(u, psi1), muls(v, psi2)), roughness)));
+    }
+    return r;
+}
+
+DEV f3 beer(float x, const float* c, f3 L0) {                          // raytracer.cpp:416-423
+    return mk(L0.x * expf(-c[0] * x), L0.y * expf(-c[1] * x), L0.z * expf(-c[2] * x));
+}
+
+// ---------------------------------------------------------------------------
+// Ray tree: PerformShading (raytracer.cpp:65-134) with the recursion of
+// ComputeMirrorReflection / ...Dielectric... / ...Conductor... unrolled onto an
+// explicit per-thread stack.  Children are evaluated depth-first in the
+// reference's order and combined with the reference's expressions, so the
+// summation association is identical.
+// ---------------------------------------------------------------------------
+enum { FK_MIRROR = 0, FK_CONDUCTOR = 1, FK_TIR = 2, FK_DIEL = 3 };
+
+struct Frame {
+    f3 color;          // GI + ambient + direct of this node
+    f3 coef;           // mirror reflectance
+    f3 refl;           // dielectric: finished reflected term
+    f3 reflDir;        // dielectric: reflected direction (env lookups)
+    f3 rOrigin, rDir;  // dielectric: refracted ray (unnormalised dir)
+    int kind, stage;
+    float ratio, rT;   // conductor ratio / dielectric rReflect, rRefract
+    float rMedium, roughness;
+    float selfT, selfMedium;
+    int matIdx, depth;
+    uint64_t key;
+};
+
+struct Node {          // a ray that hit something, about to be shaded
+    Ray r;
+    Hit h;
+    f3 eye;
+    float medium, mbTime;
+    int depth;
+    uint64_t key;
+};
+
+struct Child {
+    Ray r;
+    float medium;
+};
+
+// Shades `cur`.  Returns true and fills `f`/`ch` if the node spawns a child ray;
+// otherwise `out` is the node's final colour.
+template <bool STATS>
+DEV bool shade_node(const DevScene& S, const Node& cur, f3& out, Frame& f, Child& ch, Cnt<STATS>& cn) {
+    const DevObject& ob = S.objects[cur.h.obj];
+    ShadeCtx c;
+    c.ob = &ob;
+    c.mat = &S.materials[ob.material];
+    c.s = surface<STATS>(S, cur.r, cur.mbTime, cur.h, cn);
+    const DevMaterial& mat = *c.mat;
+    const f3 w_o = makeUnit(sub(cur.eye, c.s.p));
+    const float refractiveIndexOfVacuum = 1.00001;
+    const bool inside = cur.medium > refractiveIndexOfVacuum;
+    if (mat.type == 3) {                                                // Emissive
+        out = muls(muls(ld3(mat.radiance), 2.0f), (float)RT_PI);
+        return false;
+    }
+    if (ob.tex_replace_all >= 0) {
+        out = tex_rgb(S, S.textures[ob.tex_replace_all], c.s.u, c.s.v);
+        return false;
+    }
+    f3 color = mk(0, 0, 0);
+    if (!inside) {
+        color = add(color, mulv(mk(S.ambient[0], S.ambient[1], S.ambient[2]), ld3(mat.ambient)));
+        color = add(color, direct<STATS>(S, c, w_o, cur.mbTime, cur.key, cn));
+    }
+    const f3 n = c.s.n, hp = c.s.p;
+    if (mat.type == 0) {                                                // Mirror (raytracer.cpp:442-472)
+        if (cur.depth <= 0) { out = add(color, mk(0, 0, 0)); return false; }
+        f.kind = FK_MIRROR;
+        f.coef = ld3(mat.mirror);
+        ch.r.d = reflect(n, w_o, mat.roughness, cur.key, RP_ROUGH_REFL);
+        ch.r.o = add(hp, muls(n, S.eps));
+        ch.medium = 1.0f;
+    } else if (mat.type == 2) {                                         // Conductor (raytracer.cpp:208-254)
+        if (cur.depth <= 0) { out = add(color, mk(0, 0, 0)); return false; }
+        f3 d = neg(w_o);
+        float cosTheta = -dot(d, n);
+        float n2 = mat.refractive_index, k2 = mat.absorption_index;
+        float n2k2 = n2 * n2 + k2 * k2;
+        float n2cosTheta2 = 2 * n2 * cosTheta;
+        float cosThetaSqr = cosTheta * cosTheta;
+        float rs = (n2k2 - n2cosTheta2 + cosThetaSqr) / (n2k2 + n2cosTheta2 + cosThetaSqr);
+        float rp = (n2k2 * cosThetaSqr - n2cosTheta2 + 1) / (n2k2 * cosThetaSqr + n2cosTheta2 + 1);
+        float reflectRatio = (float)(0.5 * (rs + rp));
+        if (!(reflectRatio > 0.0001)) { out = add(color, mk(0, 0, 0)); return false; }
+        f.kind = FK_CONDUCTOR;
+        f.coef = ld3(mat.mirror);
+        f.ratio = reflectRatio;
+        ch.r.d = reflect(n, w_o, mat.roughness, cur.key, RP_ROUGH_REFL);
+        ch.r.o = add(hp, muls(n, S.eps));
+        ch.medium = 1.0f;
+    } else if (mat.type == 1) {                                         // Dielectric (raytracer.cpp:261-415)
+        if (cur.depth <= 0) { out = add(color, mk(0, 0, 0)); return false; }
+        float n1 = cur.medium, n2 = mat.refractive_index;
+        f3 d = neg(w_o);
+        f3 modN = n;
+        float cosTheta = -dot(d, modN);
+        bool isEntering = cosTheta > 0.f;
+        float objN = n2;
+        if (!isEntering) {
+            n1 = n2; n2 = 1.0f; objN = 1.0f;
+            cosTheta = fabsf(cosTheta);
+            modN = neg(modN);
+        }
+        float r = n1 / n2;
+        float sinThetaSqr = 1 - (cosTheta * cosTheta);
+        float criticalTerm = r * r * sinThetaSqr;
+        if (criticalTerm > 1) {
+            f.kind = FK_TIR;
+            ch.r.d = reflect(modN, w_o, mat.roughness, cur.key, RP_ROUGH_REFL);
+            ch.r.o = add(hp, muls(modN, S.eps));
+            ch.medium = cur.medium;
+        } else {
+            float cosPhi = sqrtf(1 - criticalTerm);
+            float n2cosTheta = n2 * cosTheta;
+            float n1cosPhi = n1 * cosPhi;
+            float rpar = (n2cosTheta - n1cosPhi) / (n2cosTheta + n1cosPhi);
+            float rperp = (n1 * cosTheta - n2 * cosPhi) / (n1 * cosTheta + n2 * cosPhi);
+            float rReflect = (rpar * rpar + rperp * rperp) / 2;
+            f.kind = FK_DIEL;
+            f.stage = 0;
+            f.ratio = rReflect;
+            f.rT = 1 - rReflect;
+            ch.r.d = reflect(modN, w_o, mat.roughness, cur.key, RP_ROUGH_REFL);
+            ch.r.o = add(hp, muls(modN, S.eps));
+            ch.medium = isEntering ? objN : 1.0f;
+            f.reflDir = ch.r.d;
+            f.rDir = sub(muls(add(d, muls(modN, cosTheta)), r), muls(modN, cosPhi));
+            f.rOrigin = add(hp, muls(neg(modN), S.eps));
+            f.rMedium = isEntering ? objN : 1.0f;
+            f.roughness = mat.roughness;
+        }
+    } else {
+        out = color;                                                    // Default material
+        return false;
+    }
+    f.color = color;
+    f.matIdx = ob.material;
+    f.depth = cur.depth;
+    f.key = cur.key;
+    f.selfT = cur.h.t;
+    f.selfMedium = cur.medium;
+    return true;
+}
+
+DEV f3 env_or_zero(const DevScene& S, f3 dir) {
+    return S.num_env > 0 ? env_sample(S, 0, dir) : mk(0, 0, 0);
+}
+
+// Whole ray tree of one pixel sample; returns RenderPixel's colour
+// (raytracer.cpp:38-63).
+template <int MAXD, bool STATS>
+DEV f3 render_sample(const DevScene& S, const DevCamera& C, int px, int py, uint64_t key, Cnt<STATS>& cn) {
+    // GenerateRay (raytracer.cpp:661-699) + Camera::GetImagePlanePosition (camera.cpp:74-80)
+    const f3 q = ld3(C.q), right = ld3(C.right), up = ld3(C.up), cpos = ld3(C.pos);
+    float su = (float)((px + 0.5) * (double)(C.right_ext - C.left) / C.width);
+    float sv = (float)((py + 0.5) * (double)(C.top - C.bottom) / C.height);
+    f3 ipp = add(add(q, muls(right, su)), muls(up, -sv));
+    Ray ray;
+    ray.o = cpos;
+    if (C.aperture > 0.0001) {
+        f3 aps = ray.o;
+        float first01 = 2.0f * rnd(key, RP_DOF, 0) - 1.0f;
+        aps = add(aps, muls(up, first01 * C.aperture * 0.5f));
+        float second01 = 2.0f * rnd(key, RP_DOF, 1) - 1.0f;
+        aps = add(aps, muls(right, second01 * C.aperture * 0.5f));
+        f3 dir = makeUnit(sub(ray.o, ipp));
+        float tFd = C.focus_distance / dot(dir, ld3(C.gaze));
+        f3 bent = add(ray.o, muls(dir, tFd));
+        ray.d = makeUnit(sub(bent, aps));
+        ray.o = aps;
+    } else {
+        ray.d = makeUnit(sub(ipp, ray.o));
+    }
+    const float mbTime = rnd(key, RP_MOTION, 0);
+    cn.cam();
+    Node cur;
+    if (!trace<false, STATS>(S, ray, mbTime, INFINITY, INFINITY, cur.h, cn)) {
+        if (S.bg_texture >= 0) {
+            float u = px / (float)C.width, v = py / (float)C.height;
+            return tex_rgb(S, S.textures[S.bg_texture], u, v);
+        }
+        if (S.num_env > 0) return env_sample(S, 0, ray.d);
+        return mk((float)S.background[0], (float)S.background[1], (float)S.background[2]);
+    }
+    cur.r = ray;
+    cur.eye = cpos;
+    cur.medium = 1.0f;
+    cur.mbTime = mbTime;
+    cur.depth = S.max_depth;
+    cur.key = key;
+
+    Frame stack[MAXD > 0 ? MAXD : 1];
+    int sp = 0;
+    f3 value;
+    bool vHit;
+    float vT = 0.f, vMedium = 1.f;
+    for (;;) {
+        // ---- shade the current node; a node with children pushes a frame
+        Child ch;
+        const bool spawn = shade_node<STATS>(S, cur, value, stack[MAXD > 0 ? sp : 0], ch, cn);
+        if (MAXD > 0 && spawn) {
+            ++sp;
+            const Frame& f = stack[sp - 1];
+            cn.sec();
+            Node nx;
+            if (trace<false, STATS>(S, ch.r, cur.mbTime, INFINITY, INFINITY, nx.h, cn)) {
+                nx.r = ch.r; nx.eye = ch.r.o; nx.medium = ch.medium; nx.mbTime = cur.mbTime;
+                nx.depth = f.depth - 1;
+                nx.key = child_key(f.key, 0);
+                cur = nx;
+                continue;
+            }
+            // miss (ComputeMirrorReflection :461-470, dielectric reflected :351-356)
+            if (f.kind == FK_MIRROR) value = env_or_zero(S, ch.r.d);
+            else if (f.kind == FK_DIEL) value = env_or_zero(S, f.reflDir);
+            else value = mk(0, 0, 0);
+            vHit = false;
+        } else {
+            vHit = true; vT = cur.h.t; vMedium = cur.medium;
+        }
+        // ---- propagate finished values up the stack
+        bool descended = false;
+        while (MAXD > 0 && sp > 0) {
+            Frame& f = stack[sp - 1];
+            const DevMaterial& pm = S.materials[f.matIdx];
+            if (f.kind == FK_DIEL && f.stage == 0) {
+                f.refl = (vHit && vMedium > 1.00001f) ? beer(vT, pm.absorption, value) : value;
+                f.stage = 1;
+                // refracted ray (raytracer.cpp:362-392)
+                f3 wr = f.rDir;
+                if (f.roughness > 0.001) {
+                    f3 u, v;
+                    onb(wr, u, v);
+                    float psi1 = rnd(f.key, RP_ROUGH_REFR, 0) - 0.5f;
+                    float psi2 = rnd(f.key, RP_ROUGH_REFR, 1) - 0.5f;
+                    wr = makeUnit(add(wr, muls(add(muls(u, psi1), muls(v, psi2)), f.roughness)));
+                } else {
+                    wr = makeUnit(wr);
+                }
+                Ray rr;
+                rr.o = f.rOrigin;
+                rr.d = wr;
+                cn.sec();
+                Node nx;
+                if (trace<false, STATS>(S, rr, cur.mbTime, INFINITY, INFINITY, nx.h, cn)) {
+                    nx.r = rr; nx.eye = rr.o; nx.medium = f.rMedium; nx.mbTime = cur.mbTime;
+                    nx.depth = f.depth - 1;
+                    nx.key = child_key(f.key, 1);
+                    cur = nx;
+                    descended = true;
+                    break;
+                }
+                value = env_or_zero(S, f.reflDir);      // refracted miss uses the reflected dir (:408)
+                vHit = false;
+                continue;
+            }
+            f3 term;
+            if (f.kind == FK_MIRROR) {
+                term = mulv(f.coef, value);
+            } else if (f.kind == FK_CONDUCTOR) {
+                term = muls(vHit ? mulv(f.coef, value) : mk(0, 0, 0), f.ratio);
+            } else if (f.kind == FK_TIR) {
+                term = vHit ? ((vMedium > 1.0001) ? beer(vT, pm.absorption, value) : value) : mk(0, 0, 0);
+            } else {
+                f3 refr = (vHit && vMedium > 1.001f) ? beer(vT, pm.absorption, value) : value;
+                term = add(muls(f.refl, f.ratio), muls(refr, f.rT));
+            }
+            value = add(f.color, term);
+            vHit = true;
+            vT = f.selfT;
+            vMedium = f.selfMedium;
+            --sp;
+        }
+        if (!descended) return value;
+    }
+}
+
+// Gaussian2D (gaussian.h:3-21) with sigma = 1/6 pixel
+DEV float gauss_weight(float x, float y) {
+    const float sigma = 1.0f / 6.0f;
+    const float sigmaSqr = sigma * sigma;
+    const float c1 = (float)(1.0f / (2.0f * RT_PI * sigmaSqr));
+    float exponent = (float)(-0.5 * ((x * x + y * y) / sigmaSqr));
+    return c1 * expf(exponent);
+}
+
+// x86 cvttss2si + clamp (helperMath.cpp:140-152): out-of-range and NaN give INT_MIN -> 0
+DEV unsigned char ldr(float c) {
+    int i = (c > -2147483904.0f && c < 2147483648.0f) ? (int)c : (int)0x80000000;
+    return (unsigned char)(i < 0 ? 0 : (i > 255 ? 255 : i));
+}
+
+// ---------------------------------------------------------------------------
+// Kernel: one thread per pixel; a 256-thread block covers a 16x16 tile, each wave an
+// 8x8 sub-tile (coherent primary rays).  Tiles are dealt so consecutive tiles share
+// an XCD (blocks b and b+8 share one under round-robin dispatch): better L2 reuse
+// of the BVH levels near the rays' paths.
+// ---------------------------------------------------------------------------
+template <int MAXD, bool STATS>
+__global__ __launch_bounds__(256) void k_render(DevScene S, DevCamera C, RenderParams P, float* __restrict__ hdr,
+                                                unsigned char* __restrict__ ldrOut, float* __restrict__ accum,
+                                                DevCounters* __restrict__ counters) {
+    const int b = blockIdx.x;
+    const int nwg = P.num_tiles;
+    const int q8 = nwg / 8, r8 = nwg % 8, xcd = b % 8;
+    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
+    const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    const int px = tx * 16 + (w & 1) * 8 + (l & 7);
+    const int py = P.row_begin + ty * 16 + (w >> 1) * 8 + (l >> 3);
+    Cnt<STATS> cn;
+    if (px < C.width && py < P.row_end) {
+        const int pixel = px + py * C.width;
+        f3 color;
+        if (C.spp <= 1 && !P.accum_only) {
+            color = render_sample<MAXD, STATS>(S, C, px, py, root_key(P.seed, pixel, 0), cn);
+        } else {
+            // renderThreadMain multisampling (main.cpp:60-101): stratified jitter only
+            // feeds the Gaussian weights; every sample traces the pixel centre.
+            const int nRows = (int)sqrt((double)C.spp);
+            const int nCols = nRows;
+            f3 acc = mk(0, 0, 0);
+            float sumW = 0.0f;
+            for (int s = P.sample_begin; s < P.sample_begin + P.sample_count; ++s) {
+                const uint64_t key = root_key(P.seed, pixel, s);
+                float sx = 0.f, sy = 0.f;
+                if (s < nRows * nCols) {
+                    const int row = s / nCols, col = s % nCols;
+                    float psi1 = rnd(key, RP_JITTER, 0), psi2 = rnd(key, RP_JITTER, 1);
+                    sx = (col + psi1) / nCols;
+                    sy = (row + psi2) / nRows;
+                }
+                f3 col = render_sample<MAXD, STATS>(S, C, px, py, key, cn);
+                float gw = gauss_weight(sx - 0.5f, sy - 0.5f);
+                acc.x += col.x * gw;
+                acc.y += col.y * gw;
+                acc.z += col.z * gw;
+                sumW += gw;
+            }
+            if (P.accum_only) {
+                float4* a4 = reinterpret_cast<float4*>(accum);
+                a4[pixel] = make_float4(acc.x, acc.y, acc.z, sumW);
+                color = mk(0, 0, 0);
+            } else {
+                color = mk(acc.x / sumW, acc.y / sumW, acc.z / sumW);
+            }
+        }
+        if (!P.accum_only) {
+            const size_t idx = 3 * (size_t)pixel;
+            if (hdr) { hdr[idx] = color.x; hdr[idx + 1] = color.y; hdr[idx + 2] = color.z; }
+            if (ldrOut) { ldrOut[idx] = ldr(color.x); ldrOut[idx + 1] = ldr(color.y); ldrOut[idx + 2] = ldr(color.z); }
+        }
+    }
+    if constexpr (STATS) {
+        // one atomic per wave per counter
+        unsigned long long v[7] = {cn.cams, cn.secs, cn.shds, cn.nodes, cn.tris, cn.sphs, cn.objs};
+        for (int k = 0; k < 7; ++k) {
+            unsigned long long x = v[k];
+            for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
+            if (l == 0) atomicAdd(&((unsigned long long*)counters)[k], x);
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host-side launch helpers
+// ---------------------------------------------------------------------------
+int upload_perlin_tables(const int* perm512, const float* grad36) {
+    if (hipMemcpyToSymbol(HIP_SYMBOL(c_perm), perm512, 512 * sizeof(int)) != hipSuccess) return -1;
+    if (hipMemcpyToSymbol(HIP_SYMBOL(c_grad), grad36, 36 * sizeof(float)) != hipSuccess) return -1;
+    return 0;
+}
+
+template <int MAXD, bool STATS>
+static hipError_t launch_t(const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr, unsigned char* l,
+                           float* accum, DevCounters* cnt, hipStream_t stream) {
+    hipLaunchKernelGGL((k_render<MAXD, STATS>), dim3(P.num_tiles), dim3(256), 0, stream, S, C, P, hdr, l, accum, cnt);
+    return hipGetLastError();
+}
+
+int max_supported_depth() { return 32; }
+
+hipError_t launch_render(const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr, unsigned char* l,
+                         float* accum, DevCounters* cnt, bool stats, hipStream_t stream) {
+    const int d = S.max_depth;
+    if (stats) {
+        if (d <= 0) return launch_t<0, true>(S, C, P, hdr, l, accum, cnt, stream);
+        if (d <= 8) return launch_t<8, true>(S, C, P, hdr, l, accum, cnt, stream);
+        return launch_t<32, true>(S, C, P, hdr, l, accum, cnt, stream);
+    }
+    if (d <= 0) return launch_t<0, false>(S, C, P, hdr, l, accum, cnt, stream);
+    if (d <= 8) return launch_t<8, false>(S, C, P, hdr, l, accum, cnt, stream);
+    return launch_t<32, false>(S, C, P, hdr, l, accum, cnt, stream);
+}
+
+}  // namespace rtg

@@ -1,0 +1,96 @@
+// ORACLE -- test infrastructure only.  Driver linked against the reference's own
+// sources (compiled from /root/reference/src by oracle/Makefile into oracle/_ref/;
+// nothing of the reference is copied into this repository).
+//
+//   refdriver dump  <scene.xml> <out.bin> [camera]
+//       Single-threaded loop calling Raytracer::RenderPixel(x, y, cam) for every pixel
+//       of one camera (raytracer.hpp:19), i.e. the spp==1 path of renderThreadMain
+//       (main.cpp:102-105).  Writes "RTGF" int32 w, int32 h, then w*h*3 float32 RGB,
+//       row-major 3*(x+y*w) (main.cpp:109).  Deterministic scenes only (the reference's
+//       random streams are seeded from rand() and raced by its threads).
+//   refdriver bench <scene.xml> <threads> <reps> [camera]
+//       Times the reference's row-band render exactly as main.cpp:164-185 partitions it
+//       (rows [t*(H/T), (t+1)*(H/T)) per thread; spawn -> join), spp==1 per pixel via
+//       RenderPixel, and prints one JSON line with the per-rep seconds.
+#define STB_IMAGE_WRITE_IMPLEMENTATION
+#include "stb_image_write.h"
+#define STB_IMAGE_IMPLEMENTATION
+#define TINYEXR_IMPLEMENTATION
+
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#include "raytracer.hpp"
+
+using namespace DorkTracer;
+
+static int dump(const char* xml, const char* out, int ci) {
+    Scene scene;
+    scene.loadFromXml(xml);
+    Raytracer renderer(scene);
+    if (ci < 0 || ci >= (int)scene.cameras.size()) { std::fprintf(stderr, "bad camera\n"); return 2; }
+    Camera& cam = scene.cameras[ci];
+    if (cam.IsPathTracingEnabled()) renderer.EnablePathTracing(cam.GetRendererParams());
+    renderer.activeCamera = &cam;
+    const int w = cam.imageWidth, h = cam.imageHeight;
+    std::vector<float> img((size_t)w * h * 3);
+    for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x) {
+            Vec3f c = renderer.RenderPixel(x, y, cam);
+            size_t i = 3 * ((size_t)x + (size_t)y * w);
+            img[i] = c.x; img[i + 1] = c.y; img[i + 2] = c.z;
+        }
+    FILE* f = std::fopen(out, "wb");
+    if (!f) { std::perror(out); return 1; }
+    int32_t hdr[2] = {w, h};
+    std::fwrite("RTGF", 1, 4, f);
+    std::fwrite(hdr, sizeof(int32_t), 2, f);
+    std::fwrite(img.data(), sizeof(float), img.size(), f);
+    std::fclose(f);
+    return 0;
+}
+
+static int bench(const char* xml, int threads, int reps, int ci) {
+    Scene scene;
+    scene.loadFromXml(xml);
+    Raytracer renderer(scene);
+    Camera& cam = scene.cameras[ci];
+    renderer.activeCamera = &cam;
+    const int w = cam.imageWidth, h = cam.imageHeight;
+    std::vector<float> img((size_t)w * h * 3);
+    std::printf("{\"threads\": %d, \"width\": %d, \"height\": %d, \"seconds\": [", threads, w, h);
+    for (int r = 0; r < reps; ++r) {
+        auto t0 = std::chrono::steady_clock::now();
+        std::vector<std::thread> th;
+        for (int t = 0; t < threads; ++t) {
+            th.emplace_back([&, t]() {
+                int y0 = t * (h / threads), y1 = y0 + h / threads;
+                for (int y = y0; y < y1; ++y)
+                    for (int x = 0; x < w; ++x) {
+                        Vec3f c = renderer.RenderPixel(x, y, cam);
+                        size_t i = 3 * ((size_t)x + (size_t)y * w);
+                        img[i] = c.x; img[i + 1] = c.y; img[i + 2] = c.z;
+                    }
+            });
+        }
+        for (auto& t : th) t.join();
+        double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+        std::printf("%s%.6f", r ? ", " : "", s);
+    }
+    double checksum = 0;
+    for (float v : img) checksum += v;
+    std::printf("], \"checksum\": %.6f}\n", checksum);
+    return 0;
+}
+
+int main(int argc, char** argv) {
+    if (argc >= 4 && !std::strcmp(argv[1], "dump")) return dump(argv[2], argv[3], argc > 4 ? std::atoi(argv[4]) : 0);
+    if (argc >= 5 && !std::strcmp(argv[1], "bench"))
+        return bench(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), argc > 5 ? std::atoi(argv[5]) : 0);
+    std::fprintf(stderr, "usage: refdriver dump <scene.xml> <out.bin> [camera] | bench <scene.xml> <threads> <reps> [camera]\n");
+    return 2;
+}
