@@ -137,7 +137,9 @@ std::string need_text(XmlNode* e, const char* what) {
 // ---------------------------------------------------------------------------
 void Loader::load(const std::string& path) {
     XmlDocument file;
-    if (!file.Load(path)) fail(RTG_ERR_PARSE, "Error: The xml file cannot be loaded. " + file.error);
+    if (!file.Load(path))
+        fail(file.error.rfind("cannot open", 0) == 0 ? RTG_ERR_IO : RTG_ERR_PARSE,
+             "Error: The xml file cannot be loaded. " + file.error);
     XmlNode* root = file.FirstChild();
     if (!root) fail(RTG_ERR_PARSE, "Error: Root is not found.");
 
@@ -743,7 +745,7 @@ void Loader::computeTransform(Xform& xf, const std::string& str) {   // parser.c
             int id = digit(idx + 1);
             if (id < 1 || id > (int)rotations.size()) fail(RTG_ERR_PARSE, "rotation id out of range");
             Rot r = rotations[id - 1];
-            double angle = r.w * (M_PI / 180.0f);
+            float angle = r.w * (M_PI / 180.0f);   // float, as parser.cpp:665
             M4 rot, invRot;
             rot.valid = invRot.valid = false;
             if (r.x >= 0.99 && r.y <= 0.001 && r.z <= 0.0001) { rot = M4::rotX(angle); invRot = M4::rotX(-angle); }

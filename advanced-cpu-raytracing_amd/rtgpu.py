@@ -1,0 +1,212 @@
+"""ctypes binding of the rtgpu C-ABI (include/rtgpu.h).
+
+Mirrors the reference's render interface for Python callers (tests, bench.py):
+
+* ``HostScene(xml)``          -- ``DorkTracer::Scene::loadFromXml`` (src/parser.cpp:26-577)
+* ``DeviceScene(host, dev)``  -- ``Raytracer::Raytracer(Scene&)`` (src/raytracer.cpp:7-16),
+                                 a device-resident replica on HIP device ``dev``
+* ``DeviceScene.render(cam)`` -- the per-camera block of ``main()`` (src/main.cpp:142-196):
+                                 every pixel through ``RenderPixel`` (raytracer.hpp:19),
+                                 returning the float image (main.cpp:114-116) and the
+                                 ``clamp((int)c)`` LDR image (main.cpp:121)
+
+The product path is librtgpu.so only; importing this module fails loudly when the
+library has not been built.  There is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "librtgpu.so")
+
+RTG_RENDER_COUNT_STATS = 1
+RTG_RENDER_ACCUM_ONLY = 2
+
+
+class RTGError(RuntimeError):
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"rtgpu error {code}: {msg}")
+        self.code = code
+
+
+class RenderOpts(ctypes.Structure):
+    _fields_ = [
+        ("camera", ctypes.c_int32),
+        ("sample_begin", ctypes.c_int32),
+        ("sample_count", ctypes.c_int32),
+        ("row_begin", ctypes.c_int32),
+        ("row_end", ctypes.c_int32),
+        ("flags", ctypes.c_int32),
+        ("seed", ctypes.c_uint64),
+    ]
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_uint64) for n in (
+        "camera_rays", "secondary_rays", "shadow_rays", "node_visits", "tri_tests",
+        "sphere_tests", "object_tests", "pad0")]
+
+    def as_dict(self) -> dict:
+        return {n: int(getattr(self, n)) for n, _ in self._fields_ if n != "pad0"}
+
+
+# every symbol include/rtgpu.h declares
+EXPORTED = [
+    "rtg_host_scene_load_xml", "rtg_host_scene_desc", "rtg_host_scene_free",
+    "rtg_desc_camera_info", "rtg_desc_counts", "rtg_scene_create", "rtg_scene_destroy",
+    "rtg_device_count", "rtg_render", "rtg_render_device", "rtg_resolve_accum",
+    "rtg_scene_stats", "rtg_scene_reset_stats", "rtg_write_png", "rtg_write_hdr",
+    "rtg_last_error", "rtg_abi_version",
+]
+
+_lib = None
+
+
+def lib() -> ctypes.CDLL:
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise RTGError(-1, f"{LIB_PATH} not built: run `make -C {HERE}` (or __graft_entry__.build())")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, i32, P = ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER
+    L.rtg_last_error.restype = ctypes.c_char_p
+    L.rtg_abi_version.restype = ctypes.c_int
+    L.rtg_host_scene_load_xml.argtypes = [ctypes.c_char_p, P(vp)]
+    L.rtg_host_scene_desc.argtypes = [vp]
+    L.rtg_host_scene_desc.restype = vp
+    L.rtg_host_scene_free.argtypes = [vp]
+    L.rtg_host_scene_free.restype = None
+    L.rtg_desc_camera_info.argtypes = [vp, ctypes.c_int, P(i32), P(i32), P(i32), P(i32)]
+    L.rtg_desc_counts.argtypes = [vp] + [P(ctypes.c_int64)] * 4
+    L.rtg_scene_create.argtypes = [vp, ctypes.c_int, P(vp)]
+    L.rtg_scene_destroy.argtypes = [vp]
+    L.rtg_scene_destroy.restype = None
+    L.rtg_device_count.argtypes = [P(i32)]
+    L.rtg_render.argtypes = [vp, P(RenderOpts), vp, vp]
+    L.rtg_render_device.argtypes = [vp, P(RenderOpts), vp, vp, vp, vp]
+    L.rtg_resolve_accum.argtypes = [vp, i32, i32, vp, vp]
+    L.rtg_scene_stats.argtypes = [vp, P(Stats)]
+    L.rtg_scene_reset_stats.argtypes = [vp]
+    L.rtg_write_png.argtypes = [ctypes.c_char_p, i32, i32, vp]
+    L.rtg_write_hdr.argtypes = [ctypes.c_char_p, i32, i32, vp]
+    _lib = L
+    return L
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise RTGError(rc, lib().rtg_last_error().decode(errors="replace"))
+
+
+def device_count() -> int:
+    n = ctypes.c_int32()
+    _check(lib().rtg_device_count(ctypes.byref(n)))
+    return n.value
+
+
+class HostScene:
+    """Parsed + flattened scene (rtg_host_scene).  Paths inside the XML resolve like the
+    reference's: PLY relative to the current directory, images as ``inputs/<name>``."""
+
+    def __init__(self, xml_path: str):
+        h = ctypes.c_void_p()
+        _check(lib().rtg_host_scene_load_xml(os.fsencode(xml_path), ctypes.byref(h)))
+        self._h = h
+        self.desc = lib().rtg_host_scene_desc(h)
+
+    def camera(self, idx: int = 0) -> dict:
+        w, h, s, t = (ctypes.c_int32() for _ in range(4))
+        _check(lib().rtg_desc_camera_info(self.desc, idx, ctypes.byref(w), ctypes.byref(h),
+                                          ctypes.byref(s), ctypes.byref(t)))
+        return {"width": w.value, "height": h.value, "spp": s.value, "tonemapped": bool(t.value)}
+
+    def counts(self) -> dict:
+        v = [ctypes.c_int64() for _ in range(4)]
+        _check(lib().rtg_desc_counts(self.desc, *[ctypes.byref(x) for x in v]))
+        return dict(zip(("objects", "faces", "nodes", "lights"), (x.value for x in v)))
+
+    def num_cameras(self) -> int:
+        n = 0
+        while True:
+            try:
+                self.camera(n)
+            except RTGError:
+                return n
+            n += 1
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().rtg_host_scene_free(self._h)
+            self._h = None
+            self.desc = None
+
+    def __del__(self):
+        self.close()
+
+
+class DeviceScene:
+    """Device-resident scene replica (rtg_scene) on HIP device ``device``."""
+
+    def __init__(self, host: HostScene, device: int = 0):
+        s = ctypes.c_void_p()
+        _check(lib().rtg_scene_create(host.desc, device, ctypes.byref(s)))
+        self._s = s
+        self.host = host
+        self.device = device
+
+    @staticmethod
+    def opts(camera=0, sample_begin=0, sample_count=-1, rows=(0, 0), flags=0, seed=0x5EED) -> RenderOpts:
+        return RenderOpts(camera, sample_begin, sample_count, rows[0], rows[1], flags, seed)
+
+    def render(self, camera: int = 0, rows=(0, 0), flags: int = 0, seed: int = 0x5EED):
+        """Host-buffer render of one camera -> (hdr float32 HxWx3, ldr uint8 HxWx3)."""
+        c = self.host.camera(camera)
+        hdr = np.zeros((c["height"], c["width"], 3), np.float32)
+        ldr = np.zeros((c["height"], c["width"], 3), np.uint8)
+        o = self.opts(camera, 0, -1, rows, flags, seed)
+        _check(lib().rtg_render(self._s, ctypes.byref(o), hdr.ctypes.data, ldr.ctypes.data))
+        return hdr, ldr
+
+    def render_device(self, hdr_ptr: int, ldr_ptr: int, stream: int = 0, camera: int = 0, flags: int = 0,
+                      seed: int = 0x5EED, accum_ptr: int = 0, sample_begin: int = 0, sample_count: int = -1,
+                      rows=(0, 0)):
+        """Asynchronous render into device buffers (e.g. torch tensor data_ptr()s) on ``stream``."""
+        o = self.opts(camera, sample_begin, sample_count, rows, flags, seed)
+        _check(lib().rtg_render_device(self._s, ctypes.byref(o), hdr_ptr or None, ldr_ptr or None,
+                                       accum_ptr or None, stream or None))
+
+    def stats(self) -> dict:
+        st = Stats()
+        _check(lib().rtg_scene_stats(self._s, ctypes.byref(st)))
+        return st.as_dict()
+
+    def reset_stats(self):
+        _check(lib().rtg_scene_reset_stats(self._s))
+
+    def close(self):
+        if getattr(self, "_s", None):
+            lib().rtg_scene_destroy(self._s)
+            self._s = None
+
+    def __del__(self):
+        self.close()
+
+
+def resolve_accum(accum: np.ndarray):
+    """(sum w*c, sum w) per pixel -> (hdr, ldr); host side (samples split across devices)."""
+    h, w, _ = accum.shape
+    accum = np.ascontiguousarray(accum, np.float32)
+    hdr = np.zeros((h, w, 3), np.float32)
+    ldr = np.zeros((h, w, 3), np.uint8)
+    _check(lib().rtg_resolve_accum(accum.ctypes.data, w, h, hdr.ctypes.data, ldr.ctypes.data))
+    return hdr, ldr
+
+
+def write_png(path: str, ldr: np.ndarray):
+    ldr = np.ascontiguousarray(ldr, np.uint8)
+    _check(lib().rtg_write_png(os.fsencode(path), ldr.shape[1], ldr.shape[0], ldr.ctypes.data))

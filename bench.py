@@ -1,0 +1,222 @@
+"""Headline bench: Mrays/s on the BASELINE.json synthetic K-triangle scene at 1920x1080
+(primary + shadow rays), with the HBM-roofline fraction of the render kernel and the
+reference's own multithreaded CPU path timed on this host beside it.
+
+    python bench.py [--gpus N --steps K --warmup W]
+    python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
+        --master-port P bench.py --gpus N --steps K --warmup W
+
+A step = one full 1920x1080 frame (one sample pass) traced and shaded on each rank,
+inputs (scene, BVH) resident in HBM.  Ranks are independent (sample-parallel: rank r
+traces sample pass r of the same frame) -> weak scaling, no collective on the data path;
+the only collectives are the barriers around the timed region and the max-over-ranks of
+the elapsed time.
+"""
+import argparse
+import json
+import os
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+PKG = os.path.join(ROOT, "advanced-cpu-raytracing_amd")
+sys.path.insert(0, PKG)
+
+METRIC = "Mrays/sec + achieved HBM GB/s fraction, 1920×1080 primary+shadow rays"
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md)
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--warmup", type=int, default=3)
+    p.add_argument("--K", type=int, default=100352, help="triangles in the synthetic height field")
+    p.add_argument("--width", type=int, default=1920)
+    p.add_argument("--height", type=int, default=1080)
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-threads", type=int, default=8, help="reference THREAD_COUNT (main.cpp:15)")
+    p.add_argument("--cpu-reps", type=int, default=3)
+    p.add_argument("--sweep", action="store_true", help="also report K in {1k,10k,1M} (extra field)")
+    return p.parse_args()
+
+
+def cpu_baseline(xml_dir, xml, rays_per_frame, threads, reps):
+    """Reference CPU path (oracle/_ref/refdriver: the reference's own sources, row-band
+    threads exactly as main.cpp:38-39,164-185) on this host; falls back to the oracle
+    restatement ("port") when the reference build is absent."""
+    drv = os.path.join(ROOT, "oracle", "_ref", "refdriver")
+    sample = f"full 1920x1080 frame x {reps} reps, {threads} threads (render only: spawn->join)"
+    if os.path.exists(drv):
+        out = subprocess.run([drv, "bench", os.path.basename(xml), str(threads), str(reps)], cwd=xml_dir,
+                             capture_output=True, text=True, timeout=600, check=True).stdout
+        line = [l for l in out.splitlines() if l.startswith("{")][-1]
+        secs = sorted(json.loads(line)["seconds"])
+        med = secs[len(secs) // 2]
+        return {"value": round(rays_per_frame / med / 1e6, 3), "unit": "Mrays/s", "cores": threads,
+                "kind": "reference", "sample": sample, "seconds_median": round(med, 4)}
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_bind as ob
+    import rtgpu
+    hs = rtgpu.HostScene(xml)
+    secs = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        ob.render(hs, threads=threads)
+        secs.append(time.perf_counter() - t0)
+    secs.sort()
+    med = secs[len(secs) // 2]
+    return {"value": round(rays_per_frame / med / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": sample, "seconds_median": round(med, 4)}
+
+
+def measure(ds, torch, hdr, ldr, steps, warmup, seed, barrier):
+    stream = torch.cuda.current_stream()
+    sptr = stream.cuda_stream
+    for _ in range(warmup):
+        ds.render_device(hdr.data_ptr(), ldr.data_ptr(), sptr, seed=seed)
+    torch.cuda.synchronize()
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(steps):
+        starts[k].record(stream)
+        ds.render_device(hdr.data_ptr(), ldr.data_ptr(), sptr, seed=seed)
+        ends[k].record(stream)
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / steps
+    return elapsed, kern_ms
+
+
+def main():
+    args = parse()
+    import torch
+
+    import rtgpu
+    import scenes
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    barrier = (lambda: dist.barrier()) if dist else (lambda: None)
+
+    tmp = tempfile.mkdtemp(prefix=f"rtg_bench_r{rank}_")
+    old = os.getcwd()
+    try:
+        xml = scenes.synthetic_heightfield(tmp, K=args.K, width=args.width, height=args.height)
+        os.chdir(tmp)
+        hs = rtgpu.HostScene(xml)
+        ds = rtgpu.DeviceScene(hs, local)
+        cam = hs.camera(0)
+        H, W = cam["height"], cam["width"]
+        hdr = torch.empty((H, W, 3), dtype=torch.float32, device=f"cuda:{local}")
+        ldr = torch.empty((H, W, 3), dtype=torch.uint8, device=f"cuda:{local}")
+        seed = 0x5EED + rank
+
+        # untimed counting pass: rays / BVH nodes / triangle tests per frame
+        ds.reset_stats()
+        ds.render_device(hdr.data_ptr(), ldr.data_ptr(), torch.cuda.current_stream().cuda_stream, seed=seed,
+                         flags=rtgpu.RTG_RENDER_COUNT_STATS)
+        torch.cuda.synchronize()
+        st = ds.stats()
+        rays = st["camera_rays"] + st["secondary_rays"] + st["shadow_rays"]
+
+        elapsed, kern_ms = measure(ds, torch, hdr, ldr, args.steps, args.warmup, seed, barrier)
+        if dist:
+            t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            elapsed = float(t.item())
+            k = torch.tensor([kern_ms], dtype=torch.float64, device=f"cuda:{local}")
+            dist.all_reduce(k, op=dist.ReduceOp.MAX)
+            kern_ms = float(k.item())
+
+        value = world * rays * args.steps / elapsed / 1e6
+        # algorithmic HBM bytes of one launch: 32 B per node visit, 36 B per
+        # triangle test, 64 B per ray (ray in + hit out), 15 B per pixel written
+        algo_bytes = 32 * st["node_visits"] + 36 * st["tri_tests"] + 64 * rays + 15 * W * H
+        achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
+        result = {
+            "metric": METRIC,
+            "value": round(value, 2),
+            "unit": "Mrays/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 4),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (seeded procedural height field, written as the reference's XML+PLY)",
+            "config": {
+                "workload": f"synthetic height field K={args.K} tris, {W}x{H}, 1 spp, 1 point light, "
+                            "default Blinn-Phong, primary+shadow rays",
+                "scene_K": int(args.K),
+                "width": W, "height": H, "spp": 1,
+                "rays_per_frame": int(rays),
+                "camera_rays": int(st["camera_rays"]), "shadow_rays": int(st["shadow_rays"]),
+                "node_visits_per_ray": round(st["node_visits"] / max(rays, 1), 2),
+                "tri_tests_per_ray": round(st["tri_tests"] / max(rays, 1), 2),
+                "parallelism": f"sample-parallel x{world} (rank r traces sample pass r)",
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None,
+                "kernel": "k_render",
+                "kernel_ms": round(kern_ms, 4),
+                "algo_bytes_per_launch": int(algo_bytes),
+            },
+            "cpu_baseline": None,
+        }
+        if args.sweep and rank == 0:
+            sweep = {}
+            for K in (1000, 10082, 1002528):
+                sub = tempfile.mkdtemp(prefix="rtg_sweep_")
+                x2 = scenes.synthetic_heightfield(sub, K=K, width=W, height=H)
+                os.chdir(sub)
+                h2 = rtgpu.HostScene(x2)
+                d2 = rtgpu.DeviceScene(h2, local)
+                d2.reset_stats()
+                d2.render_device(hdr.data_ptr(), ldr.data_ptr(), torch.cuda.current_stream().cuda_stream,
+                                 flags=rtgpu.RTG_RENDER_COUNT_STATS)
+                torch.cuda.synchronize()
+                s2 = d2.stats()
+                r2 = s2["camera_rays"] + s2["shadow_rays"] + s2["secondary_rays"]
+                e2, k2 = measure(d2, torch, hdr, ldr, max(3, args.steps // 2), 1, 0x5EED, lambda: None)
+                sweep[str(K)] = {"mrays_s": round(r2 * max(3, args.steps // 2) / e2 / 1e6, 1),
+                                 "kernel_ms": round(k2, 3), "rays": int(r2)}
+                d2.close()
+                h2.close()
+                shutil.rmtree(sub, ignore_errors=True)
+            result["sweep_K"] = sweep
+        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+            result["cpu_baseline"] = cpu_baseline(tmp, xml, rays, args.cpu_threads, args.cpu_reps)
+        if rank == 0:
+            print(json.dumps(result), flush=True)
+    finally:
+        os.chdir(old)
+        shutil.rmtree(tmp, ignore_errors=True)
+        if dist:
+            dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -274,9 +274,11 @@ private:
     }
 
     // ---- bvh.cpp:5-30
-    bool IntersectBVH(int node, Ray& ray, const rtg_mesh& M, const rtg_object& ob) {
+    // count_root=false: the root box was just tested as the mesh bbox (mesh.cpp:172 tests
+    // this->bbox, which equals bvh[0].bbox) -- counted once, as the GPU walk does
+    bool IntersectBVH(int node, Ray& ray, const rtg_mesh& M, const rtg_object& ob, bool count_root = true) {
         const rtg_bvh_node& n = S.nodes[M.node_offset + node];
-        cnt.nodes++;
+        if (count_root) cnt.nodes++;
         if (!BoxHit(n.bmin, n.bmax, ray)) return false;
         bool hasHit = false;
         if (n.left < 0 && n.count > 0) {
@@ -298,8 +300,9 @@ private:
         ray.origin = applyT(ob.inv_transform, ray.origin, 1.0f);
         ray.dir = applyT(ob.inv_transform, ray.dir, 0.0f);
         if (ob.flags & RTG_OBJF_MOTION_BLUR) ray.origin = ray.origin + V(ob.motion_blur) * ray.motionBlurTime;
+        cnt.nodes++;
         if (BoxHit(ob.bbox_min, ob.bbox_max, ray)) {
-            bool hasHit = IntersectBVH(0, ray, M, ob);
+            bool hasHit = IntersectBVH(0, ray, M, ob, false);
             ray.origin = oc;
             ray.dir = dc;
             if (hasHit) {

@@ -1,0 +1,93 @@
+"""Test-only binding of the CPU oracle (oracle/liboracle.so) and golden fixtures.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg use this module;
+the product (advanced-cpu-raytracing_amd/) never imports it.
+"""
+import ctypes
+import json
+import os
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE_LIB = os.path.join(ROOT, "oracle", "liboracle.so")
+REF_DRIVER = os.path.join(ROOT, "oracle", "_ref", "refdriver")
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(ORACLE_LIB):
+            raise RuntimeError(f"{ORACLE_LIB} not built: run `make -C {os.path.dirname(ORACLE_LIB)}`")
+        L = ctypes.CDLL(ORACLE_LIB)
+        vp = ctypes.c_void_p
+        L.oracle_render.argtypes = [vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_uint64, ctypes.c_int, vp, vp, vp, vp]
+        L.oracle_render.restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+STAT_NAMES = ("camera_rays", "secondary_rays", "shadow_rays", "node_visits", "tri_tests", "sphere_tests",
+              "object_tests")
+
+
+def render(host_scene, camera=0, rows=(0, 0), seed=0x5EED, threads=None, sample_begin=0, sample_count=-1,
+           accum=False):
+    """CPU restatement of RenderPixel over a parsed scene -> (hdr, ldr, stats) or (accum, stats)."""
+    c = host_scene.camera(camera)
+    h, w = c["height"], c["width"]
+    threads = threads or min(16, os.cpu_count() or 1)
+    st = np.zeros(7, np.uint64)
+    if accum:
+        acc = np.zeros((h, w, 4), np.float32)
+        rc = lib().oracle_render(host_scene.desc, camera, rows[0], rows[1], sample_begin, sample_count, seed,
+                                 threads, None, None, acc.ctypes.data, st.ctypes.data)
+        if rc:
+            raise RuntimeError("oracle_render failed")
+        return acc, dict(zip(STAT_NAMES, map(int, st)))
+    hdr = np.zeros((h, w, 3), np.float32)
+    ldr = np.zeros((h, w, 3), np.uint8)
+    rc = lib().oracle_render(host_scene.desc, camera, rows[0], rows[1], sample_begin, sample_count, seed, threads,
+                             hdr.ctypes.data, ldr.ctypes.data, None, st.ctypes.data)
+    if rc:
+        raise RuntimeError("oracle_render failed")
+    return hdr, ldr, dict(zip(STAT_NAMES, map(int, st)))
+
+
+def clamp_ldr(hdr):
+    """x86 (int) conversion + clamp to [0,255] (helperMath.cpp:140-152)."""
+    x = np.asarray(hdr, np.float64)
+    ok = (x > -2147483904.0) & (x < 2147483648.0)
+    i = np.where(ok, np.trunc(np.where(ok, x, 0)), -2147483648.0)
+    return np.clip(i, 0, 255).astype(np.uint8)
+
+
+def load_golden(name):
+    d = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    return d["hdr"]
+
+
+def manifest():
+    with open(os.path.join(GOLDEN, "manifest.json")) as f:
+        return json.load(f)
+
+
+def compare(got, ref, rel=1e-4):
+    """Parity figures: relative check |d| <= rel*max(1,|ref|), bit-exact and LDR-exact rates."""
+    got = np.asarray(got, np.float32)
+    ref = np.asarray(ref, np.float32)
+    d = np.abs(got.astype(np.float64) - ref.astype(np.float64))
+    tol = rel * np.maximum(1.0, np.abs(ref.astype(np.float64)))
+    both_nan = np.isnan(got) & np.isnan(ref)
+    ok = (d <= tol) | both_nan
+    return {
+        "rel_pass": float(np.mean(ok)),
+        "bit_exact": float(np.mean((got.view(np.uint32) == ref.view(np.uint32)) | both_nan)),
+        "ldr_exact": float(np.mean(clamp_ldr(got) == clamp_ldr(ref))),
+        "max_abs": float(np.nanmax(np.where(both_nan, 0, d))) if d.size else 0.0,
+        "n_fail": int(np.sum(~ok)),
+    }
