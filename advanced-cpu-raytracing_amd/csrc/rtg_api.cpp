@@ -3,6 +3,7 @@
 
 #include <cstdarg>
 #include <cstdio>
+#include <algorithm>
 #include <cstring>
 #include <memory>
 #include <string>
@@ -89,6 +90,15 @@ struct rtg_scene {
     DevBuf<rtg::DevDirLight> dir_lights;
     DevBuf<rtg::DevSpotLight> spot_lights;
     DevBuf<rtg::DevCounters> counters;
+    DevBuf<int> perm;
+    DevBuf<float> grad;
+    bool wave_ok = false;             // scene renders on the wavefront pipeline
+    int num_slots = 0;                // lights per pixel (wavefront light slots)
+    // wavefront buffers, grown on demand
+    size_t wave_pixels = 0;
+    int wave_slots = 0;
+    void* wave_mem = nullptr;
+    rtg::WaveBufs wave;
     // scratch for the host-buffer entry point
     float* d_hdr = nullptr;
     unsigned char* d_ldr = nullptr;
@@ -96,6 +106,7 @@ struct rtg_scene {
     ~rtg_scene() {
         if (d_hdr) (void)hipFree(d_hdr);
         if (d_ldr) (void)hipFree(d_ldr);
+        if (wave_mem) (void)hipFree(wave_mem);
     }
 };
 
@@ -260,12 +271,25 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
         for (int k = 0; k < 3; ++k) { D.bmin[k] = o.bbox_min[k]; D.bmax[k] = o.bbox_max[k]; }
         f4(D.mbv, o.motion_blur);
         f4(D.center, o.center, o.radius);
+        bool ident = true;
         for (int k = 0; k < 12; ++k) {
             D.inv[k] = o.inv_transform[k];
             D.invT[k] = o.inv_transpose[k];
             D.baseInvT[k] = o.base_inv_transpose[k];
+            ident &= o.inv_transform[k] == ((k % 5 == 0) ? 1.0 : 0.0);
         }
+        if (ident) D.flags |= rtg::OBJF_IDENTITY;
     }
+    // wavefront eligibility: no ray-tree children and no motion blur
+    bool branching = false, blur = false;
+    for (int i = 0; i < d->num_materials; ++i) {
+        int t = d->materials[i].type;
+        branching |= (t == RTG_MAT_MIRROR || t == RTG_MAT_DIELECTRIC || t == RTG_MAT_CONDUCTOR);
+    }
+    for (int i = 0; i < d->num_objects; ++i) blur |= (d->objects[i].flags & RTG_OBJF_MOTION_BLUR) != 0;
+    sc->wave_ok = !blur && (d->max_recursion_depth <= 0 || !branching);
+    sc->num_slots = d->num_point_lights + d->num_area_lights + d->num_env_lights + d->num_dir_lights +
+                    d->num_spot_lights;
     std::vector<rtg::DevMaterial> mats(d->num_materials);
     for (int i = 0; i < d->num_materials; ++i) {
         const rtg_material& m = d->materials[i];
@@ -356,9 +380,10 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     std::memset(zero.data(), 0, sizeof(rtg::DevCounters));
     HIP_TRY(sc->counters.upload(zero));
     {
-        int perm[512];
+        std::vector<int> perm(512);
         for (int i = 0; i < 512; ++i) perm[i] = kPerm256[i & 255];
-        if (rtg::upload_perlin_tables(perm, kGrad) != 0) return set_err(RTG_ERR_HIP, "perlin table upload failed");
+        HIP_TRY(sc->perm.upload(perm));
+        HIP_TRY(sc->grad.upload(std::vector<float>(kGrad, kGrad + 36)));
     }
 
     rtg::DevScene& S = sc->ds;
@@ -370,6 +395,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     S.textures = sc->textures.p; S.images = sc->images.p; S.texels = sc->texels.p;
     S.point_lights = sc->point_lights.p; S.area_lights = sc->area_lights.p; S.dir_lights = sc->dir_lights.p;
     S.spot_lights = sc->spot_lights.p; S.env_images = sc->env_images.p;
+    S.perm = sc->perm.p; S.grad = sc->grad.p;
     S.num_objects = d->num_objects; S.num_point = d->num_point_lights; S.num_area = d->num_area_lights;
     S.num_dir = d->num_dir_lights; S.num_spot = d->num_spot_lights; S.num_env = d->num_env_lights;
     S.max_depth = d->max_recursion_depth;
@@ -416,6 +442,56 @@ static int prepare(rtg_scene* s, const rtg_render_opts* o, rtg::DevCamera& C, rt
     return RTG_OK;
 }
 
+// Sizes the wavefront buffers for `pixels` pixels x `slots` light slots (one allocation).
+static int ensure_wave(rtg_scene* s, size_t pixels, int slots) {
+    if (s->wave_mem && s->wave_pixels >= pixels && s->wave_slots >= slots) return RTG_OK;
+    if (s->wave_mem) { (void)hipFree(s->wave_mem); s->wave_mem = nullptr; }
+    const size_t ns = pixels * (size_t)std::max(slots, 1);
+    auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+    size_t off[11], total = 0;
+    const size_t sz[11] = {pixels * 4, pixels * 4, pixels * 4, pixels * 16, ns * 16, ns, ns * 16, ns * 16, ns * 4, 16,
+                           pixels * 16};
+    for (int k = 0; k < 11; ++k) { off[k] = total; total += al(sz[k]); }
+    HIP_TRY(hipMalloc(&s->wave_mem, total));
+    char* b = (char*)s->wave_mem;
+    rtg::WaveBufs& W = s->wave;
+    W.hit_t = (float*)(b + off[0]); W.hit_obj = (int*)(b + off[1]); W.hit_face = (int*)(b + off[2]);
+    W.base = (float4*)(b + off[3]); W.term = (float4*)(b + off[4]); W.occ = (unsigned char*)(b + off[5]);
+    W.q_o = (float4*)(b + off[6]); W.q_d = (float4*)(b + off[7]); W.q_slot = (int*)(b + off[8]);
+    W.q_count = (int*)(b + off[9]); W.accum = (float4*)(b + off[10]);
+    s->wave_pixels = pixels;
+    s->wave_slots = slots;
+    return RTG_OK;
+}
+
+static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& C, const rtg::RenderParams& P,
+                  float* d_hdr, uint8_t* d_ldr, float* d_accum, hipStream_t stream) {
+    const bool stats = (o->flags & RTG_RENDER_COUNT_STATS) != 0;
+    if (s->wave_ok && !(o->flags & RTG_RENDER_FUSED)) {
+        const size_t rows = (size_t)(P.row_end - P.row_begin);
+        int rc = ensure_wave(s, rows * C.width, s->num_slots);
+        if (rc) return rc;
+        rtg::WaveBufs W = s->wave;
+        W.num_slots = s->num_slots;
+        W.pixel_base = P.row_begin * C.width;
+        if (P.accum_only) W.accum = (float4*)d_accum;
+        else if (C.spp > 1) {   // internal accumulator indexed by absolute pixel
+            size_t need = (size_t)C.width * C.height;
+            if (need > s->wave_pixels) {
+                int rc2 = ensure_wave(s, need, s->num_slots);
+                if (rc2) return rc2;
+                W = s->wave;
+                W.num_slots = s->num_slots;
+                W.pixel_base = P.row_begin * C.width;
+            }
+        }
+        HIP_TRY(rtg::launch_wave(s->ds, C, P, W, d_hdr, d_ldr, s->counters.p, stats, stream));
+        return RTG_OK;
+    }
+    HIP_TRY(rtg::launch_mega(s->ds, C, P, d_hdr, d_ldr, d_accum, s->counters.p, stats, stream));
+    return RTG_OK;
+}
+
 int rtg_render_device(rtg_scene* s, const rtg_render_opts* o, float* d_hdr, uint8_t* d_ldr, float* d_accum,
                       void* stream) {
     rtg::DevCamera C;
@@ -424,9 +500,7 @@ int rtg_render_device(rtg_scene* s, const rtg_render_opts* o, float* d_hdr, uint
     if (rc) return rc;
     if (P.accum_only && !d_accum) return set_err(RTG_ERR_INVALID, "RTG_RENDER_ACCUM_ONLY needs an accumulation buffer");
     HIP_TRY(hipSetDevice(s->device));
-    HIP_TRY(rtg::launch_render(s->ds, C, P, d_hdr, d_ldr, d_accum, s->counters.p, (o->flags & RTG_RENDER_COUNT_STATS) != 0,
-                               (hipStream_t)stream));
-    return RTG_OK;
+    return launch(s, o, C, P, d_hdr, d_ldr, d_accum, (hipStream_t)stream);
 }
 
 int rtg_render(rtg_scene* s, const rtg_render_opts* o, float* hdr_rgb, uint8_t* ldr_rgb) {
@@ -447,8 +521,8 @@ int rtg_render(rtg_scene* s, const rtg_render_opts* o, float* hdr_rgb, uint8_t* 
     }
     HIP_TRY(hipMemset(s->d_hdr, 0, pixels * 3 * sizeof(float)));
     HIP_TRY(hipMemset(s->d_ldr, 0, pixels * 3));
-    HIP_TRY(rtg::launch_render(s->ds, C, P, s->d_hdr, s->d_ldr, nullptr, s->counters.p,
-                               (o->flags & RTG_RENDER_COUNT_STATS) != 0, nullptr));
+    rc = launch(s, o, C, P, s->d_hdr, s->d_ldr, nullptr, nullptr);
+    if (rc) return rc;
     HIP_TRY(hipDeviceSynchronize());
     // rows outside [row_begin, row_end) are left untouched in the caller's buffers
     const size_t off = (size_t)P.row_begin * C.width * 3, n = (size_t)(P.row_end - P.row_begin) * C.width * 3;
@@ -486,6 +560,8 @@ int rtg_scene_stats(rtg_scene* s, rtg_stats* out) {
     out->tri_tests = c.tri_tests;
     out->sphere_tests = c.sphere_tests;
     out->object_tests = c.object_tests;
+    out->shadow_node_visits = c.shadow_node_visits;
+    out->shadow_tri_tests = c.shadow_tri_tests;
     out->pad0 = 0;
     return RTG_OK;
 }

@@ -1,16 +1,16 @@
-// gfx950 render path: camera rays, threaded BVH traversal, Cramer's-rule triangle
-// and analytic sphere tests, Whitted shading with the five BRDFs, shadow rays, and
-// mirror / dielectric / conductor secondaries.
+// Device code shared by the render kernels (rtg_mega.hip, rtg_wave.hip): camera rays,
+// threaded BVH traversal, Cramer's-rule triangle and analytic sphere tests, textures,
+// the five BRDFs, Shade, direct lighting and shadow rays.
 //
 // Numerics: this file is compiled with -ffp-contract=off and IEEE div/sqrt, and every
 // expression keeps the reference's association and float/double choices, so the
 // only differences from the CPU path are the last-ulp results of transcendental
 // library calls (powf, acosf, expf, atan2f, double pow/cos).
+#pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
 #include "rtg_device.hpp"
-#include "rtg_kernels.hpp"
 
 namespace rtg {
 
@@ -81,12 +81,16 @@ enum { RP_MOTION = 1, RP_DOF = 2, RP_JITTER = 3, RP_AREA = 4, RP_ENV = 5, RP_ROU
 // Counters
 // ---------------------------------------------------------------------------
 template <bool STATS> struct Cnt {
-    DEV void node() {} DEV void tri() {} DEV void sph() {} DEV void obj() {}
+    template <bool ANY> DEV void node() {}
+    template <bool ANY> DEV void tri() {}
+    DEV void sph() {} DEV void obj() {}
     DEV void cam() {} DEV void sec() {} DEV void shd() {}
 };
 template <> struct Cnt<true> {
-    uint32_t nodes = 0, tris = 0, sphs = 0, objs = 0, cams = 0, secs = 0, shds = 0;
-    DEV void node() { ++nodes; } DEV void tri() { ++tris; } DEV void sph() { ++sphs; } DEV void obj() { ++objs; }
+    uint32_t nodes = 0, tris = 0, sphs = 0, objs = 0, cams = 0, secs = 0, shds = 0, snodes = 0, stris = 0;
+    template <bool ANY> DEV void node() { if (ANY) ++snodes; else ++nodes; }
+    template <bool ANY> DEV void tri() { if (ANY) ++stris; else ++tris; }
+    DEV void sph() { ++sphs; } DEV void obj() { ++objs; }
     DEV void cam() { ++cams; } DEV void sec() { ++secs; } DEV void shd() { ++shds; }
 };
 
@@ -150,14 +154,14 @@ DEV bool walk_bvh(const DevScene& S, int i, const int end, const Ray& r, float& 
     while (i < end) {
         const float4 a = S.node_a[i];
         const float4 b = S.node_b[i];
-        c.node();
+        c.template node<ANY>();
         const int skip = __float_as_int(b.z);
         if (box_hit(a.x, a.y, a.z, a.w, b.x, b.y, r, minT)) {
             const int first = __float_as_int(b.w);
             if (first >= 0) {
                 const int cnt = S.node_cnt[i];
                 for (int f = first; f < first + cnt; ++f) {
-                    c.tri();
+                    c.template tri<ANY>();
                     float t;
                     if (tri_test(S, f, r, minT, t)) {
                         minT = t;
@@ -205,6 +209,15 @@ DEV Ray local_ray(const DevObject& ob, const Ray& r, float mbTime) {
     if (ob.flags & OBJF_MOTION_BLUR) lr.o = add(lr.o, muls(ld3(ob.mbv), mbTime));
     return lr;
 }
+// Traversal-only variant: an exact identity transform changes at most the sign of a zero
+// component (1*x + 0*y + ...), which no box / triangle / sphere decision or t value
+// depends on, so it is skipped.  Shading (surface()) always applies the full transform.
+DEV Ray trav_ray(const DevObject& ob, const Ray& r, float mbTime) {
+    if (!(ob.flags & OBJF_IDENTITY)) return local_ray(ob, r, mbTime);
+    Ray lr = r;
+    if (ob.flags & OBJF_MOTION_BLUR) lr.o = add(lr.o, muls(ld3(ob.mbv), mbTime));
+    return lr;
+}
 
 struct Hit {
     float t;
@@ -227,7 +240,7 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
         c.obj();
         if (ob.kind == OBJ_SPHERE) {
             c.sph();
-            Ray lr = local_ray(ob, r, mbTime);
+            Ray lr = trav_ray(ob, r, mbTime);
             float t;
             if (sphere_t(ob, lr, h.t, t)) {
                 h.t = t; h.obj = k; h.face = -1; h.o = r.o;
@@ -246,7 +259,7 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
             }
         }
         // Mesh::Intersect (mesh.cpp:158-188); the mesh bbox test equals the root-node test
-        Ray lr = local_ray(ob, r, mbTime);
+        Ray lr = trav_ray(ob, r, mbTime);
         int face = -1;
         float t = h.t;
         if (walk_bvh<ANY, STATS>(S, ob.node_begin, ob.node_end, lr, t, face, limit, c)) {
@@ -344,8 +357,6 @@ DEV f3 image_rgb(const DevScene& S, const DevTexture& tx, float u, float v) {   
                    muls(texel(S, im, ip, iq + 1), w3)), muls(texel(S, im, ip + 1, iq + 1), w4));
 }
 
-__constant__ int c_perm[512];
-__constant__ float c_grad[36];
 
 DEV double perlin_f(float x) {                                          // perlinTexture.h:153-160
     x = fabsf(x);
@@ -354,15 +365,16 @@ DEV double perlin_f(float x) {                                          // perli
     float xCube = xSqr * x;
     return (-6 * xCube * xSqr) + 15 * xCube * x - 10 * xCube + 1;
 }
-DEV float gdot(int g, float x, float y, float z) {
-    return c_grad[3 * g] * x + c_grad[3 * g + 1] * y + c_grad[3 * g + 2] * z;
+DEV float gdot(const float* grad, int g, float x, float y, float z) {
+    return grad[3 * g] * x + grad[3 * g + 1] * y + grad[3 * g + 2] * z;
 }
-DEV float perlin(const DevTexture& tx, float x, float y, float z) {     // perlinTexture.h:57-123
+DEV float perlin(const DevScene& S, const DevTexture& tx, float x, float y, float z) {   // perlinTexture.h:57-123
     x *= tx.noise_scale; y *= tx.noise_scale; z *= tx.noise_scale;
     int X = (int)floorf(x), Y = (int)floorf(y), Z = (int)floorf(z);
     float dx = x - X, dy = y - Y, dz = z - Z;
     X = X & 255; Y = Y & 255; Z = Z & 255;
-    const int* p = c_perm;
+    const int* p = S.perm;
+    const float* gr = S.grad;
     int ind0 = p[X + p[Y + p[Z]]] % 12;
     int ind1 = p[X + p[Y + p[Z + 1]]] % 12;
     int ind2 = p[X + p[Y + 1 + p[Z]]] % 12;
@@ -371,9 +383,9 @@ DEV float perlin(const DevTexture& tx, float x, float y, float z) {     // perli
     int ind5 = p[X + 1 + p[Y + p[Z + 1]]] % 12;
     int ind6 = p[X + 1 + p[Y + 1 + p[Z]]] % 12;
     int ind7 = p[X + 1 + p[Y + 1 + p[Z + 1]]] % 12;
-    double c0 = gdot(ind0, dx, dy, dz), c1 = gdot(ind4, dx - 1, dy, dz), c2 = gdot(ind2, dx, dy - 1, dz),
-           c3 = gdot(ind6, dx - 1, dy - 1, dz), c4 = gdot(ind1, dx, dy, dz - 1), c5 = gdot(ind5, dx - 1, dy, dz - 1),
-           c6 = gdot(ind3, dx, dy - 1, dz - 1), c7 = gdot(ind7, dx - 1, dy - 1, dz - 1);
+    double c0 = gdot(gr, ind0, dx, dy, dz), c1 = gdot(gr, ind4, dx - 1, dy, dz), c2 = gdot(gr, ind2, dx, dy - 1, dz),
+           c3 = gdot(gr, ind6, dx - 1, dy - 1, dz), c4 = gdot(gr, ind1, dx, dy, dz - 1), c5 = gdot(gr, ind5, dx - 1, dy, dz - 1),
+           c6 = gdot(gr, ind3, dx, dy - 1, dz - 1), c7 = gdot(gr, ind7, dx - 1, dy - 1, dz - 1);
     double fdx = perlin_f(dx), fdy = perlin_f(dy), fdz = perlin_f(dz);
     double fdx1 = perlin_f(dx - 1), fdy1 = perlin_f(dy - 1), fdz1 = perlin_f(dz - 1);
     double w0 = fdx * fdy * fdz, w1 = fdx1 * fdy * fdz, w2 = fdx * fdy1 * fdz, w3 = fdx1 * fdy1 * fdz;
@@ -490,7 +502,7 @@ DEV f3 kd_coeff(const DevScene& S, const ShadeCtx& c) {                // raytra
     if (c.ob->tex_diffuse >= 0) {
         const DevTexture tx = S.textures[c.ob->tex_diffuse];
         f3 t;
-        if (tx.kind == 1) { float p = perlin(tx, c.s.p.x, c.s.p.y, c.s.p.z); t = mk(p, p, p); }
+        if (tx.kind == 1) { float p = perlin(S, tx, c.s.p.x, c.s.p.y, c.s.p.z); t = mk(p, p, p); }
         else t = divs(image_rgb(S, tx, c.s.u, c.s.v), 255.0f);
         refl = tx.blend ? divs(add(t, ld3(c.mat->diffuse)), 2.0f) : t;
     }
@@ -501,7 +513,7 @@ DEV f3 ks_coeff(const DevScene& S, const ShadeCtx& c) {                // raytra
     if (c.ob->tex_specular >= 0 && c.ob->tex_diffuse >= 0) {
         const DevTexture tx = S.textures[c.ob->tex_diffuse];
         f3 t;
-        if (tx.kind == 1) { float p = perlin(tx, c.s.p.x, c.s.p.y, c.s.p.z); t = mk(p, p, p); }
+        if (tx.kind == 1) { float p = perlin(S, tx, c.s.p.x, c.s.p.y, c.s.p.z); t = mk(p, p, p); }
         else t = divs(image_rgb(S, tx, c.s.u, c.s.v), 255.0f);
         refl = tx.blend ? divs(add(t, ld3(c.mat->diffuse)), 2.0f) : t;
     }
@@ -628,158 +640,9 @@ DEV f3 beer(float x, const float* c, f3 L0) {                          // raytra
     return mk(L0.x * expf(-c[0] * x), L0.y * expf(-c[1] * x), L0.z * expf(-c[2] * x));
 }
 
-// ---------------------------------------------------------------------------
-// Ray tree: PerformShading (raytracer.cpp:65-134) with the recursion of
-// ComputeMirrorReflection / ...Dielectric... / ...Conductor... unrolled onto an
-// explicit per-thread stack.  Children are evaluated depth-first in the
-// reference's order and combined with the reference's expressions, so the
-// summation association is identical.
-// ---------------------------------------------------------------------------
-enum { FK_MIRROR = 0, FK_CONDUCTOR = 1, FK_TIR = 2, FK_DIEL = 3 };
 
-struct Frame {
-    f3 color;          // GI + ambient + direct of this node
-    f3 coef;           // mirror reflectance
-    f3 refl;           // dielectric: finished reflected term
-    f3 reflDir;        // dielectric: reflected direction (env lookups)
-    f3 rOrigin, rDir;  // dielectric: refracted ray (unnormalised dir)
-    int kind, stage;
-    float ratio, rT;   // conductor ratio / dielectric rReflect, rRefract
-    float rMedium, roughness;
-    float selfT, selfMedium;
-    int matIdx, depth;
-    uint64_t key;
-};
-
-struct Node {          // a ray that hit something, about to be shaded
-    Ray r;
-    Hit h;
-    f3 eye;
-    float medium, mbTime;
-    int depth;
-    uint64_t key;
-};
-
-struct Child {
-    Ray r;
-    float medium;
-};
-
-// Shades `cur`.  Returns true and fills `f`/`ch` if the node spawns a child ray;
-// otherwise `out` is the node's final colour.
-template <bool STATS>
-DEV bool shade_node(const DevScene& S, const Node& cur, f3& out, Frame& f, Child& ch, Cnt<STATS>& cn) {
-    const DevObject& ob = S.objects[cur.h.obj];
-    ShadeCtx c;
-    c.ob = &ob;
-    c.mat = &S.materials[ob.material];
-    c.s = surface<STATS>(S, cur.r, cur.mbTime, cur.h, cn);
-    const DevMaterial& mat = *c.mat;
-    const f3 w_o = makeUnit(sub(cur.eye, c.s.p));
-    const float refractiveIndexOfVacuum = 1.00001;
-    const bool inside = cur.medium > refractiveIndexOfVacuum;
-    if (mat.type == 3) {                                                // Emissive
-        out = muls(muls(ld3(mat.radiance), 2.0f), (float)RT_PI);
-        return false;
-    }
-    if (ob.tex_replace_all >= 0) {
-        out = tex_rgb(S, S.textures[ob.tex_replace_all], c.s.u, c.s.v);
-        return false;
-    }
-    f3 color = mk(0, 0, 0);
-    if (!inside) {
-        color = add(color, mulv(mk(S.ambient[0], S.ambient[1], S.ambient[2]), ld3(mat.ambient)));
-        color = add(color, direct<STATS>(S, c, w_o, cur.mbTime, cur.key, cn));
-    }
-    const f3 n = c.s.n, hp = c.s.p;
-    if (mat.type == 0) {                                                // Mirror (raytracer.cpp:442-472)
-        if (cur.depth <= 0) { out = add(color, mk(0, 0, 0)); return false; }
-        f.kind = FK_MIRROR;
-        f.coef = ld3(mat.mirror);
-        ch.r.d = reflect(n, w_o, mat.roughness, cur.key, RP_ROUGH_REFL);
-        ch.r.o = add(hp, muls(n, S.eps));
-        ch.medium = 1.0f;
-    } else if (mat.type == 2) {                                         // Conductor (raytracer.cpp:208-254)
-        if (cur.depth <= 0) { out = add(color, mk(0, 0, 0)); return false; }
-        f3 d = neg(w_o);
-        float cosTheta = -dot(d, n);
-        float n2 = mat.refractive_index, k2 = mat.absorption_index;
-        float n2k2 = n2 * n2 + k2 * k2;
-        float n2cosTheta2 = 2 * n2 * cosTheta;
-        float cosThetaSqr = cosTheta * cosTheta;
-        float rs = (n2k2 - n2cosTheta2 + cosThetaSqr) / (n2k2 + n2cosTheta2 + cosThetaSqr);
-        float rp = (n2k2 * cosThetaSqr - n2cosTheta2 + 1) / (n2k2 * cosThetaSqr + n2cosTheta2 + 1);
-        float reflectRatio = (float)(0.5 * (rs + rp));
-        if (!(reflectRatio > 0.0001)) { out = add(color, mk(0, 0, 0)); return false; }
-        f.kind = FK_CONDUCTOR;
-        f.coef = ld3(mat.mirror);
-        f.ratio = reflectRatio;
-        ch.r.d = reflect(n, w_o, mat.roughness, cur.key, RP_ROUGH_REFL);
-        ch.r.o = add(hp, muls(n, S.eps));
-        ch.medium = 1.0f;
-    } else if (mat.type == 1) {                                         // Dielectric (raytracer.cpp:261-415)
-        if (cur.depth <= 0) { out = add(color, mk(0, 0, 0)); return false; }
-        float n1 = cur.medium, n2 = mat.refractive_index;
-        f3 d = neg(w_o);
-        f3 modN = n;
-        float cosTheta = -dot(d, modN);
-        bool isEntering = cosTheta > 0.f;
-        float objN = n2;
-        if (!isEntering) {
-            n1 = n2; n2 = 1.0f; objN = 1.0f;
-            cosTheta = fabsf(cosTheta);
-            modN = neg(modN);
-        }
-        float r = n1 / n2;
-        float sinThetaSqr = 1 - (cosTheta * cosTheta);
-        float criticalTerm = r * r * sinThetaSqr;
-        if (criticalTerm > 1) {
-            f.kind = FK_TIR;
-            ch.r.d = reflect(modN, w_o, mat.roughness, cur.key, RP_ROUGH_REFL);
-            ch.r.o = add(hp, muls(modN, S.eps));
-            ch.medium = cur.medium;
-        } else {
-            float cosPhi = sqrtf(1 - criticalTerm);
-            float n2cosTheta = n2 * cosTheta;
-            float n1cosPhi = n1 * cosPhi;
-            float rpar = (n2cosTheta - n1cosPhi) / (n2cosTheta + n1cosPhi);
-            float rperp = (n1 * cosTheta - n2 * cosPhi) / (n1 * cosTheta + n2 * cosPhi);
-            float rReflect = (rpar * rpar + rperp * rperp) / 2;
-            f.kind = FK_DIEL;
-            f.stage = 0;
-            f.ratio = rReflect;
-            f.rT = 1 - rReflect;
-            ch.r.d = reflect(modN, w_o, mat.roughness, cur.key, RP_ROUGH_REFL);
-            ch.r.o = add(hp, muls(modN, S.eps));
-            ch.medium = isEntering ? objN : 1.0f;
-            f.reflDir = ch.r.d;
-            f.rDir = sub(muls(add(d, muls(modN, cosTheta)), r), muls(modN, cosPhi));
-            f.rOrigin = add(hp, muls(neg(modN), S.eps));
-            f.rMedium = isEntering ? objN : 1.0f;
-            f.roughness = mat.roughness;
-        }
-    } else {
-        out = color;                                                    // Default material
-        return false;
-    }
-    f.color = color;
-    f.matIdx = ob.material;
-    f.depth = cur.depth;
-    f.key = cur.key;
-    f.selfT = cur.h.t;
-    f.selfMedium = cur.medium;
-    return true;
-}
-
-DEV f3 env_or_zero(const DevScene& S, f3 dir) {
-    return S.num_env > 0 ? env_sample(S, 0, dir) : mk(0, 0, 0);
-}
-
-// Whole ray tree of one pixel sample; returns RenderPixel's colour
-// (raytracer.cpp:38-63).
-template <int MAXD, bool STATS>
-DEV f3 render_sample(const DevScene& S, const DevCamera& C, int px, int py, uint64_t key, Cnt<STATS>& cn) {
-    // GenerateRay (raytracer.cpp:661-699) + Camera::GetImagePlanePosition (camera.cpp:74-80)
+// GenerateRay (raytracer.cpp:661-699) + Camera::GetImagePlanePosition (camera.cpp:74-80)
+DEV Ray camera_ray(const DevCamera& C, int px, int py, uint64_t key, float& mbTime) {
     const f3 q = ld3(C.q), right = ld3(C.right), up = ld3(C.up), cpos = ld3(C.pos);
     float su = (float)((px + 0.5) * (double)(C.right_ext - C.left) / C.width);
     float sv = (float)((py + 0.5) * (double)(C.top - C.bottom) / C.height);
@@ -800,108 +663,18 @@ DEV f3 render_sample(const DevScene& S, const DevCamera& C, int px, int py, uint
     } else {
         ray.d = makeUnit(sub(ipp, ray.o));
     }
-    const float mbTime = rnd(key, RP_MOTION, 0);
-    cn.cam();
-    Node cur;
-    if (!trace<false, STATS>(S, ray, mbTime, INFINITY, INFINITY, cur.h, cn)) {
-        if (S.bg_texture >= 0) {
-            float u = px / (float)C.width, v = py / (float)C.height;
-            return tex_rgb(S, S.textures[S.bg_texture], u, v);
-        }
-        if (S.num_env > 0) return env_sample(S, 0, ray.d);
-        return mk((float)S.background[0], (float)S.background[1], (float)S.background[2]);
-    }
-    cur.r = ray;
-    cur.eye = cpos;
-    cur.medium = 1.0f;
-    cur.mbTime = mbTime;
-    cur.depth = S.max_depth;
-    cur.key = key;
+    mbTime = rnd(key, RP_MOTION, 0);
+    return ray;
+}
 
-    Frame stack[MAXD > 0 ? MAXD : 1];
-    int sp = 0;
-    f3 value;
-    bool vHit;
-    float vT = 0.f, vMedium = 1.f;
-    for (;;) {
-        // ---- shade the current node; a node with children pushes a frame
-        Child ch;
-        const bool spawn = shade_node<STATS>(S, cur, value, stack[MAXD > 0 ? sp : 0], ch, cn);
-        if (MAXD > 0 && spawn) {
-            ++sp;
-            const Frame& f = stack[sp - 1];
-            cn.sec();
-            Node nx;
-            if (trace<false, STATS>(S, ch.r, cur.mbTime, INFINITY, INFINITY, nx.h, cn)) {
-                nx.r = ch.r; nx.eye = ch.r.o; nx.medium = ch.medium; nx.mbTime = cur.mbTime;
-                nx.depth = f.depth - 1;
-                nx.key = child_key(f.key, 0);
-                cur = nx;
-                continue;
-            }
-            // miss (ComputeMirrorReflection :461-470, dielectric reflected :351-356)
-            if (f.kind == FK_MIRROR) value = env_or_zero(S, ch.r.d);
-            else if (f.kind == FK_DIEL) value = env_or_zero(S, f.reflDir);
-            else value = mk(0, 0, 0);
-            vHit = false;
-        } else {
-            vHit = true; vT = cur.h.t; vMedium = cur.medium;
-        }
-        // ---- propagate finished values up the stack
-        bool descended = false;
-        while (MAXD > 0 && sp > 0) {
-            Frame& f = stack[sp - 1];
-            const DevMaterial& pm = S.materials[f.matIdx];
-            if (f.kind == FK_DIEL && f.stage == 0) {
-                f.refl = (vHit && vMedium > 1.00001f) ? beer(vT, pm.absorption, value) : value;
-                f.stage = 1;
-                // refracted ray (raytracer.cpp:362-392)
-                f3 wr = f.rDir;
-                if (f.roughness > 0.001) {
-                    f3 u, v;
-                    onb(wr, u, v);
-                    float psi1 = rnd(f.key, RP_ROUGH_REFR, 0) - 0.5f;
-                    float psi2 = rnd(f.key, RP_ROUGH_REFR, 1) - 0.5f;
-                    wr = makeUnit(add(wr, muls(add(muls(u, psi1), muls(v, psi2)), f.roughness)));
-                } else {
-                    wr = makeUnit(wr);
-                }
-                Ray rr;
-                rr.o = f.rOrigin;
-                rr.d = wr;
-                cn.sec();
-                Node nx;
-                if (trace<false, STATS>(S, rr, cur.mbTime, INFINITY, INFINITY, nx.h, cn)) {
-                    nx.r = rr; nx.eye = rr.o; nx.medium = f.rMedium; nx.mbTime = cur.mbTime;
-                    nx.depth = f.depth - 1;
-                    nx.key = child_key(f.key, 1);
-                    cur = nx;
-                    descended = true;
-                    break;
-                }
-                value = env_or_zero(S, f.reflDir);      // refracted miss uses the reflected dir (:408)
-                vHit = false;
-                continue;
-            }
-            f3 term;
-            if (f.kind == FK_MIRROR) {
-                term = mulv(f.coef, value);
-            } else if (f.kind == FK_CONDUCTOR) {
-                term = muls(vHit ? mulv(f.coef, value) : mk(0, 0, 0), f.ratio);
-            } else if (f.kind == FK_TIR) {
-                term = vHit ? ((vMedium > 1.0001) ? beer(vT, pm.absorption, value) : value) : mk(0, 0, 0);
-            } else {
-                f3 refr = (vHit && vMedium > 1.001f) ? beer(vT, pm.absorption, value) : value;
-                term = add(muls(f.refl, f.ratio), muls(refr, f.rT));
-            }
-            value = add(f.color, term);
-            vHit = true;
-            vT = f.selfT;
-            vMedium = f.selfMedium;
-            --sp;
-        }
-        if (!descended) return value;
+// PerPixel miss branch (raytracer.cpp:49-62)
+DEV f3 miss_color(const DevScene& S, const DevCamera& C, int px, int py, f3 dir) {
+    if (S.bg_texture >= 0) {
+        float u = px / (float)C.width, v = py / (float)C.height;
+        return tex_rgb(S, S.textures[S.bg_texture], u, v);
     }
+    if (S.num_env > 0) return env_sample(S, 0, dir);
+    return mk((float)S.background[0], (float)S.background[1], (float)S.background[2]);
 }
 
 // Gaussian2D (gaussian.h:3-21) with sigma = 1/6 pixel
@@ -913,113 +686,50 @@ DEV float gauss_weight(float x, float y) {
     return c1 * expf(exponent);
 }
 
+// renderThreadMain's stratified jitter (main.cpp:66-76) feeds only the Gaussian weight;
+// samples beyond nRows*nCols keep (0,0) (the reused `samples` vector, main.cpp:47).
+DEV float sample_weight(int spp, int s, uint64_t key) {
+    const int nRows = (int)sqrt((double)spp);
+    const int nCols = nRows;
+    float sx = 0.f, sy = 0.f;
+    if (s < nRows * nCols) {
+        const int row = s / nCols, col = s % nCols;
+        float psi1 = rnd(key, RP_JITTER, 0), psi2 = rnd(key, RP_JITTER, 1);
+        sx = (col + psi1) / nCols;
+        sy = (row + psi2) / nRows;
+    }
+    return gauss_weight(sx - 0.5f, sy - 0.5f);
+}
+
 // x86 cvttss2si + clamp (helperMath.cpp:140-152): out-of-range and NaN give INT_MIN -> 0
 DEV unsigned char ldr(float c) {
     int i = (c > -2147483904.0f && c < 2147483648.0f) ? (int)c : (int)0x80000000;
     return (unsigned char)(i < 0 ? 0 : (i > 255 ? 255 : i));
 }
 
-// ---------------------------------------------------------------------------
-// Kernel: one thread per pixel; a 256-thread block covers a 16x16 tile, each wave an
-// 8x8 sub-tile (coherent primary rays).  Tiles are dealt so consecutive tiles share
-// an XCD (blocks b and b+8 share one under round-robin dispatch): better L2 reuse
-// of the BVH levels near the rays' paths.
-// ---------------------------------------------------------------------------
-template <int MAXD, bool STATS>
-__global__ __launch_bounds__(256) void k_render(DevScene S, DevCamera C, RenderParams P, float* __restrict__ hdr,
-                                                unsigned char* __restrict__ ldrOut, float* __restrict__ accum,
-                                                DevCounters* __restrict__ counters) {
+// 16x16-pixel tile per 256-thread block, 8x8 per wave; tiles dealt so that consecutive
+// tiles share an XCD (blocks b and b+8 share one under round-robin dispatch).
+DEV void tile_pixel(const RenderParams& P, int& px, int& py) {
     const int b = blockIdx.x;
     const int nwg = P.num_tiles;
     const int q8 = nwg / 8, r8 = nwg % 8, xcd = b % 8;
     const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
     const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    const int px = tx * 16 + (w & 1) * 8 + (l & 7);
-    const int py = P.row_begin + ty * 16 + (w >> 1) * 8 + (l >> 3);
-    Cnt<STATS> cn;
-    if (px < C.width && py < P.row_end) {
-        const int pixel = px + py * C.width;
-        f3 color;
-        if (C.spp <= 1 && !P.accum_only) {
-            color = render_sample<MAXD, STATS>(S, C, px, py, root_key(P.seed, pixel, 0), cn);
-        } else {
-            // renderThreadMain multisampling (main.cpp:60-101): stratified jitter only
-            // feeds the Gaussian weights; every sample traces the pixel centre.
-            const int nRows = (int)sqrt((double)C.spp);
-            const int nCols = nRows;
-            f3 acc = mk(0, 0, 0);
-            float sumW = 0.0f;
-            for (int s = P.sample_begin; s < P.sample_begin + P.sample_count; ++s) {
-                const uint64_t key = root_key(P.seed, pixel, s);
-                float sx = 0.f, sy = 0.f;
-                if (s < nRows * nCols) {
-                    const int row = s / nCols, col = s % nCols;
-                    float psi1 = rnd(key, RP_JITTER, 0), psi2 = rnd(key, RP_JITTER, 1);
-                    sx = (col + psi1) / nCols;
-                    sy = (row + psi2) / nRows;
-                }
-                f3 col = render_sample<MAXD, STATS>(S, C, px, py, key, cn);
-                float gw = gauss_weight(sx - 0.5f, sy - 0.5f);
-                acc.x += col.x * gw;
-                acc.y += col.y * gw;
-                acc.z += col.z * gw;
-                sumW += gw;
-            }
-            if (P.accum_only) {
-                float4* a4 = reinterpret_cast<float4*>(accum);
-                a4[pixel] = make_float4(acc.x, acc.y, acc.z, sumW);
-                color = mk(0, 0, 0);
-            } else {
-                color = mk(acc.x / sumW, acc.y / sumW, acc.z / sumW);
-            }
-        }
-        if (!P.accum_only) {
-            const size_t idx = 3 * (size_t)pixel;
-            if (hdr) { hdr[idx] = color.x; hdr[idx + 1] = color.y; hdr[idx + 2] = color.z; }
-            if (ldrOut) { ldrOut[idx] = ldr(color.x); ldrOut[idx + 1] = ldr(color.y); ldrOut[idx + 2] = ldr(color.z); }
-        }
-    }
+    px = tx * 16 + (w & 1) * 8 + (l & 7);
+    py = P.row_begin + ty * 16 + (w >> 1) * 8 + (l >> 3);
+}
+
+template <bool STATS>
+DEV void flush_counters(Cnt<STATS>& cn, DevCounters* counters) {
     if constexpr (STATS) {
-        // one atomic per wave per counter
-        unsigned long long v[7] = {cn.cams, cn.secs, cn.shds, cn.nodes, cn.tris, cn.sphs, cn.objs};
-        for (int k = 0; k < 7; ++k) {
+        unsigned long long v[9] = {cn.cams, cn.secs, cn.shds, cn.nodes, cn.tris, cn.sphs, cn.objs, cn.snodes, cn.stris};
+        for (int k = 0; k < 9; ++k) {
             unsigned long long x = v[k];
             for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
-            if (l == 0) atomicAdd(&((unsigned long long*)counters)[k], x);
+            if ((threadIdx.x & 63) == 0 && x) atomicAdd(&((unsigned long long*)counters)[k], x);
         }
     }
-}
-
-// ---------------------------------------------------------------------------
-// Host-side launch helpers
-// ---------------------------------------------------------------------------
-int upload_perlin_tables(const int* perm512, const float* grad36) {
-    if (hipMemcpyToSymbol(HIP_SYMBOL(c_perm), perm512, 512 * sizeof(int)) != hipSuccess) return -1;
-    if (hipMemcpyToSymbol(HIP_SYMBOL(c_grad), grad36, 36 * sizeof(float)) != hipSuccess) return -1;
-    return 0;
-}
-
-template <int MAXD, bool STATS>
-static hipError_t launch_t(const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr, unsigned char* l,
-                           float* accum, DevCounters* cnt, hipStream_t stream) {
-    hipLaunchKernelGGL((k_render<MAXD, STATS>), dim3(P.num_tiles), dim3(256), 0, stream, S, C, P, hdr, l, accum, cnt);
-    return hipGetLastError();
-}
-
-int max_supported_depth() { return 32; }
-
-hipError_t launch_render(const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr, unsigned char* l,
-                         float* accum, DevCounters* cnt, bool stats, hipStream_t stream) {
-    const int d = S.max_depth;
-    if (stats) {
-        if (d <= 0) return launch_t<0, true>(S, C, P, hdr, l, accum, cnt, stream);
-        if (d <= 8) return launch_t<8, true>(S, C, P, hdr, l, accum, cnt, stream);
-        return launch_t<32, true>(S, C, P, hdr, l, accum, cnt, stream);
-    }
-    if (d <= 0) return launch_t<0, false>(S, C, P, hdr, l, accum, cnt, stream);
-    if (d <= 8) return launch_t<8, false>(S, C, P, hdr, l, accum, cnt, stream);
-    return launch_t<32, false>(S, C, P, hdr, l, accum, cnt, stream);
 }
 
 }  // namespace rtg

@@ -23,7 +23,8 @@
 namespace rtg {
 
 enum { OBJ_MESH = 0, OBJ_INSTANCE = 1, OBJ_SPHERE = 2 };
-enum { OBJF_SHADOW_SKIP = 1, OBJF_NORMAL_TWICE = 2, OBJF_MOTION_BLUR = 4, OBJF_HAS_UV = 8 };
+enum { OBJF_SHADOW_SKIP = 1, OBJF_NORMAL_TWICE = 2, OBJF_MOTION_BLUR = 4, OBJF_HAS_UV = 8,
+       OBJF_IDENTITY = 16 };   // inverse transform is exactly the identity: traversal skips it
 
 struct DevObject {
     int kind, material, flags, pad0;
@@ -88,6 +89,8 @@ struct DevScene {
     const DevDirLight* __restrict__ dir_lights;
     const DevSpotLight* __restrict__ spot_lights;
     const int* __restrict__ env_images;
+    const int* __restrict__ perm;    // Perlin permutation (512) and gradients (12x3)
+    const float* __restrict__ grad;
     int num_objects, num_point, num_area, num_dir, num_spot, num_env;
     int max_depth, bg_texture;
     float eps;
@@ -111,10 +114,28 @@ struct RenderParams {
     unsigned long long seed;
 };
 
+// Wavefront pipeline buffers (rtg_wave.hip), one entry per pixel of the rendered rows
+// and one light slot per (pixel, light) in the reference's light order.
+struct WaveBufs {
+    float* __restrict__ hit_t;
+    int* __restrict__ hit_obj;
+    int* __restrict__ hit_face;
+    float4* __restrict__ base;          // rgb + flags (w): bit0 final, bit1 add a zero child term
+    float4* __restrict__ term;          // per light slot: Shade(...) of that light
+    unsigned char* __restrict__ occ;    // per light slot: 1 = in shadow
+    float4* __restrict__ q_o;           // shadow-ray queue: origin + initial minT
+    float4* __restrict__ q_d;           //                   dir + acceptance limit
+    int* __restrict__ q_slot;           //                   light slot it decides
+    int* __restrict__ q_count;
+    float4* __restrict__ accum;         // multi-sample: sum w*c, sum w
+    int num_slots;                      // lights per pixel
+    int pixel_base;                     // row_begin * width
+};
+
 // Per-launch ray/traversal counters (RTG_RENDER_COUNT_STATS).
 struct DevCounters {
     unsigned long long camera_rays, secondary_rays, shadow_rays, node_visits, tri_tests, sphere_tests,
-        object_tests, pad0;
+        object_tests, shadow_node_visits, shadow_tri_tests, pad0;
 };
 
 }  // namespace rtg

@@ -6,9 +6,12 @@
 
 namespace rtg {
 
-int upload_perlin_tables(const int* perm512, const float* grad36);
 int max_supported_depth();
-hipError_t launch_render(const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr, unsigned char* ldr,
-                         float* accum, DevCounters* counters, bool stats, hipStream_t stream);
+// fused kernel (rtg_mega.hip): any scene
+hipError_t launch_mega(const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr, unsigned char* ldr,
+                       float* accum, DevCounters* counters, bool stats, hipStream_t stream);
+// wavefront pipeline (rtg_wave.hip): scenes without secondary rays / motion blur
+hipError_t launch_wave(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W, float* hdr,
+                       unsigned char* ldr, DevCounters* counters, bool stats, hipStream_t stream);
 
 }  // namespace rtg

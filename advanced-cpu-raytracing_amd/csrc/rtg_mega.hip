@@ -1,0 +1,329 @@
+// Fused ("mega") render kernel: one thread per pixel walks the pixel's whole ray tree
+// -- PerformShading (raytracer.cpp:65-134) with the recursion of ComputeMirrorReflection /
+// ...Dielectric... / ...Conductor... unrolled onto an explicit per-thread stack.  Used for
+// scenes whose materials spawn secondary rays (and for motion blur); scenes without
+// secondary rays take the wavefront pipeline in rtg_wave.hip.
+#include "rtg_common.hpp"
+#include "rtg_kernels.hpp"
+
+namespace rtg {
+
+// ---------------------------------------------------------------------------
+// Ray tree: PerformShading (raytracer.cpp:65-134) with the recursion of
+// ComputeMirrorReflection / ...Dielectric... / ...Conductor... unrolled onto an
+// explicit per-thread stack.  Children are evaluated depth-first in the
+// reference's order and combined with the reference's expressions, so the
+// summation association is identical.
+// ---------------------------------------------------------------------------
+enum { FK_MIRROR = 0, FK_CONDUCTOR = 1, FK_TIR = 2, FK_DIEL = 3 };
+
+struct Frame {
+    f3 color;          // GI + ambient + direct of this node
+    f3 coef;           // mirror reflectance
+    f3 refl;           // dielectric: finished reflected term
+    f3 reflDir;        // dielectric: reflected direction (env lookups)
+    f3 rOrigin, rDir;  // dielectric: refracted ray (unnormalised dir)
+    int kind, stage;
+    float ratio, rT;   // conductor ratio / dielectric rReflect, rRefract
+    float rMedium, roughness;
+    float selfT, selfMedium;
+    int matIdx, depth;
+    uint64_t key;
+};
+
+struct Node {          // a ray that hit something, about to be shaded
+    Ray r;
+    Hit h;
+    f3 eye;
+    float medium, mbTime;
+    int depth;
+    uint64_t key;
+};
+
+struct Child {
+    Ray r;
+    float medium;
+};
+
+// Shades `cur`.  Returns true and fills `f`/`ch` if the node spawns a child ray;
+// otherwise `out` is the node's final colour.
+template <bool STATS>
+DEV bool shade_node(const DevScene& S, const Node& cur, f3& out, Frame& f, Child& ch, Cnt<STATS>& cn) {
+    const DevObject& ob = S.objects[cur.h.obj];
+    ShadeCtx c;
+    c.ob = &ob;
+    c.mat = &S.materials[ob.material];
+    c.s = surface<STATS>(S, cur.r, cur.mbTime, cur.h, cn);
+    const DevMaterial& mat = *c.mat;
+    const f3 w_o = makeUnit(sub(cur.eye, c.s.p));
+    const float refractiveIndexOfVacuum = 1.00001;
+    const bool inside = cur.medium > refractiveIndexOfVacuum;
+    if (mat.type == 3) {                                                // Emissive
+        out = muls(muls(ld3(mat.radiance), 2.0f), (float)RT_PI);
+        return false;
+    }
+    if (ob.tex_replace_all >= 0) {
+        out = tex_rgb(S, S.textures[ob.tex_replace_all], c.s.u, c.s.v);
+        return false;
+    }
+    f3 color = mk(0, 0, 0);
+    if (!inside) {
+        color = add(color, mulv(mk(S.ambient[0], S.ambient[1], S.ambient[2]), ld3(mat.ambient)));
+        color = add(color, direct<STATS>(S, c, w_o, cur.mbTime, cur.key, cn));
+    }
+    const f3 n = c.s.n, hp = c.s.p;
+    if (mat.type == 0) {                                                // Mirror (raytracer.cpp:442-472)
+        if (cur.depth <= 0) { out = add(color, mk(0, 0, 0)); return false; }
+        f.kind = FK_MIRROR;
+        f.coef = ld3(mat.mirror);
+        ch.r.d = reflect(n, w_o, mat.roughness, cur.key, RP_ROUGH_REFL);
+        ch.r.o = add(hp, muls(n, S.eps));
+        ch.medium = 1.0f;
+    } else if (mat.type == 2) {                                         // Conductor (raytracer.cpp:208-254)
+        if (cur.depth <= 0) { out = add(color, mk(0, 0, 0)); return false; }
+        f3 d = neg(w_o);
+        float cosTheta = -dot(d, n);
+        float n2 = mat.refractive_index, k2 = mat.absorption_index;
+        float n2k2 = n2 * n2 + k2 * k2;
+        float n2cosTheta2 = 2 * n2 * cosTheta;
+        float cosThetaSqr = cosTheta * cosTheta;
+        float rs = (n2k2 - n2cosTheta2 + cosThetaSqr) / (n2k2 + n2cosTheta2 + cosThetaSqr);
+        float rp = (n2k2 * cosThetaSqr - n2cosTheta2 + 1) / (n2k2 * cosThetaSqr + n2cosTheta2 + 1);
+        float reflectRatio = (float)(0.5 * (rs + rp));
+        if (!(reflectRatio > 0.0001)) { out = add(color, mk(0, 0, 0)); return false; }
+        f.kind = FK_CONDUCTOR;
+        f.coef = ld3(mat.mirror);
+        f.ratio = reflectRatio;
+        ch.r.d = reflect(n, w_o, mat.roughness, cur.key, RP_ROUGH_REFL);
+        ch.r.o = add(hp, muls(n, S.eps));
+        ch.medium = 1.0f;
+    } else if (mat.type == 1) {                                         // Dielectric (raytracer.cpp:261-415)
+        if (cur.depth <= 0) { out = add(color, mk(0, 0, 0)); return false; }
+        float n1 = cur.medium, n2 = mat.refractive_index;
+        f3 d = neg(w_o);
+        f3 modN = n;
+        float cosTheta = -dot(d, modN);
+        bool isEntering = cosTheta > 0.f;
+        float objN = n2;
+        if (!isEntering) {
+            n1 = n2; n2 = 1.0f; objN = 1.0f;
+            cosTheta = fabsf(cosTheta);
+            modN = neg(modN);
+        }
+        float r = n1 / n2;
+        float sinThetaSqr = 1 - (cosTheta * cosTheta);
+        float criticalTerm = r * r * sinThetaSqr;
+        if (criticalTerm > 1) {
+            f.kind = FK_TIR;
+            ch.r.d = reflect(modN, w_o, mat.roughness, cur.key, RP_ROUGH_REFL);
+            ch.r.o = add(hp, muls(modN, S.eps));
+            ch.medium = cur.medium;
+        } else {
+            float cosPhi = sqrtf(1 - criticalTerm);
+            float n2cosTheta = n2 * cosTheta;
+            float n1cosPhi = n1 * cosPhi;
+            float rpar = (n2cosTheta - n1cosPhi) / (n2cosTheta + n1cosPhi);
+            float rperp = (n1 * cosTheta - n2 * cosPhi) / (n1 * cosTheta + n2 * cosPhi);
+            float rReflect = (rpar * rpar + rperp * rperp) / 2;
+            f.kind = FK_DIEL;
+            f.stage = 0;
+            f.ratio = rReflect;
+            f.rT = 1 - rReflect;
+            ch.r.d = reflect(modN, w_o, mat.roughness, cur.key, RP_ROUGH_REFL);
+            ch.r.o = add(hp, muls(modN, S.eps));
+            ch.medium = isEntering ? objN : 1.0f;
+            f.reflDir = ch.r.d;
+            f.rDir = sub(muls(add(d, muls(modN, cosTheta)), r), muls(modN, cosPhi));
+            f.rOrigin = add(hp, muls(neg(modN), S.eps));
+            f.rMedium = isEntering ? objN : 1.0f;
+            f.roughness = mat.roughness;
+        }
+    } else {
+        out = color;                                                    // Default material
+        return false;
+    }
+    f.color = color;
+    f.matIdx = ob.material;
+    f.depth = cur.depth;
+    f.key = cur.key;
+    f.selfT = cur.h.t;
+    f.selfMedium = cur.medium;
+    return true;
+}
+
+DEV f3 env_or_zero(const DevScene& S, f3 dir) {
+    return S.num_env > 0 ? env_sample(S, 0, dir) : mk(0, 0, 0);
+}
+
+// Whole ray tree of one pixel sample; returns RenderPixel's colour
+// (raytracer.cpp:38-63).
+template <int MAXD, bool STATS>
+DEV f3 render_sample(const DevScene& S, const DevCamera& C, int px, int py, uint64_t key, Cnt<STATS>& cn) {
+    float mbTime;
+    Ray ray = camera_ray(C, px, py, key, mbTime);
+    const f3 cpos = ld3(C.pos);
+    cn.cam();
+    Node cur;
+    if (!trace<false, STATS>(S, ray, mbTime, INFINITY, INFINITY, cur.h, cn)) return miss_color(S, C, px, py, ray.d);
+    cur.r = ray;
+    cur.eye = cpos;
+    cur.medium = 1.0f;
+    cur.mbTime = mbTime;
+    cur.depth = S.max_depth;
+    cur.key = key;
+
+    Frame stack[MAXD > 0 ? MAXD : 1];
+    int sp = 0;
+    f3 value;
+    bool vHit;
+    float vT = 0.f, vMedium = 1.f;
+    for (;;) {
+        // ---- shade the current node; a node with children pushes a frame
+        Child ch;
+        const bool spawn = shade_node<STATS>(S, cur, value, stack[MAXD > 0 ? sp : 0], ch, cn);
+        if (MAXD > 0 && spawn) {
+            ++sp;
+            const Frame& f = stack[sp - 1];
+            cn.sec();
+            Node nx;
+            if (trace<false, STATS>(S, ch.r, cur.mbTime, INFINITY, INFINITY, nx.h, cn)) {
+                nx.r = ch.r; nx.eye = ch.r.o; nx.medium = ch.medium; nx.mbTime = cur.mbTime;
+                nx.depth = f.depth - 1;
+                nx.key = child_key(f.key, 0);
+                cur = nx;
+                continue;
+            }
+            // miss (ComputeMirrorReflection :461-470, dielectric reflected :351-356)
+            if (f.kind == FK_MIRROR) value = env_or_zero(S, ch.r.d);
+            else if (f.kind == FK_DIEL) value = env_or_zero(S, f.reflDir);
+            else value = mk(0, 0, 0);
+            vHit = false;
+        } else {
+            vHit = true; vT = cur.h.t; vMedium = cur.medium;
+        }
+        // ---- propagate finished values up the stack
+        bool descended = false;
+        while (MAXD > 0 && sp > 0) {
+            Frame& f = stack[sp - 1];
+            const DevMaterial& pm = S.materials[f.matIdx];
+            if (f.kind == FK_DIEL && f.stage == 0) {
+                f.refl = (vHit && vMedium > 1.00001f) ? beer(vT, pm.absorption, value) : value;
+                f.stage = 1;
+                // refracted ray (raytracer.cpp:362-392)
+                f3 wr = f.rDir;
+                if (f.roughness > 0.001) {
+                    f3 u, v;
+                    onb(wr, u, v);
+                    float psi1 = rnd(f.key, RP_ROUGH_REFR, 0) - 0.5f;
+                    float psi2 = rnd(f.key, RP_ROUGH_REFR, 1) - 0.5f;
+                    wr = makeUnit(add(wr, muls(add(muls(u, psi1), muls(v, psi2)), f.roughness)));
+                } else {
+                    wr = makeUnit(wr);
+                }
+                Ray rr;
+                rr.o = f.rOrigin;
+                rr.d = wr;
+                cn.sec();
+                Node nx;
+                if (trace<false, STATS>(S, rr, cur.mbTime, INFINITY, INFINITY, nx.h, cn)) {
+                    nx.r = rr; nx.eye = rr.o; nx.medium = f.rMedium; nx.mbTime = cur.mbTime;
+                    nx.depth = f.depth - 1;
+                    nx.key = child_key(f.key, 1);
+                    cur = nx;
+                    descended = true;
+                    break;
+                }
+                value = env_or_zero(S, f.reflDir);      // refracted miss uses the reflected dir (:408)
+                vHit = false;
+                continue;
+            }
+            f3 term;
+            if (f.kind == FK_MIRROR) {
+                term = mulv(f.coef, value);
+            } else if (f.kind == FK_CONDUCTOR) {
+                term = muls(vHit ? mulv(f.coef, value) : mk(0, 0, 0), f.ratio);
+            } else if (f.kind == FK_TIR) {
+                term = vHit ? ((vMedium > 1.0001) ? beer(vT, pm.absorption, value) : value) : mk(0, 0, 0);
+            } else {
+                f3 refr = (vHit && vMedium > 1.001f) ? beer(vT, pm.absorption, value) : value;
+                term = add(muls(f.refl, f.ratio), muls(refr, f.rT));
+            }
+            value = add(f.color, term);
+            vHit = true;
+            vT = f.selfT;
+            vMedium = f.selfMedium;
+            --sp;
+        }
+        if (!descended) return value;
+    }
+}
+
+template <int MAXD, bool STATS>
+__global__ __launch_bounds__(256) void k_render(DevScene S, DevCamera C, RenderParams P, float* __restrict__ hdr,
+                                                unsigned char* __restrict__ ldrOut, float* __restrict__ accum,
+                                                DevCounters* __restrict__ counters) {
+    int px, py;
+    tile_pixel(P, px, py);
+    Cnt<STATS> cn;
+    if (px < C.width && py < P.row_end) {
+        const int pixel = px + py * C.width;
+        f3 color;
+        if (C.spp <= 1 && !P.accum_only) {
+            color = render_sample<MAXD, STATS>(S, C, px, py, root_key(P.seed, pixel, 0), cn);
+        } else {
+            // renderThreadMain multisampling (main.cpp:60-101): stratified jitter only
+            // feeds the Gaussian weights; every sample traces the pixel centre.
+            f3 acc = mk(0, 0, 0);
+            float sumW = 0.0f;
+            for (int s = P.sample_begin; s < P.sample_begin + P.sample_count; ++s) {
+                const uint64_t key = root_key(P.seed, pixel, s);
+                const float gw = sample_weight(C.spp, s, key);
+                f3 col = render_sample<MAXD, STATS>(S, C, px, py, key, cn);
+                acc.x += col.x * gw;
+                acc.y += col.y * gw;
+                acc.z += col.z * gw;
+                sumW += gw;
+            }
+            if (P.accum_only) {
+                float4* a4 = reinterpret_cast<float4*>(accum);
+                a4[pixel] = make_float4(acc.x, acc.y, acc.z, sumW);
+                color = mk(0, 0, 0);
+            } else {
+                color = mk(acc.x / sumW, acc.y / sumW, acc.z / sumW);
+            }
+        }
+        if (!P.accum_only) {
+            const size_t idx = 3 * (size_t)pixel;
+            if (hdr) { hdr[idx] = color.x; hdr[idx + 1] = color.y; hdr[idx + 2] = color.z; }
+            if (ldrOut) { ldrOut[idx] = ldr(color.x); ldrOut[idx + 1] = ldr(color.y); ldrOut[idx + 2] = ldr(color.z); }
+        }
+    }
+    flush_counters<STATS>(cn, counters);
+}
+
+// ---------------------------------------------------------------------------
+// Host-side launch helpers
+// ---------------------------------------------------------------------------
+template <int MAXD, bool STATS>
+static hipError_t launch_t(const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr, unsigned char* l,
+                           float* accum, DevCounters* cnt, hipStream_t stream) {
+    hipLaunchKernelGGL((k_render<MAXD, STATS>), dim3(P.num_tiles), dim3(256), 0, stream, S, C, P, hdr, l, accum, cnt);
+    return hipGetLastError();
+}
+
+int max_supported_depth() { return 32; }
+
+hipError_t launch_mega(const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr, unsigned char* l,
+                         float* accum, DevCounters* cnt, bool stats, hipStream_t stream) {
+    const int d = S.max_depth;
+    if (stats) {
+        if (d <= 0) return launch_t<0, true>(S, C, P, hdr, l, accum, cnt, stream);
+        if (d <= 8) return launch_t<8, true>(S, C, P, hdr, l, accum, cnt, stream);
+        return launch_t<32, true>(S, C, P, hdr, l, accum, cnt, stream);
+    }
+    if (d <= 0) return launch_t<0, false>(S, C, P, hdr, l, accum, cnt, stream);
+    if (d <= 8) return launch_t<8, false>(S, C, P, hdr, l, accum, cnt, stream);
+    return launch_t<32, false>(S, C, P, hdr, l, accum, cnt, stream);
+}
+
+}  // namespace rtg

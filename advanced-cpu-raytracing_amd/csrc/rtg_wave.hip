@@ -1,0 +1,291 @@
+// Wavefront render pipeline for scenes whose rays do not branch (no reflection /
+// refraction children, no motion blur): every camera ray is one closest-hit query, and
+// every hit spawns one shadow query per light.  Per sample pass:
+//
+//   k_primary  one thread per pixel: GenerateRay + IntersectObjects -> hit (t,obj,face)
+//              lean kernel: the traversal loop alone sets its register budget
+//   k_shade    one thread per pixel: PerformShading up to the light loop -- ambient,
+//              and for every light (reference order: point, area, env, dir, spot) the
+//              Shade() term and, where the reference casts one, a shadow ray.  Shadow
+//              rays are compacted into a dense queue with a wave ballot + mbcnt prefix
+//              sum and one atomic per wave.
+//   k_shadow   one thread per queued shadow ray: CastShadowRay as early-exit any-hit
+//   k_resolve  one thread per pixel: SampleDirectLighting's sum over unshadowed lights
+//              in light order, the PerformShading sum, LDR clamp / spp accumulation
+//
+// The float operations and their order are those of the fused kernel / the reference
+// (only unshadowed terms are summed, left to right), so both paths produce the same bits.
+#include "rtg_common.hpp"
+#include "rtg_kernels.hpp"
+
+namespace rtg {
+
+enum { BASE_FINAL = 1, BASE_ADD_ZERO = 2 };
+
+template <bool STATS>
+__global__ __launch_bounds__(256) void k_primary(const DevScene S, const DevCamera C, const RenderParams P,
+                                                 const int sample, const WaveBufs W, DevCounters* counters) {
+    int px, py;
+    tile_pixel(P, px, py);
+    Cnt<STATS> cn;
+    if (px < C.width && py < P.row_end) {
+        const int pixel = px + py * C.width;
+        const uint64_t key = root_key(P.seed, pixel, sample);
+        float mbTime;
+        Ray ray = camera_ray(C, px, py, key, mbTime);
+        cn.cam();
+        Hit h;
+        trace<false, STATS>(S, ray, mbTime, INFINITY, INFINITY, h, cn);
+        const int i = pixel - W.pixel_base;
+        W.hit_t[i] = h.t;
+        W.hit_obj[i] = h.obj;
+        W.hit_face[i] = h.face;
+    }
+    flush_counters<STATS>(cn, counters);
+}
+
+// wave-aggregated append: returns this lane's queue index (or -1)
+DEV int queue_append(bool want, int* count) {
+    const unsigned long long mask = __ballot(want);
+    if (!mask) return -1;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)mask) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(count, __popcll(mask));
+    base = __shfl(base, leader);
+    const int rank = __popcll(mask & ((1ull << lane) - 1ull));
+    return want ? base + rank : -1;
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(256) void k_shade(const DevScene S, const DevCamera C, const RenderParams P,
+                                               const int sample, const WaveBufs W, DevCounters* counters) {
+    int px, py;
+    tile_pixel(P, px, py);
+    Cnt<STATS> cn;
+    const bool valid = px < C.width && py < P.row_end;
+    const int pixel = valid ? px + py * C.width : 0;
+    const int i = pixel - W.pixel_base;
+    const uint64_t key = root_key(P.seed, pixel, sample);
+    const int obj = valid ? W.hit_obj[i] : -1;
+    // lanes that need the light loop
+    bool lit = false;
+    ShadeCtx c;
+    f3 w_o = mk(0, 0, 0);
+    if (valid) {
+        float mbTime;
+        Ray ray = camera_ray(C, px, py, key, mbTime);
+        if (obj < 0) {
+            f3 m = miss_color(S, C, px, py, ray.d);
+            W.base[i] = make_float4(m.x, m.y, m.z, __int_as_float(BASE_FINAL));
+        } else {
+            const DevObject& ob = S.objects[obj];
+            Hit h;
+            h.t = W.hit_t[i];
+            h.obj = obj;
+            h.face = W.hit_face[i];
+            h.o = ray.o;
+            c.ob = &ob;
+            c.mat = &S.materials[ob.material];
+            c.s = surface<STATS>(S, ray, mbTime, h, cn);
+            w_o = makeUnit(sub(ld3(C.pos), c.s.p));
+            const DevMaterial& mat = *c.mat;
+            if (mat.type == 3) {                                    // Emissive (raytracer.cpp:81-84)
+                f3 e = muls(muls(ld3(mat.radiance), 2.0f), (float)RT_PI);
+                W.base[i] = make_float4(e.x, e.y, e.z, __int_as_float(BASE_FINAL));
+            } else if (ob.tex_replace_all >= 0) {                   // replace_all (:87-89)
+                f3 e = tex_rgb(S, S.textures[ob.tex_replace_all], c.s.u, c.s.v);
+                W.base[i] = make_float4(e.x, e.y, e.z, __int_as_float(BASE_FINAL));
+            } else {
+                // primary rays travel in vacuum (medium 1.0): ambient + direct always apply
+                f3 color = add(mk(0, 0, 0), mulv(mk(S.ambient[0], S.ambient[1], S.ambient[2]), ld3(mat.ambient)));
+                const int flags = (mat.type == 0 || mat.type == 1 || mat.type == 2) ? BASE_ADD_ZERO : 0;
+                W.base[i] = make_float4(color.x, color.y, color.z, __int_as_float(flags));
+                lit = true;
+            }
+        }
+    }
+    // ---- lights, in SampleDirectLighting's order (raytracer.cpp:706-803)
+    int slot = i * W.num_slots;
+    const f3 p = lit ? c.s.p : mk(0, 0, 0), n = lit ? c.s.n : mk(0, 0, 1);
+    auto push = [&](bool want, f3 target_dir_or_pos, bool directional) {
+        // IsInShadow / IsInShadowDirectional shadow-ray set-up (raytracer.cpp:555-584)
+        float4 qo, qd;
+        if (want) {
+            cn.shd();
+            const f3 o = add(p, muls(n, S.eps));
+            if (directional) {
+                const f3 d = neg(target_dir_or_pos);
+                qo = make_float4(o.x, o.y, o.z, INFINITY);
+                qd = make_float4(d.x, d.y, d.z, INFINITY);
+            } else {
+                const f3 dir = sub(target_dir_or_pos, p);
+                const float lightT = len(dir);
+                const f3 d = divs(dir, lightT);
+                qo = make_float4(o.x, o.y, o.z, lightT + 0.01f);
+                qd = make_float4(d.x, d.y, d.z, lightT);
+            }
+        }
+        const int q = queue_append(want, W.q_count);
+        if (want) {
+            W.q_o[q] = qo;
+            W.q_d[q] = qd;
+            W.q_slot[q] = slot;
+            W.occ[slot] = 0;
+        }
+    };
+    auto put = [&](f3 t) { W.term[slot] = make_float4(t.x, t.y, t.z, 0.f); };
+    for (int l = 0; l < S.num_point; ++l, ++slot) {
+        const f3 lp = ld3(S.point_lights[l].pos);
+        if (lit) {
+            f3 w_i = makeUnit(sub(lp, p));
+            float dist = len(sub(lp, p));
+            put(shade(S, c, w_i, w_o, divs(ld3(S.point_lights[l].intensity), dist * dist)));
+        }
+        push(lit, lp, false);
+    }
+    for (int l = 0; l < S.num_area; ++l, ++slot) {
+        f3 sp = mk(0, 0, 0);
+        if (lit) {
+            const DevAreaLight& L = S.area_lights[l];
+            float offU = rnd(key, RP_AREA, 2 * l) - 0.5f;
+            float offV = rnd(key, RP_AREA, 2 * l + 1) - 0.5f;
+            sp = add(add(ld3(L.pos), muls(ld3(L.u), L.extent * offU)), muls(ld3(L.v), L.extent * offV));
+            f3 w_i = sub(sp, p);
+            float dist = len(w_i);
+            float dSqr = dist * dist;
+            w_i = divs(w_i, dist);
+            float lc = dot(ld3(L.normal), neg(w_i));
+            if (lc < 0) lc = dot(ld3(L.normal), w_i);
+            put(shade(S, c, w_i, w_o, muls(ld3(L.radiance), L.area * lc / dSqr)));
+        }
+        push(lit, sp, false);
+    }
+    for (int l = 0; l < S.num_env; ++l, ++slot) {
+        if (lit) {                                                   // no shadow ray (:741-755)
+            f3 sd = env_direction(n, key, l);
+            put(shade(S, c, n, w_o, env_sample(S, l, sd)));
+            W.occ[slot] = 0;
+        }
+    }
+    for (int l = 0; l < S.num_dir; ++l, ++slot) {
+        const f3 ldir = ld3(S.dir_lights[l].dir);
+        if (lit) put(shade(S, c, neg(ldir), w_o, ld3(S.dir_lights[l].radiance)));
+        push(lit, ldir, true);
+    }
+    for (int l = 0; l < S.num_spot; ++l, ++slot) {
+        const DevSpotLight& L = S.spot_lights[l];
+        const f3 lp = ld3(L.pos);
+        if (lit) {
+            f3 w_i = makeUnit(sub(lp, p));
+            float distToPoint = len(sub(p, lp));                     // spotLight.h:33-57
+            f3 toPoint = divs(sub(p, lp), distToPoint);
+            double alpha = angleBetween(ld3(L.dir), toPoint);
+            f3 E;
+            if (alpha <= 0 || alpha > (L.coverage_deg / 2.0f)) {
+                E = mk(0, 0, 0);
+            } else {
+                float distSqr = distToPoint * distToPoint;
+                E = divs(ld3(L.intensity), distSqr);
+                if (alpha > (L.falloff_deg / 2.0f)) {
+                    double cosAlpha = cos(alpha * (RT_PI / 180.0f));
+                    double sv = pow((cosAlpha - L.cos_half_coverage) / (L.cos_half_falloff - L.cos_half_coverage),
+                                    (double)4.0f);
+                    E = muls(E, (float)sv);
+                }
+            }
+            put(shade(S, c, w_i, w_o, E));
+        }
+        push(lit, lp, false);
+    }
+    flush_counters<STATS>(cn, counters);
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(256) void k_shadow(const DevScene S, const WaveBufs W, DevCounters* counters) {
+    const int q = blockIdx.x * 256 + threadIdx.x;
+    Cnt<STATS> cn;
+    if (q < *W.q_count) {
+        const float4 o = W.q_o[q], d = W.q_d[q];
+        Ray r;
+        r.o = mk(o.x, o.y, o.z);
+        r.d = mk(d.x, d.y, d.z);
+        Hit h;
+        if (trace<true, STATS>(S, r, 0.f, o.w, d.w, h, cn)) W.occ[W.q_slot[q]] = 1;
+    }
+    flush_counters<STATS>(cn, counters);
+}
+
+__global__ __launch_bounds__(256) void k_resolve(const DevCamera C, const RenderParams P, const int sample,
+                                                 const int first, const int last, const WaveBufs W,
+                                                 float* __restrict__ hdr, unsigned char* __restrict__ ldrOut,
+                                                 float4* __restrict__ accum) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int npix = (P.row_end - P.row_begin) * C.width;
+    if (i >= npix) return;
+    const int pixel = i + W.pixel_base;
+    const float4 b = W.base[i];
+    const int flags = __float_as_int(b.w);
+    f3 color = mk(b.x, b.y, b.z);
+    if (!(flags & BASE_FINAL)) {
+        f3 sum = mk(0, 0, 0);
+        const int s0 = i * W.num_slots;
+        for (int l = 0; l < W.num_slots; ++l)
+            if (!W.occ[s0 + l]) {
+                const float4 t = W.term[s0 + l];
+                sum = add(sum, mk(t.x, t.y, t.z));
+            }
+        color = add(color, sum);
+        if (flags & BASE_ADD_ZERO) color = add(color, mk(0, 0, 0));   // depth-0 mirror/dielectric/conductor
+    }
+    if (C.spp <= 1 && !P.accum_only) {
+        const size_t idx = 3 * (size_t)pixel;
+        if (hdr) { hdr[idx] = color.x; hdr[idx + 1] = color.y; hdr[idx + 2] = color.z; }
+        if (ldrOut) { ldrOut[idx] = ldr(color.x); ldrOut[idx + 1] = ldr(color.y); ldrOut[idx + 2] = ldr(color.z); }
+        return;
+    }
+    // renderThreadMain multisampling (main.cpp:80-100), one sample pass per launch
+    const float gw = sample_weight(C.spp, sample, root_key(P.seed, pixel, sample));
+    float4 a = first ? make_float4(0.f, 0.f, 0.f, 0.f) : accum[pixel];
+    a.x += color.x * gw;
+    a.y += color.y * gw;
+    a.z += color.z * gw;
+    a.w += gw;
+    accum[pixel] = a;
+    if (last && !P.accum_only) {
+        const f3 c = mk(a.x / a.w, a.y / a.w, a.z / a.w);
+        const size_t idx = 3 * (size_t)pixel;
+        if (hdr) { hdr[idx] = c.x; hdr[idx + 1] = c.y; hdr[idx + 2] = c.z; }
+        if (ldrOut) { ldrOut[idx] = ldr(c.x); ldrOut[idx + 1] = ldr(c.y); ldrOut[idx + 2] = ldr(c.z); }
+    }
+}
+
+template <bool STATS>
+static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W,
+                                float* hdr, unsigned char* l, DevCounters* cnt, hipStream_t st) {
+    const int npix = (P.row_end - P.row_begin) * C.width;
+    const int nshadow_max = npix * (S.num_point + S.num_area + S.num_dir + S.num_spot);
+    float4* accum = W.accum;
+    for (int s = P.sample_begin; s < P.sample_begin + P.sample_count; ++s) {
+        hipError_t e = hipMemsetAsync(W.q_count, 0, sizeof(int), st);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((k_primary<STATS>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
+        hipLaunchKernelGGL((k_shade<STATS>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
+        if (nshadow_max > 0)
+            hipLaunchKernelGGL((k_shadow<STATS>), dim3((nshadow_max + 255) / 256), dim3(256), 0, st, S, W, cnt);
+        const int first = s == P.sample_begin, last = s == P.sample_begin + P.sample_count - 1;
+        hipLaunchKernelGGL(k_resolve, dim3((npix + 255) / 256), dim3(256), 0, st, C, P, s, first, last, W, hdr, l,
+                           accum);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_wave(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W, float* hdr,
+                       unsigned char* l, DevCounters* cnt, bool stats, hipStream_t stream) {
+    return stats ? launch_wave_t<true>(S, C, P, W, hdr, l, cnt, stream)
+                 : launch_wave_t<false>(S, C, P, W, hdr, l, cnt, stream);
+}
+
+}  // namespace rtg

@@ -25,6 +25,7 @@ LIB_PATH = os.path.join(HERE, "librtgpu.so")
 
 RTG_RENDER_COUNT_STATS = 1
 RTG_RENDER_ACCUM_ONLY = 2
+RTG_RENDER_FUSED = 4
 
 
 class RTGError(RuntimeError):
@@ -48,7 +49,7 @@ class RenderOpts(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "camera_rays", "secondary_rays", "shadow_rays", "node_visits", "tri_tests",
-        "sphere_tests", "object_tests", "pad0")]
+        "sphere_tests", "object_tests", "shadow_node_visits", "shadow_tri_tests", "pad0")]
 
     def as_dict(self) -> dict:
         return {n: int(getattr(self, n)) for n, _ in self._fields_ if n != "pad0"}
@@ -72,6 +73,14 @@ def lib() -> ctypes.CDLL:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise RTGError(-1, f"{LIB_PATH} not built: run `make -C {HERE}` (or __graft_entry__.build())")
+    # One HIP runtime per process: torch's ROCm wheel ships its own libamdhip64.so.7.  If
+    # torch is loaded first, librtgpu's NEEDED libamdhip64.so.7 binds to that same copy
+    # (shared streams, events, allocations); loaded the other way round, two runtimes
+    # end up in the process and torch's fails to initialise.  So load torch first.
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     L = ctypes.CDLL(LIB_PATH)
     vp, i32, P = ctypes.c_void_p, ctypes.c_int32, ctypes.POINTER
     L.rtg_last_error.restype = ctypes.c_char_p

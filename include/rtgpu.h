@@ -256,8 +256,10 @@ int rtg_device_count(int32_t* count);
 
 enum rtg_render_flags {
     RTG_RENDER_COUNT_STATS = 1,   /* accumulate rtg_stats (slower kernel variant)      */
-    RTG_RENDER_ACCUM_ONLY = 2     /* write the weighted sample sum (r,g,b,w) only; used
+    RTG_RENDER_ACCUM_ONLY = 2,    /* write the weighted sample sum (r,g,b,w) only; used
                                      when samples are split across devices            */
+    RTG_RENDER_FUSED = 4          /* force the fused per-pixel kernel even where the
+                                     wavefront pipeline applies (for cross-checks)     */
 };
 
 typedef struct {
@@ -274,10 +276,12 @@ typedef struct {
     uint64_t camera_rays;         /* primary rays (one per pixel-sample)            */
     uint64_t secondary_rays;      /* reflection / refraction extend rays             */
     uint64_t shadow_rays;         /* CastShadowRay queries                           */
-    uint64_t node_visits;         /* BVH node box tests                              */
-    uint64_t tri_tests;           /* Mesh::IntersectFace calls                       */
-    uint64_t sphere_tests;        /* Sphere::Intersect calls                         */
-    uint64_t object_tests;        /* per-object bbox / transform visits              */
+    uint64_t node_visits;         /* BVH node box tests, extend rays                 */
+    uint64_t tri_tests;           /* Mesh::IntersectFace calls, extend rays          */
+    uint64_t sphere_tests;        /* Sphere::Intersect calls (all rays)              */
+    uint64_t object_tests;        /* per-object visits (all rays)                    */
+    uint64_t shadow_node_visits;  /* BVH node box tests, shadow rays (early exit)    */
+    uint64_t shadow_tri_tests;    /* triangle tests, shadow rays (early exit)        */
     uint64_t pad0;
 } rtg_stats;
 

@@ -120,6 +120,10 @@ const float kGrad[12][3] = {{1, 1, 0}, {-1, 1, 0}, {1, -1, 0}, {-1, -1, 0}, {1, 
 
 struct Counters {
     uint64_t camera = 0, secondary = 0, shadow = 0, nodes = 0, tris = 0, spheres = 0, objects = 0;
+    uint64_t snodes = 0, stris = 0;   // traversal work of shadow rays
+    bool in_shadow = false;
+    void node() { if (in_shadow) snodes++; else nodes++; }
+    void tri() { if (in_shadow) stris++; else tris++; }
 };
 
 // ---------------- ray.hpp ----------------
@@ -235,7 +239,7 @@ private:
     // ---- mesh.cpp:201-372 (normal/bump maps are not part of this restatement)
     bool IntersectFace(Ray& ray, const rtg_mesh& M, int faceIdx, const rtg_object& ob) {
         const rtg_face& face = S.faces[M.face_offset + faceIdx];
-        cnt.tris++;
+        cnt.tri();
         Vec3f v0 = V(face.v0), v1 = V(face.v1), v2 = V(face.v2);
         float matrixA[3][3] = {{v0.x - v1.x, v0.x - v2.x, ray.dir.x},
                                {v0.y - v1.y, v0.y - v2.y, ray.dir.y},
@@ -278,7 +282,7 @@ private:
     // this->bbox, which equals bvh[0].bbox) -- counted once, as the GPU walk does
     bool IntersectBVH(int node, Ray& ray, const rtg_mesh& M, const rtg_object& ob, bool count_root = true) {
         const rtg_bvh_node& n = S.nodes[M.node_offset + node];
-        if (count_root) cnt.nodes++;
+        if (count_root) cnt.node();
         if (!BoxHit(n.bmin, n.bmax, ray)) return false;
         bool hasHit = false;
         if (n.left < 0 && n.count > 0) {
@@ -300,7 +304,7 @@ private:
         ray.origin = applyT(ob.inv_transform, ray.origin, 1.0f);
         ray.dir = applyT(ob.inv_transform, ray.dir, 0.0f);
         if (ob.flags & RTG_OBJF_MOTION_BLUR) ray.origin = ray.origin + V(ob.motion_blur) * ray.motionBlurTime;
-        cnt.nodes++;
+        cnt.node();
         if (BoxHit(ob.bbox_min, ob.bbox_max, ray)) {
             bool hasHit = IntersectBVH(0, ray, M, ob, false);
             ray.origin = oc;
@@ -401,13 +405,16 @@ private:
 
     bool CastShadowRay(Ray& shadowRay, float lightSourceT) {              // raytracer.cpp:585-623
         cnt.shadow++;
+        cnt.in_shadow = true;
+        bool r = false;
         for (int i = 0; i < S.num_objects; i++) {
             const rtg_object& ob = S.objects[i];
             if (ob.kind != RTG_OBJ_SPHERE && (ob.flags & RTG_OBJF_SHADOW_SKIP)) continue;
             ObjectIntersect(shadowRay, i);
-            if (shadowRay.hitInfo.hasHit && shadowRay.hitInfo.minT < lightSourceT) return true;
+            if (shadowRay.hitInfo.hasHit && shadowRay.hitInfo.minT < lightSourceT) { r = true; break; }
         }
-        return false;
+        cnt.in_shadow = false;
+        return r;
     }
 
     bool IsInShadow(Ray& originalRay, Vec3f lightPos) {                   // raytracer.cpp:567-584
@@ -889,7 +896,8 @@ extern "C" {
 // hdr (w*h*3 floats) / ldr (w*h*3 bytes); either may be NULL.  accum (w*h*4), if
 // non-NULL, receives the per-pixel (sum w*c, sum w) of samples
 // [sample_begin, sample_begin+sample_count) instead (sample_count<0: spp).
-// `stats` (7 x uint64: camera, secondary, shadow, nodes, tris, spheres, objects) may be NULL.
+// `stats` (9 x uint64: camera, secondary, shadow, nodes, tris, spheres, objects, shadow
+// nodes, shadow tris) may be NULL.
 int oracle_render(const rtg_scene_desc* desc, int camera, int row_begin, int row_end, int sample_begin,
                   int sample_count, uint64_t seed, int threads, float* hdr, uint8_t* ldr, float* accum,
                   uint64_t* stats) {
@@ -951,10 +959,11 @@ int oracle_render(const rtg_scene_desc* desc, int camera, int row_begin, int row
         for (auto& t : th) t.join();
     }
     if (stats) {
-        std::memset(stats, 0, 7 * sizeof(uint64_t));
+        std::memset(stats, 0, 9 * sizeof(uint64_t));
         for (auto& c : counts) {
             stats[0] += c.camera; stats[1] += c.secondary; stats[2] += c.shadow; stats[3] += c.nodes;
-            stats[4] += c.tris; stats[5] += c.spheres; stats[6] += c.objects;
+            stats[4] += c.tris; stats[5] += c.spheres; stats[6] += c.objects; stats[7] += c.snodes;
+            stats[8] += c.stris;
         }
     }
     return 0;

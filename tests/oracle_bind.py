@@ -32,7 +32,7 @@ def lib():
 
 
 STAT_NAMES = ("camera_rays", "secondary_rays", "shadow_rays", "node_visits", "tri_tests", "sphere_tests",
-              "object_tests")
+              "object_tests", "shadow_node_visits", "shadow_tri_tests")
 
 
 def render(host_scene, camera=0, rows=(0, 0), seed=0x5EED, threads=None, sample_begin=0, sample_count=-1,
@@ -41,7 +41,7 @@ def render(host_scene, camera=0, rows=(0, 0), seed=0x5EED, threads=None, sample_
     c = host_scene.camera(camera)
     h, w = c["height"], c["width"]
     threads = threads or min(16, os.cpu_count() or 1)
-    st = np.zeros(7, np.uint64)
+    st = np.zeros(9, np.uint64)
     if accum:
         acc = np.zeros((h, w, 4), np.float32)
         rc = lib().oracle_render(host_scene.desc, camera, rows[0], rows[1], sample_begin, sample_count, seed,

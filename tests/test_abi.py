@@ -43,7 +43,7 @@ def test_abi_version():
 def test_struct_layouts_are_plain_c():
     # the opts/stats structs Python mirrors must match the header's sizes
     assert ctypes.sizeof(rtgpu.RenderOpts) == 32
-    assert ctypes.sizeof(rtgpu.Stats) == 64
+    assert ctypes.sizeof(rtgpu.Stats) == 80
 
 
 def test_errors_are_codes_not_crashes(tmp_path):

@@ -94,6 +94,6 @@ def test_oracle_traversal_counts_match_survey():
     hs = rtgpu.HostScene("scienceTree_diamond.xml")
     _, _, st = ob.render(hs)
     assert st["camera_rays"] == 288 * 144
-    per_ray = st["tri_tests"] / (st["camera_rays"] + st["secondary_rays"] + st["shadow_rays"])
+    per_ray = (st["tri_tests"] + st["shadow_tri_tests"]) / (st["camera_rays"] + st["secondary_rays"] + st["shadow_rays"])
     # 108023024 tests / (1036800 + 1073849 + 793976) rays at full size
     assert 30 < per_ray < 45, per_ray
