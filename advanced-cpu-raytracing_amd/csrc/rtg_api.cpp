@@ -103,7 +103,12 @@ struct rtg_scene {
     float* d_hdr = nullptr;
     unsigned char* d_ldr = nullptr;
     size_t d_pixels = 0;
+    // RTG_RENDER_TIMING events (stage k runs between ev[k] and ev[k+1])
+    hipEvent_t ev[rtg::MAX_STAGES + 1] = {};
+    int timed_stages = 0;             // stages recorded by the last timed render
     ~rtg_scene() {
+        for (auto& e : ev)
+            if (e) (void)hipEventDestroy(e);
         if (d_hdr) (void)hipFree(d_hdr);
         if (d_ldr) (void)hipFree(d_ldr);
         if (wave_mem) (void)hipFree(wave_mem);
@@ -467,6 +472,12 @@ static int ensure_wave(rtg_scene* s, size_t pixels, int slots) {
 static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& C, const rtg::RenderParams& P,
                   float* d_hdr, uint8_t* d_ldr, float* d_accum, hipStream_t stream) {
     const bool stats = (o->flags & RTG_RENDER_COUNT_STATS) != 0;
+    hipEvent_t* ev = nullptr;
+    if (o->flags & RTG_RENDER_TIMING) {
+        for (auto& e : s->ev)
+            if (!e) HIP_TRY(hipEventCreate(&e));
+        ev = s->ev;
+    }
     if (s->wave_ok && !(o->flags & RTG_RENDER_FUSED)) {
         const size_t rows = (size_t)(P.row_end - P.row_begin);
         int rc = ensure_wave(s, rows * C.width, s->num_slots);
@@ -485,10 +496,12 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
                 W.pixel_base = P.row_begin * C.width;
             }
         }
-        HIP_TRY(rtg::launch_wave(s->ds, C, P, W, d_hdr, d_ldr, s->counters.p, stats, stream));
+        HIP_TRY(rtg::launch_wave(s->ds, C, P, W, d_hdr, d_ldr, s->counters.p, stats, stream, ev));
+        if (ev) s->timed_stages = rtg::WAVE_STAGES;
         return RTG_OK;
     }
-    HIP_TRY(rtg::launch_mega(s->ds, C, P, d_hdr, d_ldr, d_accum, s->counters.p, stats, stream));
+    HIP_TRY(rtg::launch_mega(s->ds, C, P, d_hdr, d_ldr, d_accum, s->counters.p, stats, stream, ev));
+    if (ev) s->timed_stages = rtg::MEGA_STAGES;
     return RTG_OK;
 }
 
@@ -570,6 +583,25 @@ int rtg_scene_reset_stats(rtg_scene* s) {
     if (!s) return set_err(RTG_ERR_INVALID, "null argument");
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipMemset(s->counters.p, 0, sizeof(rtg::DevCounters)));
+    return RTG_OK;
+}
+
+int rtg_scene_timings(rtg_scene* s, float* ms, const char** names, int32_t cap, int32_t* count) {
+    static const char* kWave[rtg::WAVE_STAGES] = {"k_primary", "k_shade", "k_shadow", "k_resolve"};
+    static const char* kMega[rtg::MEGA_STAGES] = {"k_render"};
+    if (!s || !count) return set_err(RTG_ERR_INVALID, "null argument");
+    if (!s->timed_stages) return set_err(RTG_ERR_INVALID, "no render was issued with RTG_RENDER_TIMING");
+    HIP_TRY(hipSetDevice(s->device));
+    const int n = s->timed_stages;
+    HIP_TRY(hipEventSynchronize(s->ev[n]));
+    const char** nm = n == rtg::WAVE_STAGES ? kWave : kMega;
+    for (int k = 0; k < n && k < cap; ++k) {
+        float t = 0.f;
+        HIP_TRY(hipEventElapsedTime(&t, s->ev[k], s->ev[k + 1]));
+        if (ms) ms[k] = t;
+        if (names) names[k] = nm[k];
+    }
+    *count = n;
     return RTG_OK;
 }
 

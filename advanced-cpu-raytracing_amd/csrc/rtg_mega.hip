@@ -313,8 +313,8 @@ static hipError_t launch_t(const DevScene& S, const DevCamera& C, const RenderPa
 
 int max_supported_depth() { return 32; }
 
-hipError_t launch_mega(const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr, unsigned char* l,
-                         float* accum, DevCounters* cnt, bool stats, hipStream_t stream) {
+static hipError_t launch_any(const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr, unsigned char* l,
+                             float* accum, DevCounters* cnt, bool stats, hipStream_t stream) {
     const int d = S.max_depth;
     if (stats) {
         if (d <= 0) return launch_t<0, true>(S, C, P, hdr, l, accum, cnt, stream);
@@ -324,6 +324,14 @@ hipError_t launch_mega(const DevScene& S, const DevCamera& C, const RenderParams
     if (d <= 0) return launch_t<0, false>(S, C, P, hdr, l, accum, cnt, stream);
     if (d <= 8) return launch_t<8, false>(S, C, P, hdr, l, accum, cnt, stream);
     return launch_t<32, false>(S, C, P, hdr, l, accum, cnt, stream);
+}
+
+hipError_t launch_mega(const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr, unsigned char* l,
+                       float* accum, DevCounters* cnt, bool stats, hipStream_t stream, hipEvent_t* ev) {
+    if (ev) (void)hipEventRecord(ev[0], stream);
+    hipError_t e = launch_any(S, C, P, hdr, l, accum, cnt, stats, stream);
+    if (ev) (void)hipEventRecord(ev[1], stream);
+    return e;
 }
 
 }  // namespace rtg

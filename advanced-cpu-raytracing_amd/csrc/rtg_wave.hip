@@ -262,20 +262,26 @@ __global__ __launch_bounds__(256) void k_resolve(const DevCamera C, const Render
 
 template <bool STATS>
 static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W,
-                                float* hdr, unsigned char* l, DevCounters* cnt, hipStream_t st) {
+                                float* hdr, unsigned char* l, DevCounters* cnt, hipStream_t st, hipEvent_t* ev) {
     const int npix = (P.row_end - P.row_begin) * C.width;
     const int nshadow_max = npix * (S.num_point + S.num_area + S.num_dir + S.num_spot);
     float4* accum = W.accum;
     for (int s = P.sample_begin; s < P.sample_begin + P.sample_count; ++s) {
+        const int first = s == P.sample_begin, last = s == P.sample_begin + P.sample_count - 1;
+        hipEvent_t* e5 = last ? ev : nullptr;
         hipError_t e = hipMemsetAsync(W.q_count, 0, sizeof(int), st);
         if (e != hipSuccess) return e;
+        if (e5) (void)hipEventRecord(e5[0], st);
         hipLaunchKernelGGL((k_primary<STATS>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
+        if (e5) (void)hipEventRecord(e5[1], st);
         hipLaunchKernelGGL((k_shade<STATS>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
+        if (e5) (void)hipEventRecord(e5[2], st);
         if (nshadow_max > 0)
             hipLaunchKernelGGL((k_shadow<STATS>), dim3((nshadow_max + 255) / 256), dim3(256), 0, st, S, W, cnt);
-        const int first = s == P.sample_begin, last = s == P.sample_begin + P.sample_count - 1;
+        if (e5) (void)hipEventRecord(e5[3], st);
         hipLaunchKernelGGL(k_resolve, dim3((npix + 255) / 256), dim3(256), 0, st, C, P, s, first, last, W, hdr, l,
                            accum);
+        if (e5) (void)hipEventRecord(e5[4], st);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -283,9 +289,9 @@ static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const Ren
 }
 
 hipError_t launch_wave(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W, float* hdr,
-                       unsigned char* l, DevCounters* cnt, bool stats, hipStream_t stream) {
-    return stats ? launch_wave_t<true>(S, C, P, W, hdr, l, cnt, stream)
-                 : launch_wave_t<false>(S, C, P, W, hdr, l, cnt, stream);
+                       unsigned char* l, DevCounters* cnt, bool stats, hipStream_t stream, hipEvent_t* ev) {
+    return stats ? launch_wave_t<true>(S, C, P, W, hdr, l, cnt, stream, ev)
+                 : launch_wave_t<false>(S, C, P, W, hdr, l, cnt, stream, ev);
 }
 
 }  // namespace rtg

@@ -26,6 +26,7 @@ LIB_PATH = os.path.join(HERE, "librtgpu.so")
 RTG_RENDER_COUNT_STATS = 1
 RTG_RENDER_ACCUM_ONLY = 2
 RTG_RENDER_FUSED = 4
+RTG_RENDER_TIMING = 8
 
 
 class RTGError(RuntimeError):
@@ -60,7 +61,7 @@ EXPORTED = [
     "rtg_host_scene_load_xml", "rtg_host_scene_desc", "rtg_host_scene_free",
     "rtg_desc_camera_info", "rtg_desc_counts", "rtg_scene_create", "rtg_scene_destroy",
     "rtg_device_count", "rtg_render", "rtg_render_device", "rtg_resolve_accum",
-    "rtg_scene_stats", "rtg_scene_reset_stats", "rtg_write_png", "rtg_write_hdr",
+    "rtg_scene_stats", "rtg_scene_reset_stats", "rtg_scene_timings", "rtg_write_png", "rtg_write_hdr",
     "rtg_last_error", "rtg_abi_version",
 ]
 
@@ -101,6 +102,7 @@ def lib() -> ctypes.CDLL:
     L.rtg_resolve_accum.argtypes = [vp, i32, i32, vp, vp]
     L.rtg_scene_stats.argtypes = [vp, P(Stats)]
     L.rtg_scene_reset_stats.argtypes = [vp]
+    L.rtg_scene_timings.argtypes = [vp, P(ctypes.c_float), P(ctypes.c_char_p), i32, P(i32)]
     L.rtg_write_png.argtypes = [ctypes.c_char_p, i32, i32, vp]
     L.rtg_write_hdr.argtypes = [ctypes.c_char_p, i32, i32, vp]
     _lib = L
@@ -196,6 +198,14 @@ class DeviceScene:
 
     def reset_stats(self):
         _check(lib().rtg_scene_reset_stats(self._s))
+
+    def timings(self) -> dict:
+        """{kernel: ms} of the last render issued with RTG_RENDER_TIMING (synchronises)."""
+        ms = (ctypes.c_float * 8)()
+        names = (ctypes.c_char_p * 8)()
+        n = ctypes.c_int32()
+        _check(lib().rtg_scene_timings(self._s, ms, names, 8, ctypes.byref(n)))
+        return {names[k].decode(): float(ms[k]) for k in range(n.value)}
 
     def close(self):
         if getattr(self, "_s", None):

@@ -95,6 +95,30 @@ def measure(ds, torch, hdr, ldr, steps, warmup, seed, barrier):
     return elapsed, kern_ms
 
 
+def kernel_times(ds, torch, hdr, ldr, steps, seed):
+    """Per-kernel durations: HIP events recorded by the library around each kernel on the
+    render's stream (RTG_RENDER_TIMING), averaged over `steps` frames run after the timed
+    region."""
+    import rtgpu
+    sptr = torch.cuda.current_stream().cuda_stream
+    acc = {}
+    for _ in range(steps):
+        ds.render_device(hdr.data_ptr(), ldr.data_ptr(), sptr, seed=seed, flags=rtgpu.RTG_RENDER_TIMING)
+        for k, v in ds.timings().items():
+            acc[k] = acc.get(k, 0.0) + v
+    return {k: v / steps for k, v in acc.items()}
+
+
+def kernel_bytes(st, W, H):
+    """Algorithmic HBM bytes per launch of each kernel (32 B per node visit,
+    36 B per triangle test, 64 B per ray = ray in + hit out, 15 B per pixel written)."""
+    ext_rays = st["camera_rays"] + st["secondary_rays"]
+    ext = 32 * st["node_visits"] + 36 * st["tri_tests"] + 64 * ext_rays
+    shd = 32 * st["shadow_node_visits"] + 36 * st["shadow_tri_tests"] + 64 * st["shadow_rays"]
+    return {"k_primary": ext, "k_shadow": shd, "k_render": ext + shd + 15 * W * H,
+            "frame": ext + shd + 15 * W * H}
+
+
 def main():
     args = parse()
     import torch
@@ -145,10 +169,13 @@ def main():
             kern_ms = float(k.item())
 
         value = world * rays * args.steps / elapsed / 1e6
-        # algorithmic HBM bytes of one launch: 32 B per node visit, 36 B per
-        # triangle test, 64 B per ray (ray in + hit out), 15 B per pixel written
-        algo_bytes = 32 * st["node_visits"] + 36 * st["tri_tests"] + 64 * rays + 15 * W * H
-        achieved = algo_bytes / (kern_ms * 1e-3) / 1e9
+        ktimes = kernel_times(ds, torch, hdr, ldr, args.steps, seed)
+        kbytes = kernel_bytes(st, W, H)
+        # the dominant traversal kernel: k_primary (wavefront) or k_render (fused)
+        dom = max((k for k in ktimes if k in kbytes), key=lambda k: ktimes[k])
+        algo_bytes = kbytes[dom]
+        achieved = algo_bytes / (ktimes[dom] * 1e-3) / 1e9
+        frame_gbs = kbytes["frame"] / (kern_ms * 1e-3) / 1e9
         result = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -169,8 +196,10 @@ def main():
                 "width": W, "height": H, "spp": 1,
                 "rays_per_frame": int(rays),
                 "camera_rays": int(st["camera_rays"]), "shadow_rays": int(st["shadow_rays"]),
-                "node_visits_per_ray": round(st["node_visits"] / max(rays, 1), 2),
-                "tri_tests_per_ray": round(st["tri_tests"] / max(rays, 1), 2),
+                "node_visits_per_extend_ray": round(st["node_visits"] / max(rays - st["shadow_rays"], 1), 2),
+                "tri_tests_per_extend_ray": round(st["tri_tests"] / max(rays - st["shadow_rays"], 1), 2),
+                "shadow_node_visits_per_ray": round(st["shadow_node_visits"] / max(st["shadow_rays"], 1), 2),
+                "shadow_tri_tests_per_ray": round(st["shadow_tri_tests"] / max(st["shadow_rays"], 1), 2),
                 "parallelism": f"sample-parallel x{world} (rank r traces sample pass r)",
             },
             "roofline": {
@@ -180,9 +209,13 @@ def main():
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
                 "traffic": None,
-                "kernel": "k_render",
-                "kernel_ms": round(kern_ms, 4),
+                "kernel": dom,
+                "kernel_ms": round(ktimes[dom], 4),
                 "algo_bytes_per_launch": int(algo_bytes),
+                "kernels_ms": {k: round(v, 4) for k, v in ktimes.items()},
+                "frame_ms": round(kern_ms, 4),
+                "frame_algo_bytes": int(kbytes["frame"]),
+                "frame_frac": round(frame_gbs / HBM_PEAK_GBS, 4),
             },
             "cpu_baseline": None,
         }

@@ -258,8 +258,10 @@ enum rtg_render_flags {
     RTG_RENDER_COUNT_STATS = 1,   /* accumulate rtg_stats (slower kernel variant)      */
     RTG_RENDER_ACCUM_ONLY = 2,    /* write the weighted sample sum (r,g,b,w) only; used
                                      when samples are split across devices            */
-    RTG_RENDER_FUSED = 4          /* force the fused per-pixel kernel even where the
+    RTG_RENDER_FUSED = 4,         /* force the fused per-pixel kernel even where the
                                      wavefront pipeline applies (for cross-checks)     */
+    RTG_RENDER_TIMING = 8         /* record HIP events around every kernel of the
+                                     render (last sample pass); see rtg_scene_timings */
 };
 
 typedef struct {
@@ -306,6 +308,12 @@ int rtg_resolve_accum(const float* accum, int32_t width, int32_t height, float* 
 /* Stats of the last RTG_RENDER_COUNT_STATS render (synchronises). */
 int rtg_scene_stats(rtg_scene* scene, rtg_stats* out);
 int rtg_scene_reset_stats(rtg_scene* scene);
+
+/* Kernel durations (ms, HIP events on the render's stream) of the last render issued
+ * with RTG_RENDER_TIMING, for its last sample pass; synchronises on that render.
+ * Wavefront pipeline: names "k_primary", "k_shade", "k_shadow", "k_resolve"; fused
+ * kernel: "k_render".  Writes up to `cap` entries; *count = number of stages. */
+int rtg_scene_timings(rtg_scene* scene, float* ms, const char** names, int32_t cap, int32_t* count);
 
 /* ------------------------------------------------------------------------- */
 /* Output (main.cpp:187-195)                                                  */
