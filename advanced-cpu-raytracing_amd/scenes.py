@@ -153,3 +153,16 @@ def with_resolution(src_xml: str, dst_xml: str, width: int, height: int, spp: in
     with open(dst_xml, "w") as f:
         f.write(s)
     return dst_xml
+
+
+def with_depth(src_xml: str, dst_xml: str, depth: int) -> str:
+    """Copy a scene with a different <MaxRecursionDepth> (0 = no ray-tree children)."""
+    import re
+    s = open(src_xml).read()
+    if "<MaxRecursionDepth>" in s:
+        s = re.sub(r"<MaxRecursionDepth>[^<]*</MaxRecursionDepth>", f"<MaxRecursionDepth>{depth}</MaxRecursionDepth>", s)
+    else:
+        s = s.replace("<Scene>", f"<Scene>\n    <MaxRecursionDepth>{depth}</MaxRecursionDepth>", 1)
+    with open(dst_xml, "w") as f:
+        f.write(s)
+    return dst_xml

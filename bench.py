@@ -109,6 +109,18 @@ def kernel_times(ds, torch, hdr, ldr, steps, seed):
     return {k: v / steps for k, v in acc.items()}
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/*_pmc.json, made by tools/pmc_summary.py from separate rocprofv3 --pmc
+    FETCH_SIZE / WRITE_SIZE passes of this bench); None when absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
+    if not files:
+        return None, None
+    k = json.load(open(files[-1]))["kernels"].get(kernel + "<false>")
+    return (k["traffic_bytes"] if k else None), os.path.basename(files[-1])
+
+
 def kernel_bytes(st, W, H):
     """Algorithmic HBM bytes per launch of each kernel (32 B per node visit,
     36 B per triangle test, 64 B per ray = ray in + hit out, 15 B per pixel written)."""
@@ -176,6 +188,7 @@ def main():
         algo_bytes = kbytes[dom]
         achieved = algo_bytes / (ktimes[dom] * 1e-3) / 1e9
         frame_gbs = kbytes["frame"] / (kern_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(dom)
         result = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -208,7 +221,8 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": None,
+                "traffic": traffic,
+                "traffic_source": traffic_src,
                 "kernel": dom,
                 "kernel_ms": round(ktimes[dom], 4),
                 "algo_bytes_per_launch": int(algo_bytes),
