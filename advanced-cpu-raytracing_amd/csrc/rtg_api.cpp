@@ -8,6 +8,8 @@
 #include <memory>
 #include <string>
 #include <vector>
+#include <tuple>
+#include <cstdlib>
 
 #include "host_assets.hpp"
 #include "host_scene.hpp"
@@ -59,6 +61,7 @@ struct DevBuf {
     size_t n = 0;
     ~DevBuf() { if (p) (void)hipFree(p); }
     hipError_t upload(const std::vector<T>& v) {
+        if (p) { (void)hipFree(p); p = nullptr; }   // hipFree waits for the device
         n = v.size();
         if (n == 0) return hipSuccess;
         hipError_t e = hipMalloc(&p, n * sizeof(T));
@@ -76,8 +79,9 @@ struct rtg_scene {
     rtg::DevScene ds;
     std::vector<rtg_camera> cameras;
     int max_depth = 0;
-    DevBuf<float4> node_a, node_b, tri_v0, tri_e1, tri_e2, face_n;
-    DevBuf<int> node_cnt, env_images;
+    DevBuf<float4> nodes, tris, face_n;
+    DevBuf<int2> node_ext;
+    DevBuf<int> env_images;
     DevBuf<float2> face_uv;
     DevBuf<rtg::DevObject> objects;
     DevBuf<rtg::DevMaterial> materials;
@@ -95,7 +99,7 @@ struct rtg_scene {
     bool wave_ok = false;             // scene renders on the wavefront pipeline
     int num_slots = 0;                // lights per pixel (wavefront light slots)
     // wavefront buffers, grown on demand
-    size_t wave_pixels = 0;
+    size_t wave_pixels = 0, wave_tiles = 0;
     int wave_slots = 0;
     void* wave_mem = nullptr;
     rtg::WaveBufs wave;
@@ -103,6 +107,9 @@ struct rtg_scene {
     float* d_hdr = nullptr;
     unsigned char* d_ldr = nullptr;
     size_t d_pixels = 0;
+    // block -> tile table for the last (tiles_x, tiles_y)
+    DevBuf<int> tile_map;
+    int tm_x = -1, tm_y = -1, tm_mode = -1;
     // RTG_RENDER_TIMING events (stage k runs between ev[k] and ev[k+1])
     hipEvent_t ev[rtg::MAX_STAGES + 1] = {};
     int timed_stages = 0;             // stages recorded by the last timed render
@@ -196,14 +203,14 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     sc->cameras.assign(d->cameras, d->cameras + d->num_cameras);
 
     // ---- BVH: reference topology -> pre-order with skip links (rtg_device.hpp)
-    std::vector<float4> na, nb;
-    std::vector<int> ncnt;
-    na.reserve(d->num_nodes); nb.reserve(d->num_nodes); ncnt.reserve(d->num_nodes);
+    std::vector<float4> nodes;
+    std::vector<int2> next;
+    nodes.reserve(2 * d->num_nodes); next.reserve(d->num_nodes);
     std::vector<int> meshBegin(d->num_meshes), meshEnd(d->num_meshes);
     for (int m = 0; m < d->num_meshes; ++m) {
         const rtg_mesh& M = d->meshes[m];
         const rtg_bvh_node* N = d->nodes + M.node_offset;
-        const int base = (int)na.size();
+        const int base = (int)(nodes.size() / 2);
         meshBegin[m] = base;
         // pre-order, recording each node's subtree end for the skip link
         std::vector<int> order;
@@ -226,28 +233,30 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
         for (int k : order) {
             const rtg_bvh_node& n = N[k];
             int skip = base + pos[k] + size[k];
-            int first = n.left >= 0 ? -1 : M.face_offset + n.first;
+            const int first = M.face_offset + n.first;
+            int leaf = -1;
+            if (n.left < 0) leaf = (first < (1 << 23) && n.count < 255) ? (first << 8) | n.count : rtg::LEAF_EXT;
             float4 a, b;
             a.x = n.bmin[0]; a.y = n.bmin[1]; a.z = n.bmin[2]; a.w = n.bmax[0];
             b.x = n.bmax[1]; b.y = n.bmax[2];
             std::memcpy(&b.z, &skip, 4);
-            std::memcpy(&b.w, &first, 4);
-            na.push_back(a); nb.push_back(b);
-            ncnt.push_back(n.left >= 0 ? 0 : n.count);
+            std::memcpy(&b.w, &leaf, 4);
+            nodes.push_back(a); nodes.push_back(b);
+            next.push_back(make_int2(n.left < 0 ? first : -1, n.left < 0 ? n.count : 0));
         }
-        meshEnd[m] = (int)na.size();
+        meshEnd[m] = (int)(nodes.size() / 2);
     }
 
     // ---- faces (already BVH-permuted)
-    std::vector<float4> v0(d->num_faces), e1(d->num_faces), e2(d->num_faces), fn(d->num_faces);
+    std::vector<float4> tris(3 * d->num_faces), fn(d->num_faces);
     bool anyUV = false;
     for (int m = 0; m < d->num_meshes; ++m) anyUV |= d->meshes[m].has_uv != 0;
     std::vector<float2> fuv(anyUV ? 3 * d->num_faces : 0);
     for (int64_t f = 0; f < d->num_faces; ++f) {
         const rtg_face& F = d->faces[f];
-        v0[f] = make_float4(F.v0.x, F.v0.y, F.v0.z, 0.f);
-        e1[f] = make_float4(F.v0.x - F.v1.x, F.v0.y - F.v1.y, F.v0.z - F.v1.z, 0.f);
-        e2[f] = make_float4(F.v0.x - F.v2.x, F.v0.y - F.v2.y, F.v0.z - F.v2.z, 0.f);
+        tris[3 * f] = make_float4(F.v0.x, F.v0.y, F.v0.z, 0.f);
+        tris[3 * f + 1] = make_float4(F.v0.x - F.v1.x, F.v0.y - F.v1.y, F.v0.z - F.v1.z, 0.f);
+        tris[3 * f + 2] = make_float4(F.v0.x - F.v2.x, F.v0.y - F.v2.y, F.v0.z - F.v2.z, 0.f);
         fn[f] = make_float4(F.n.x, F.n.y, F.n.z, 0.f);
         if (anyUV) {
             fuv[3 * f] = make_float2(F.uv0[0], F.uv0[1]);
@@ -374,8 +383,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
         if (envs[i] < 0 || envs[i] >= d->num_images) return set_err(RTG_ERR_INVALID, "env light %d: bad image", i);
     }
 
-    HIP_TRY(sc->node_a.upload(na)); HIP_TRY(sc->node_b.upload(nb)); HIP_TRY(sc->node_cnt.upload(ncnt));
-    HIP_TRY(sc->tri_v0.upload(v0)); HIP_TRY(sc->tri_e1.upload(e1)); HIP_TRY(sc->tri_e2.upload(e2));
+    HIP_TRY(sc->nodes.upload(nodes)); HIP_TRY(sc->node_ext.upload(next)); HIP_TRY(sc->tris.upload(tris));
     HIP_TRY(sc->face_n.upload(fn)); HIP_TRY(sc->face_uv.upload(fuv));
     HIP_TRY(sc->objects.upload(objs)); HIP_TRY(sc->materials.upload(mats)); HIP_TRY(sc->brdfs.upload(brdfs));
     HIP_TRY(sc->textures.upload(texs)); HIP_TRY(sc->images.upload(imgs)); HIP_TRY(sc->texels.upload(pool));
@@ -393,8 +401,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
 
     rtg::DevScene& S = sc->ds;
     std::memset(&S, 0, sizeof(S));
-    S.node_a = sc->node_a.p; S.node_b = sc->node_b.p; S.node_cnt = sc->node_cnt.p;
-    S.tri_v0 = sc->tri_v0.p; S.tri_e1 = sc->tri_e1.p; S.tri_e2 = sc->tri_e2.p; S.face_n = sc->face_n.p;
+    S.nodes = sc->nodes.p; S.node_ext = sc->node_ext.p; S.tris = sc->tris.p; S.face_n = sc->face_n.p;
     S.face_uv = sc->face_uv.p;
     S.objects = sc->objects.p; S.materials = sc->materials.p; S.brdfs = sc->brdfs.p;
     S.textures = sc->textures.p; S.images = sc->images.p; S.texels = sc->texels.p;
@@ -417,6 +424,55 @@ void rtg_scene_destroy(rtg_scene* s) {
     if (!s) return;
     (void)hipSetDevice(s->device);
     delete s;
+}
+
+// Block -> tile assignment.  The hardware deals workgroups to the 8 XCDs round-robin
+// (block b runs on XCD b % 8), and each XCD has its own L2.  Mode 2 (default) gives each
+// XCD whole 64x64-pixel super-tiles (4x4 tiles), dealt round-robin over the image, so an
+// XCD's blocks share BVH nodes in its L2 while every XCD sees a spread of the image
+// (traversal cost varies strongly with image position; contiguous bands would leave
+// XCDs idle).  Mode 1: one contiguous band per XCD.  Mode 0: row-major tiles.
+// RTG_TILE_MAP=<mode> overrides (experiments).
+static int tile_map_mode() {
+    static int mode = [] {
+        const char* e = std::getenv("RTG_TILE_MAP");
+        return e ? std::atoi(e) : 2;
+    }();
+    return mode;
+}
+
+static std::vector<int> build_tile_map(int tx, int ty, int mode) {
+    const int n = tx * ty;
+    std::vector<int> order(n);
+    for (int t = 0; t < n; ++t) order[t] = t;
+    if (mode == 2) {
+        const int S = 4, stx = (tx + S - 1) / S;
+        auto key = [&](int t) {
+            const int x = t % tx, y = t / tx;
+            const int st = (y / S) * stx + x / S;
+            return std::make_tuple(st % 8, st / 8, (y % S) * S + x % S);
+        };
+        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return key(a) < key(b); });
+    }
+    if (mode == 0) return order;
+    // block 8k + x (XCD x) takes the k-th tile of XCD x's contiguous share of `order`
+    std::vector<int> map(n);
+    int prefix = 0;
+    for (int x = 0; x < 8; ++x) {
+        const int cnt = (n - x + 7) / 8;
+        for (int k = 0; k < cnt; ++k) map[8 * k + x] = order[prefix + k];
+        prefix += cnt;
+    }
+    return map;
+}
+
+static int ensure_tile_map(rtg_scene* s, int tx, int ty) {
+    const int mode = tile_map_mode();
+    if (s->tm_x == tx && s->tm_y == ty && s->tm_mode == mode) return RTG_OK;
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(s->tile_map.upload(build_tile_map(tx, ty, mode)));
+    s->tm_x = tx; s->tm_y = ty; s->tm_mode = mode;
+    return RTG_OK;
 }
 
 static int prepare(rtg_scene* s, const rtg_render_opts* o, rtg::DevCamera& C, rtg::RenderParams& P) {
@@ -444,18 +500,25 @@ static int prepare(rtg_scene* s, const rtg_render_opts* o, rtg::DevCamera& C, rt
     P.tiles_y = (P.row_end - P.row_begin + 15) / 16;
     P.num_tiles = P.tiles_x * P.tiles_y;
     P.seed = o->seed;
+    int rc = ensure_tile_map(s, P.tiles_x, P.tiles_y);
+    if (rc) return rc;
+    P.tile_map = s->tile_map.p;
     return RTG_OK;
 }
 
-// Sizes the wavefront buffers for `pixels` pixels x `slots` light slots (one allocation).
-static int ensure_wave(rtg_scene* s, size_t pixels, int slots) {
-    if (s->wave_mem && s->wave_pixels >= pixels && s->wave_slots >= slots) return RTG_OK;
+// Sizes the wavefront buffers for `pixels` pixels x `slots` light slots and `tiles`
+// shade blocks (queue segments of 256 * slots entries), one allocation.
+static int ensure_wave(rtg_scene* s, size_t pixels, int slots, size_t tiles) {
+    if (s->wave_mem && s->wave_pixels >= pixels && s->wave_slots >= slots && s->wave_tiles >= tiles) return RTG_OK;
     if (s->wave_mem) { (void)hipFree(s->wave_mem); s->wave_mem = nullptr; }
+    pixels = std::max(pixels, s->wave_pixels);
+    tiles = std::max(tiles, s->wave_tiles);
     const size_t ns = pixels * (size_t)std::max(slots, 1);
+    const size_t nq = tiles * 256 * (size_t)std::max(slots, 1);
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     size_t off[11], total = 0;
-    const size_t sz[11] = {pixels * 4, pixels * 4, pixels * 4, pixels * 16, ns * 16, ns, ns * 16, ns * 16, ns * 4, 16,
-                           pixels * 16};
+    const size_t sz[11] = {pixels * 4, pixels * 4, pixels * 4, pixels * 16, ns * 16, ns, nq * 16, nq * 16, nq * 4,
+                           tiles * 4, pixels * 16};
     for (int k = 0; k < 11; ++k) { off[k] = total; total += al(sz[k]); }
     HIP_TRY(hipMalloc(&s->wave_mem, total));
     char* b = (char*)s->wave_mem;
@@ -466,6 +529,7 @@ static int ensure_wave(rtg_scene* s, size_t pixels, int slots) {
     W.q_count = (int*)(b + off[9]); W.accum = (float4*)(b + off[10]);
     s->wave_pixels = pixels;
     s->wave_slots = slots;
+    s->wave_tiles = tiles;
     return RTG_OK;
 }
 
@@ -480,7 +544,7 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
     }
     if (s->wave_ok && !(o->flags & RTG_RENDER_FUSED)) {
         const size_t rows = (size_t)(P.row_end - P.row_begin);
-        int rc = ensure_wave(s, rows * C.width, s->num_slots);
+        int rc = ensure_wave(s, rows * C.width, s->num_slots, (size_t)P.num_tiles);
         if (rc) return rc;
         rtg::WaveBufs W = s->wave;
         W.num_slots = s->num_slots;
@@ -489,7 +553,7 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
         else if (C.spp > 1) {   // internal accumulator indexed by absolute pixel
             size_t need = (size_t)C.width * C.height;
             if (need > s->wave_pixels) {
-                int rc2 = ensure_wave(s, need, s->num_slots);
+                int rc2 = ensure_wave(s, need, s->num_slots, (size_t)P.num_tiles);
                 if (rc2) return rc2;
                 W = s->wave;
                 W.num_slots = s->num_slots;

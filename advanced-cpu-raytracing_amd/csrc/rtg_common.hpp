@@ -119,6 +119,46 @@ DEV bool box_hit(float mnx, float mny, float mnz, float mxx, float mxy, float mx
     return tmax > 0 && tmax >= tmin && tmin < minT;
 }
 
+// The same predicate at a fraction of the cost.  Each slab distance (m - o) / d is
+// computed as (m - o) * rcp(d): with v_rcp_f32 (<= 1 ulp) and two roundings the result is
+// within 2^-22 |t| of the correctly rounded quotient, and min/max keep that bound.  Each
+// of the three decisions is taken from the fast values only when they are farther than
+// 4x that bound from the decision boundary; otherwise the exact division test above
+// decides.  Hence the accepted set of boxes -- and every counter -- is identical.
+// `fast` is false when a direction component is 0, subnormal or huge (rcp inexact /
+// special values): those rays always take the exact test.
+struct RayRcp {
+    float ix, iy, iz;
+    bool fast;
+};
+DEV RayRcp ray_rcp(const Ray& r) {
+    RayRcp q;
+    q.ix = __builtin_amdgcn_rcpf(r.d.x);
+    q.iy = __builtin_amdgcn_rcpf(r.d.y);
+    q.iz = __builtin_amdgcn_rcpf(r.d.z);
+    const float lo = 0x1p-60f, hi = 0x1p60f;
+    const float ax = fabsf(r.d.x), ay = fabsf(r.d.y), az = fabsf(r.d.z);
+    q.fast = ax >= lo && ax <= hi && ay >= lo && ay <= hi && az >= lo && az <= hi;
+    return q;
+}
+DEV bool box_hit_fast(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, const Ray& r,
+                      const RayRcp& q, float minT) {
+    if (q.fast) {
+        const float tx1 = (mnx - r.o.x) * q.ix, tx2 = (mxx - r.o.x) * q.ix;
+        const float ty1 = (mny - r.o.y) * q.iy, ty2 = (mxy - r.o.y) * q.iy;
+        const float tz1 = (mnz - r.o.z) * q.iz, tz2 = (mxz - r.o.z) * q.iz;
+        const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+        const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+        const float atmin = fabsf(tmin), atmax = fabsf(tmax);
+        const float slack = 0x1p-20f * (atmin + atmax) + 1e-30f;
+        // all three decisions clear of their boundaries (NaN / inf fail these tests)
+        const bool sure = atmax >= 1e-30f && atmax <= 1e30f && atmin <= 1e30f && fabsf(tmax - tmin) > slack &&
+                          (minT == INFINITY || fabsf(tmin - minT) > 0x1p-20f * atmin + 1e-30f);
+        if (sure) return tmax > 0 && tmax >= tmin && tmin < minT;
+    }
+    return box_hit(mnx, mny, mnz, mxx, mxy, mxz, r, minT);
+}
+
 // determinant (helperMath.cpp:132-138)
 DEV float det3(float m00, float m01, float m02, float m10, float m11, float m12, float m20, float m21, float m22) {
     float first = m00 * (m11 * m22 - m12 * m21);
@@ -130,7 +170,7 @@ DEV float det3(float m00, float m01, float m02, float m10, float m11, float m12,
 // Mesh::IntersectFace (mesh.cpp:201-240): Cramer's rule, early outs in the same order.
 // Returns t (or a value failing 0<t<minT) and beta/gamma.
 DEV bool tri_test(const DevScene& S, int f, const Ray& r, float minT, float& tout, float* bg = nullptr) {
-    const float4 A = S.tri_v0[f], E1 = S.tri_e1[f], E2 = S.tri_e2[f];
+    const float4 A = S.tris[3 * f], E1 = S.tris[3 * f + 1], E2 = S.tris[3 * f + 2];
     const float dx = r.d.x, dy = r.d.y, dz = r.d.z;
     float detA = det3(E1.x, E2.x, dx, E1.y, E2.y, dy, E1.z, E2.z, dz);
     if (detA == 0) return false;
@@ -145,25 +185,67 @@ DEV bool tri_test(const DevScene& S, int f, const Ray& r, float minT, float& tou
     return t > 0.0f && t < minT;
 }
 
+// tri_test for traversal: beta and gamma from one reciprocal of detA, with the decisions
+// beta<0, gamma<0 (exact signs unless a quotient underflows) and beta+gamma>1 (taken
+// only when clear of 1 by 4x the error bound) identical to the division form; t itself
+// is the correctly rounded quotient.  Falls back to tri_test when unsure.
+DEV bool tri_test_fast(const DevScene& S, int f, const Ray& r, float minT, float& tout) {
+    const float4 A = S.tris[3 * f], E1 = S.tris[3 * f + 1], E2 = S.tris[3 * f + 2];
+    const float dx = r.d.x, dy = r.d.y, dz = r.d.z;
+    const float detA = det3(E1.x, E2.x, dx, E1.y, E2.y, dy, E1.z, E2.z, dz);
+    if (detA == 0) return false;
+    const float ad = fabsf(detA);
+    if (ad >= 0x1p-100f && ad <= 0x1p100f) {
+        const float rd = __builtin_amdgcn_rcpf(detA);
+        const float sx = A.x - r.o.x, sy = A.y - r.o.y, sz = A.z - r.o.z;
+        const float nb = det3(sx, E2.x, dx, sy, E2.y, dy, sz, E2.z, dz);
+        const float beta = nb * rd;
+        const bool bsure = nb == 0.0f || fabsf(beta) > 1e-30f;
+        if (bsure) {
+            if (beta < 0) return false;
+            const float ng = det3(E1.x, sx, dx, E1.y, sy, dy, E1.z, sz, dz);
+            const float gama = ng * rd;
+            const bool gsure = ng == 0.0f || fabsf(gama) > 1e-30f;
+            if (gsure) {
+                if (gama < 0) return false;
+                const float sum = gama + beta;
+                if (fabsf(sum - 1.0f) > 0x1p-19f * sum + 0x1p-22f) {
+                    if (sum > 1) return false;
+                    float t = det3(E1.x, E2.x, sx, E1.y, E2.y, sy, E1.z, E2.z, sz) / detA;
+                    tout = t;
+                    return t > 0.0f && t < minT;
+                }
+            }
+        }
+    }
+    return tri_test(S, f, r, minT, tout);
+}
+
 // BVH::IntersectBVH (bvh.cpp:5-30) as a stackless pre-order walk (rtg_device.hpp).
 // ANY: stop at the first accepted face with t < limit (CastShadowRay semantics).
 template <bool ANY, bool STATS>
 DEV bool walk_bvh(const DevScene& S, int i, const int end, const Ray& r, float& minT, int& hitFace, float limit,
                   Cnt<STATS>& c) {
     bool hit = false;
+    const RayRcp q = ray_rcp(r);
     while (i < end) {
-        const float4 a = S.node_a[i];
-        const float4 b = S.node_b[i];
+        const float4 a = S.nodes[2 * i];
+        const float4 b = S.nodes[2 * i + 1];
         c.template node<ANY>();
         const int skip = __float_as_int(b.z);
-        if (box_hit(a.x, a.y, a.z, a.w, b.x, b.y, r, minT)) {
-            const int first = __float_as_int(b.w);
-            if (first >= 0) {
-                const int cnt = S.node_cnt[i];
+        if (box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, r, q, minT)) {
+            const int leaf = __float_as_int(b.w);
+            if (leaf >= 0) {
+                int first = leaf >> 8, cnt = leaf & 255;
+                if (leaf == LEAF_EXT) {
+                    const int2 e = S.node_ext[i];
+                    first = e.x;
+                    cnt = e.y;
+                }
                 for (int f = first; f < first + cnt; ++f) {
                     c.template tri<ANY>();
                     float t;
-                    if (tri_test(S, f, r, minT, t)) {
+                    if (tri_test_fast(S, f, r, minT, t)) {
                         minT = t;
                         hitFace = f;
                         hit = true;
@@ -710,10 +792,7 @@ DEV unsigned char ldr(float c) {
 // 16x16-pixel tile per 256-thread block, 8x8 per wave; tiles dealt so that consecutive
 // tiles share an XCD (blocks b and b+8 share one under round-robin dispatch).
 DEV void tile_pixel(const RenderParams& P, int& px, int& py) {
-    const int b = blockIdx.x;
-    const int nwg = P.num_tiles;
-    const int q8 = nwg / 8, r8 = nwg % 8, xcd = b % 8;
-    const int tile = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + b / 8;
+    const int tile = P.tile_map[blockIdx.x];
     const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     px = tx * 16 + (w & 1) * 8 + (l & 7);

@@ -1,17 +1,16 @@
 // Device-side data layout for the gfx950 render path.
 //
 // HBM layout (one replica per GPU, built by rtg_scene_create):
-//   node_a[i]  float4 {min.x, min.y, min.z, max.x}                      16 B
-//   node_b[i]  float4 {max.y, max.z, skip (int bits), first (int bits)} 16 B
-//   node_cnt[i] int  leaf face count (read only at leaves)               4 B
+//   nodes[2i]   float4 {min.x, min.y, min.z, max.x}                     32 B record,
+//   nodes[2i+1] float4 {max.y, max.z, skip (int), leaf (int)}            one cache line
 //     Nodes are the reference's BVH (mesh.cpp:23-156) re-laid in pre-order
 //     (left subtree before right) with a miss/skip link, so a stackless walk
 //     "hit -> i+1, miss or leaf done -> skip" visits boxes and faces in exactly the
-//     order of BVH::IntersectBVH's recursion (bvh.cpp:5-30).  first < 0 marks
-//     an inner node.
-//   tri_v0[f]  float4 {v0.xyz, 0}                                        16 B
-//   tri_e1[f]  float4 {v0-v1, 0}   (matrixA column 0, mesh.cpp:208-210)  16 B
-//   tri_e2[f]  float4 {v0-v2, 0}   (matrixA column 1)                    16 B
+//     order of BVH::IntersectBVH's recursion (bvh.cpp:5-30).
+//     leaf < 0: inner node; else (first << 8) | count for first < 2^23, count < 255,
+//     or LEAF_EXT with {first, count} in node_ext[i].
+//   tris[3f..3f+2] float4 {v0.xyz,0}, {v0-v1,0}, {v0-v2,0}                48 B record
+//     (matrixA columns of mesh.cpp:208-210)
 //   face_n[f]  float4 {n.xyz, 0}   (read once per hit)
 //   face_uv[f] 3 x float2 (meshes with UVs only)
 // Faces are in the BVH-permuted order, so a leaf is a contiguous, coalescable
@@ -69,13 +68,12 @@ struct DevSpotLight {
     double cos_half_coverage, cos_half_falloff;
 };
 
+enum : int { LEAF_EXT = 0x7FFFFFFF };
+
 struct DevScene {
-    const float4* __restrict__ node_a;
-    const float4* __restrict__ node_b;
-    const int* __restrict__ node_cnt;
-    const float4* __restrict__ tri_v0;
-    const float4* __restrict__ tri_e1;
-    const float4* __restrict__ tri_e2;
+    const float4* __restrict__ nodes;
+    const int2* __restrict__ node_ext;
+    const float4* __restrict__ tris;
     const float4* __restrict__ face_n;
     const float2* __restrict__ face_uv;
     const DevObject* __restrict__ objects;
@@ -112,6 +110,7 @@ struct RenderParams {
     int accum_only;
     int tiles_x, tiles_y, num_tiles;
     unsigned long long seed;
+    const int* __restrict__ tile_map;   // block -> 16x16 tile (host-built, XCD-aware)
 };
 
 // Wavefront pipeline buffers (rtg_wave.hip), one entry per pixel of the rendered rows
@@ -123,10 +122,12 @@ struct WaveBufs {
     float4* __restrict__ base;          // rgb + flags (w): bit0 final, bit1 add a zero child term
     float4* __restrict__ term;          // per light slot: Shade(...) of that light
     unsigned char* __restrict__ occ;    // per light slot: 1 = in shadow
-    float4* __restrict__ q_o;           // shadow-ray queue: origin + initial minT
-    float4* __restrict__ q_d;           //                   dir + acceptance limit
-    int* __restrict__ q_slot;           //                   light slot it decides
-    int* __restrict__ q_count;
+    // shadow-ray queue, one segment of 256 * num_slots entries per k_shade block (no
+    // global atomics: a block compacts its rays with wave ballots + one LDS counter)
+    float4* __restrict__ q_o;           // origin + initial minT
+    float4* __restrict__ q_d;           // dir + acceptance limit
+    int* __restrict__ q_slot;           // light slot it decides
+    int* __restrict__ q_count;          // per block: entries in its segment
     float4* __restrict__ accum;         // multi-sample: sum w*c, sum w
     int num_slots;                      // lights per pixel
     int pixel_base;                     // row_begin * width

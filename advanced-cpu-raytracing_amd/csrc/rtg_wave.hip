@@ -44,14 +44,15 @@ __global__ __launch_bounds__(256) void k_primary(const DevScene S, const DevCame
     flush_counters<STATS>(cn, counters);
 }
 
-// wave-aggregated append: returns this lane's queue index (or -1)
-DEV int queue_append(bool want, int* count) {
+// wave-aggregated append to the block's queue segment: ballot + mbcnt rank, one LDS
+// atomic per wave; returns this lane's index in the segment (or -1)
+DEV int queue_append(bool want, int* lds_count) {
     const unsigned long long mask = __ballot(want);
     if (!mask) return -1;
     const int lane = threadIdx.x & 63;
     const int leader = __ffsll((long long)mask) - 1;
     int base = 0;
-    if (lane == leader) base = atomicAdd(count, __popcll(mask));
+    if (lane == leader) base = atomicAdd(lds_count, __popcll(mask));
     base = __shfl(base, leader);
     const int rank = __popcll(mask & ((1ull << lane) - 1ull));
     return want ? base + rank : -1;
@@ -60,8 +61,12 @@ DEV int queue_append(bool want, int* count) {
 template <bool STATS>
 __global__ __launch_bounds__(256) void k_shade(const DevScene S, const DevCamera C, const RenderParams P,
                                                const int sample, const WaveBufs W, DevCounters* counters) {
+    __shared__ int seg_count;
+    if (threadIdx.x == 0) seg_count = 0;
+    __syncthreads();
     int px, py;
     tile_pixel(P, px, py);
+    const size_t seg = (size_t)blockIdx.x * 256 * W.num_slots;
     Cnt<STATS> cn;
     const bool valid = px < C.width && py < P.row_end;
     const int pixel = valid ? px + py * C.width : 0;
@@ -126,8 +131,9 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene S, const DevCamera
                 qd = make_float4(d.x, d.y, d.z, lightT);
             }
         }
-        const int q = queue_append(want, W.q_count);
+        const int qi = queue_append(want, &seg_count);
         if (want) {
+            const size_t q = seg + qi;
             W.q_o[q] = qo;
             W.q_d[q] = qd;
             W.q_slot[q] = slot;
@@ -198,14 +204,18 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene S, const DevCamera
         }
         push(lit, lp, false);
     }
+    __syncthreads();
+    if (threadIdx.x == 0) W.q_count[blockIdx.x] = seg_count;
     flush_counters<STATS>(cn, counters);
 }
 
 template <bool STATS>
+// grid (shade blocks, slots): block (b, c) takes entries [256c, 256c+256) of segment b
 __global__ __launch_bounds__(256) void k_shadow(const DevScene S, const WaveBufs W, DevCounters* counters) {
-    const int q = blockIdx.x * 256 + threadIdx.x;
+    const int k = blockIdx.y * 256 + threadIdx.x;
+    const size_t q = ((size_t)blockIdx.x * W.num_slots) * 256 + k;
     Cnt<STATS> cn;
-    if (q < *W.q_count) {
+    if (k < W.q_count[blockIdx.x]) {
         const float4 o = W.q_o[q], d = W.q_d[q];
         Ray r;
         r.o = mk(o.x, o.y, o.z);
@@ -264,20 +274,19 @@ template <bool STATS>
 static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W,
                                 float* hdr, unsigned char* l, DevCounters* cnt, hipStream_t st, hipEvent_t* ev) {
     const int npix = (P.row_end - P.row_begin) * C.width;
-    const int nshadow_max = npix * (S.num_point + S.num_area + S.num_dir + S.num_spot);
+    const int nshadow = S.num_point + S.num_area + S.num_dir + S.num_spot;
     float4* accum = W.accum;
     for (int s = P.sample_begin; s < P.sample_begin + P.sample_count; ++s) {
         const int first = s == P.sample_begin, last = s == P.sample_begin + P.sample_count - 1;
         hipEvent_t* e5 = last ? ev : nullptr;
-        hipError_t e = hipMemsetAsync(W.q_count, 0, sizeof(int), st);
-        if (e != hipSuccess) return e;
+        hipError_t e;
         if (e5) (void)hipEventRecord(e5[0], st);
         hipLaunchKernelGGL((k_primary<STATS>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
         if (e5) (void)hipEventRecord(e5[1], st);
         hipLaunchKernelGGL((k_shade<STATS>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
         if (e5) (void)hipEventRecord(e5[2], st);
-        if (nshadow_max > 0)
-            hipLaunchKernelGGL((k_shadow<STATS>), dim3((nshadow_max + 255) / 256), dim3(256), 0, st, S, W, cnt);
+        if (nshadow > 0)
+            hipLaunchKernelGGL((k_shadow<STATS>), dim3(P.num_tiles, nshadow), dim3(256), 0, st, S, W, cnt);
         if (e5) (void)hipEventRecord(e5[3], st);
         hipLaunchKernelGGL(k_resolve, dim3((npix + 255) / 256), dim3(256), 0, st, C, P, s, first, last, W, hdr, l,
                            accum);
