@@ -97,6 +97,7 @@ struct rtg_scene {
     DevBuf<int> perm;
     DevBuf<float> grad;
     bool wave_ok = false;             // scene renders on the wavefront pipeline
+    int feat = rtg::FEAT_ALL;         // scene feature bits (traversal specialisation)
     int num_slots = 0;                // lights per pixel (wavefront light slots)
     // wavefront buffers, grown on demand
     size_t wave_pixels = 0, wave_tiles = 0;
@@ -247,6 +248,9 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
         meshEnd[m] = (int)(nodes.size() / 2);
     }
 
+    nodes.push_back(make_float4(0.f, 0.f, 0.f, 0.f));     // pad node: walk_bvh prefetches i+1
+    nodes.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
+
     // ---- faces (already BVH-permuted)
     std::vector<float4> tris(3 * d->num_faces), fn(d->num_faces);
     bool anyUV = false;
@@ -267,6 +271,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
 
     // ---- objects
     std::vector<rtg::DevObject> objs(d->num_objects);
+    int feat = 0;
     for (int i = 0; i < d->num_objects; ++i) {
         const rtg_object& o = d->objects[i];
         rtg::DevObject& D = objs[i];
@@ -293,6 +298,9 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
             ident &= o.inv_transform[k] == ((k % 5 == 0) ? 1.0 : 0.0);
         }
         if (ident) D.flags |= rtg::OBJF_IDENTITY;
+        if (o.kind == RTG_OBJ_SPHERE) feat |= rtg::FEAT_SPHERE;
+        else if (o.kind == RTG_OBJ_INSTANCE) feat |= rtg::FEAT_INSTANCE;
+        else if (!ident || (o.flags & RTG_OBJF_MOTION_BLUR)) feat |= rtg::FEAT_XFORM;
     }
     // wavefront eligibility: no ray-tree children and no motion blur
     bool branching = false, blur = false;
@@ -301,6 +309,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
         branching |= (t == RTG_MAT_MIRROR || t == RTG_MAT_DIELECTRIC || t == RTG_MAT_CONDUCTOR);
     }
     for (int i = 0; i < d->num_objects; ++i) blur |= (d->objects[i].flags & RTG_OBJF_MOTION_BLUR) != 0;
+    sc->feat = feat;
     sc->wave_ok = !blur && (d->max_recursion_depth <= 0 || !branching);
     sc->num_slots = d->num_point_lights + d->num_area_lights + d->num_env_lights + d->num_dir_lights +
                     d->num_spot_lights;
@@ -560,7 +569,7 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
                 W.pixel_base = P.row_begin * C.width;
             }
         }
-        HIP_TRY(rtg::launch_wave(s->ds, C, P, W, d_hdr, d_ldr, s->counters.p, stats, stream, ev));
+        HIP_TRY(rtg::launch_wave(s->ds, C, P, W, d_hdr, d_ldr, s->counters.p, stats, s->feat, stream, ev));
         if (ev) s->timed_stages = rtg::WAVE_STAGES;
         return RTG_OK;
     }

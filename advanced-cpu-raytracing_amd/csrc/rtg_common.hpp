@@ -312,7 +312,9 @@ struct Hit {
 // Any hit (ANY): skip emissive meshes, true as soon as a hit with t < limit exists.
 // The ray is updated in place like the reference's: an instance with motion blur whose
 // bbox test fails leaves its offset on the ray origin (instancedMesh.cpp:18-60).
-template <bool ANY, bool STATS>
+// FEAT (scene features the caller guarantees absent when the bit is clear) lets the
+// traversal kernels drop whole code paths -- and their registers -- for plain scenes.
+template <bool ANY, bool STATS, int FEAT = FEAT_ALL>
 DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit, Hit& h, Cnt<STATS>& c) {
     h.t = minT;
     h.obj = -1;
@@ -320,7 +322,7 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
     for (int k = 0; k < S.num_objects; ++k) {
         const DevObject& ob = S.objects[k];
         c.obj();
-        if (ob.kind == OBJ_SPHERE) {
+        if ((FEAT & FEAT_SPHERE) && ob.kind == OBJ_SPHERE) {
             c.sph();
             Ray lr = trav_ray(ob, r, mbTime);
             float t;
@@ -331,7 +333,7 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
             continue;
         }
         if (ANY && (ob.flags & OBJF_SHADOW_SKIP)) continue;
-        if (ob.kind == OBJ_INSTANCE) {
+        if ((FEAT & FEAT_INSTANCE) && ob.kind == OBJ_INSTANCE) {
             // InstancedMesh::Intersect (instancedMesh.cpp:16-66): world bbox first
             Ray wr = r;
             if (ob.flags & OBJF_MOTION_BLUR) wr.o = add(wr.o, muls(ld3(ob.mbv), mbTime));
@@ -341,7 +343,7 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
             }
         }
         // Mesh::Intersect (mesh.cpp:158-188); the mesh bbox test equals the root-node test
-        Ray lr = trav_ray(ob, r, mbTime);
+        Ray lr = (FEAT & FEAT_XFORM) ? trav_ray(ob, r, mbTime) : r;
         int face = -1;
         float t = h.t;
         if (walk_bvh<ANY, STATS>(S, ob.node_begin, ob.node_end, lr, t, face, limit, c)) {

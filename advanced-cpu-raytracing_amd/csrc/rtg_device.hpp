@@ -70,6 +70,10 @@ struct DevSpotLight {
 
 enum : int { LEAF_EXT = 0x7FFFFFFF };
 
+// Scene feature bits (kernel specialisation): spheres, mesh instances, any mesh with a
+// non-identity transform or motion blur.
+enum : int { FEAT_SPHERE = 1, FEAT_INSTANCE = 2, FEAT_XFORM = 4, FEAT_ALL = 7 };
+
 struct DevScene {
     const float4* __restrict__ nodes;
     const int2* __restrict__ node_ext;

@@ -13,7 +13,8 @@ hipError_t launch_mega(const DevScene& S, const DevCamera& C, const RenderParams
                        float* accum, DevCounters* counters, bool stats, hipStream_t stream, hipEvent_t* ev);
 // wavefront pipeline (rtg_wave.hip): scenes without secondary rays / motion blur
 hipError_t launch_wave(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W, float* hdr,
-                       unsigned char* ldr, DevCounters* counters, bool stats, hipStream_t stream, hipEvent_t* ev);
+                       unsigned char* ldr, DevCounters* counters, bool stats, int feat, hipStream_t stream,
+                       hipEvent_t* ev);
 enum { WAVE_STAGES = 4, MEGA_STAGES = 1, MAX_STAGES = 4 };
 
 }  // namespace rtg

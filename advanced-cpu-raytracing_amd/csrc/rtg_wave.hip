@@ -22,7 +22,7 @@ namespace rtg {
 
 enum { BASE_FINAL = 1, BASE_ADD_ZERO = 2 };
 
-template <bool STATS>
+template <bool STATS, int FEAT>
 __global__ __launch_bounds__(256) void k_primary(const DevScene S, const DevCamera C, const RenderParams P,
                                                  const int sample, const WaveBufs W, DevCounters* counters) {
     int px, py;
@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256) void k_primary(const DevScene S, const DevCame
         Ray ray = camera_ray(C, px, py, key, mbTime);
         cn.cam();
         Hit h;
-        trace<false, STATS>(S, ray, mbTime, INFINITY, INFINITY, h, cn);
+        trace<false, STATS, FEAT>(S, ray, mbTime, INFINITY, INFINITY, h, cn);
         const int i = pixel - W.pixel_base;
         W.hit_t[i] = h.t;
         W.hit_obj[i] = h.obj;
@@ -209,7 +209,7 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene S, const DevCamera
     flush_counters<STATS>(cn, counters);
 }
 
-template <bool STATS>
+template <bool STATS, int FEAT>
 // grid (shade blocks, slots): block (b, c) takes entries [256c, 256c+256) of segment b
 __global__ __launch_bounds__(256) void k_shadow(const DevScene S, const WaveBufs W, DevCounters* counters) {
     const int k = blockIdx.y * 256 + threadIdx.x;
@@ -221,7 +221,7 @@ __global__ __launch_bounds__(256) void k_shadow(const DevScene S, const WaveBufs
         r.o = mk(o.x, o.y, o.z);
         r.d = mk(d.x, d.y, d.z);
         Hit h;
-        if (trace<true, STATS>(S, r, 0.f, o.w, d.w, h, cn)) W.occ[W.q_slot[q]] = 1;
+        if (trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn)) W.occ[W.q_slot[q]] = 1;
     }
     flush_counters<STATS>(cn, counters);
 }
@@ -270,7 +270,7 @@ __global__ __launch_bounds__(256) void k_resolve(const DevCamera C, const Render
     }
 }
 
-template <bool STATS>
+template <bool STATS, int FEAT>
 static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W,
                                 float* hdr, unsigned char* l, DevCounters* cnt, hipStream_t st, hipEvent_t* ev) {
     const int npix = (P.row_end - P.row_begin) * C.width;
@@ -281,12 +281,12 @@ static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const Ren
         hipEvent_t* e5 = last ? ev : nullptr;
         hipError_t e;
         if (e5) (void)hipEventRecord(e5[0], st);
-        hipLaunchKernelGGL((k_primary<STATS>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
+        hipLaunchKernelGGL((k_primary<STATS, FEAT>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
         if (e5) (void)hipEventRecord(e5[1], st);
         hipLaunchKernelGGL((k_shade<STATS>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
         if (e5) (void)hipEventRecord(e5[2], st);
         if (nshadow > 0)
-            hipLaunchKernelGGL((k_shadow<STATS>), dim3(P.num_tiles, nshadow), dim3(256), 0, st, S, W, cnt);
+            hipLaunchKernelGGL((k_shadow<STATS, FEAT>), dim3(P.num_tiles, nshadow), dim3(256), 0, st, S, W, cnt);
         if (e5) (void)hipEventRecord(e5[3], st);
         hipLaunchKernelGGL(k_resolve, dim3((npix + 255) / 256), dim3(256), 0, st, C, P, s, first, last, W, hdr, l,
                            accum);
@@ -298,9 +298,16 @@ static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const Ren
 }
 
 hipError_t launch_wave(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W, float* hdr,
-                       unsigned char* l, DevCounters* cnt, bool stats, hipStream_t stream, hipEvent_t* ev) {
-    return stats ? launch_wave_t<true>(S, C, P, W, hdr, l, cnt, stream, ev)
-                 : launch_wave_t<false>(S, C, P, W, hdr, l, cnt, stream, ev);
+                       unsigned char* l, DevCounters* cnt, bool stats, int feat, hipStream_t stream, hipEvent_t* ev) {
+    // traversal variants: meshes only (identity transforms) / + spheres / everything
+    if (feat == 0)
+        return stats ? launch_wave_t<true, 0>(S, C, P, W, hdr, l, cnt, stream, ev)
+                     : launch_wave_t<false, 0>(S, C, P, W, hdr, l, cnt, stream, ev);
+    if (feat == FEAT_SPHERE)
+        return stats ? launch_wave_t<true, FEAT_SPHERE>(S, C, P, W, hdr, l, cnt, stream, ev)
+                     : launch_wave_t<false, FEAT_SPHERE>(S, C, P, W, hdr, l, cnt, stream, ev);
+    return stats ? launch_wave_t<true, FEAT_ALL>(S, C, P, W, hdr, l, cnt, stream, ev)
+                 : launch_wave_t<false, FEAT_ALL>(S, C, P, W, hdr, l, cnt, stream, ev);
 }
 
 }  // namespace rtg

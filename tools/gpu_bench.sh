@@ -1,0 +1,12 @@
+#!/bin/bash
+# Parity tests + one bench line (+ optional extra bench env).  Usage: gpu_bench.sh <tag>
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+out=gpurun_out/${1:-b}
+mkdir -p $out
+timeout -k 10 600 python -m pytest tests -q -m gpu -x > $out/pytest.log 2>&1
+rc=$?; echo "pytest rc=$rc" > $out/status.txt
+if [ $rc -gt 1 ]; then exit $rc; fi
+timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline > $out/bench.log 2>&1
+rc=$?; echo "bench rc=$rc" >> $out/status.txt
+exit $rc
