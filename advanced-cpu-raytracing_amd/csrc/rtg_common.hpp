@@ -143,20 +143,22 @@ DEV RayRcp ray_rcp(const Ray& r) {
 }
 DEV bool box_hit_fast(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, const Ray& r,
                       const RayRcp& q, float minT) {
-    if (q.fast) {
-        const float tx1 = (mnx - r.o.x) * q.ix, tx2 = (mxx - r.o.x) * q.ix;
-        const float ty1 = (mny - r.o.y) * q.iy, ty2 = (mxy - r.o.y) * q.iy;
-        const float tz1 = (mnz - r.o.z) * q.iz, tz2 = (mxz - r.o.z) * q.iz;
-        const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
-        const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
-        const float atmin = fabsf(tmin), atmax = fabsf(tmax);
-        const float slack = 0x1p-20f * (atmin + atmax) + 1e-30f;
-        // all three decisions clear of their boundaries (NaN / inf fail these tests)
-        const bool sure = atmax >= 1e-30f && atmax <= 1e30f && atmin <= 1e30f && fabsf(tmax - tmin) > slack &&
-                          (minT == INFINITY || fabsf(tmin - minT) > 0x1p-20f * atmin + 1e-30f);
-        if (sure) return tmax > 0 && tmax >= tmin && tmin < minT;
-    }
-    return box_hit(mnx, mny, mnz, mxx, mxy, mxz, r, minT);
+    // branch-free: every condition is evaluated (bitwise &, no short circuit), so the
+    // common path is straight-line code with one rarely taken branch to the exact test
+    const float tx1 = (mnx - r.o.x) * q.ix, tx2 = (mxx - r.o.x) * q.ix;
+    const float ty1 = (mny - r.o.y) * q.iy, ty2 = (mxy - r.o.y) * q.iy;
+    const float tz1 = (mnz - r.o.z) * q.iz, tz2 = (mxz - r.o.z) * q.iz;
+    const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+    const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+    const float atmin = fabsf(tmin), atmax = fabsf(tmax);
+    const float slack = 0x1p-20f * (atmin + atmax) + 1e-30f;
+    // all three decisions clear of their boundaries (NaN / inf fail these tests)
+    const bool sure = q.fast & (atmax >= 1e-30f) & (atmax <= 1e30f) & (atmin <= 1e30f) &
+                      (fabsf(tmax - tmin) > slack) &
+                      ((minT == INFINITY) | (fabsf(tmin - minT) > 0x1p-20f * atmin + 1e-30f));
+    const bool hit = (tmax > 0) & (tmax >= tmin) & (tmin < minT);
+    if (__builtin_expect(!sure, 0)) return box_hit(mnx, mny, mnz, mxx, mxy, mxz, r, minT);
+    return hit;
 }
 
 // determinant (helperMath.cpp:132-138)
