@@ -157,7 +157,10 @@ class HostScene:
             self.desc = None
 
     def __del__(self):
-        self.close()
+        try:
+            self.close()
+        except Exception:      # interpreter shutdown: ctypes may already be torn down
+            pass
 
 
 class DeviceScene:
@@ -213,7 +216,10 @@ class DeviceScene:
             self._s = None
 
     def __del__(self):
-        self.close()
+        try:
+            self.close()
+        except Exception:
+            pass
 
 
 def resolve_accum(accum: np.ndarray):

@@ -166,3 +166,349 @@ def with_depth(src_xml: str, dst_xml: str, depth: int) -> str:
     with open(dst_xml, "w") as f:
         f.write(s)
     return dst_xml
+
+
+# ---------------------------------------------------------------------------
+# BASELINE.json configurations C2-C5, as procedural scenes
+# ---------------------------------------------------------------------------
+
+def blob_mesh(K: int, center=(0.0, 0.0, 0.0), radius: float = 1.0, seed: int = 1234, bumps: float = 0.12):
+    """Closed, displaced UV sphere with ~K triangles ("bunny / dragon class" stand-in)."""
+    n = max(4, int(round(np.sqrt(K / 2.0))))
+    n_lat, n_lon = n, n
+    rng = np.random.default_rng(seed)
+    ph = rng.uniform(0, 2 * np.pi, 6)
+    th = np.linspace(0.0, np.pi, n_lat + 1)[1:-1]
+    lo = np.linspace(0.0, 2 * np.pi, n_lon, endpoint=False)
+    T, L = np.meshgrid(th, lo, indexing="ij")
+    r = radius * (1 + bumps * (np.sin(3 * T + ph[0]) * np.cos(4 * L + ph[1]) + 0.5 * np.sin(9 * T + ph[2])
+                               * np.sin(7 * L + ph[3]) + 0.25 * np.cos(17 * T + 13 * L + ph[4])))
+    x = r * np.sin(T) * np.cos(L)
+    y = r * np.cos(T)
+    z = r * np.sin(T) * np.sin(L)
+    ring = np.stack([x, y, z], -1).reshape(-1, 3)
+    verts = np.concatenate([[[0, radius, 0]], ring, [[0, -radius, 0]]]) + np.asarray(center)
+    verts = np.round(verts, 6).astype(np.float32)
+    idx = 1 + np.arange((n_lat - 1) * n_lon).reshape(n_lat - 1, n_lon)
+    nxt = np.roll(idx, -1, axis=1)
+    faces = [np.stack([np.zeros(n_lon, int), nxt[0], idx[0]], -1)]                       # north cap
+    a, b, c, d = idx[:-1], nxt[:-1], idx[1:], nxt[1:]
+    faces.append(np.stack([a, b, d], -1).reshape(-1, 3))
+    faces.append(np.stack([a, d, c], -1).reshape(-1, 3))
+    south = len(verts) - 1
+    faces.append(np.stack([idx[-1], nxt[-1], np.full(n_lon, south)], -1))                 # south cap
+    return verts, np.concatenate(faces).astype(np.int32)
+
+
+def _lookat_camera(pos, gaze_point, up, fovy, res, name, spp=1) -> str:
+    extra = f"\n            <NumSamples>{spp}</NumSamples>" if spp > 1 else ""
+    return f"""    <Cameras>
+        <Camera id="1" type="lookAt">
+            <Position>{_f(pos)}</Position>
+            <GazePoint>{_f(gaze_point)}</GazePoint>
+            <Up>{_f(up)}</Up>
+            <FovY>{fovy}</FovY>
+            <NearDistance>1</NearDistance>
+            <ImageResolution>{res[0]} {res[1]}</ImageResolution>
+            <ImageName>{name}</ImageName>{extra}
+        </Camera>
+    </Cameras>
+"""
+
+
+def _write(out_dir, name, xml):
+    path = os.path.join(out_dir, name + ".xml")
+    with open(path, "w") as f:
+        f.write(xml)
+    return path
+
+
+def _ground(size: float, y: float = 0.0):
+    """VertexData block (4 corners) and the 1-based faces of a ground quad."""
+    s = size
+    v = f"{-s} {y} {-s}\n        {s} {y} {-s}\n        {s} {y} {s}\n        {-s} {y} {s}"
+    return v, "1 3 2\n                1 4 3"
+
+
+def write_ppm(path: str, img: np.ndarray):
+    img = np.ascontiguousarray(np.clip(img, 0, 255).astype(np.uint8))
+    with open(path, "wb") as f:
+        f.write(f"P6\n{img.shape[1]} {img.shape[0]}\n255\n".encode())
+        f.write(img.tobytes())
+
+
+def config_c2(out_dir: str, src_xml: str, width: int = 800, height: int = 800, brdf: bool = True) -> str:
+    """C2: the conductor Cornell box at 800x800, 1 spp; with ``brdf`` an OriginalPhong BRDF on
+    the diffuse materials."""
+    import re
+    os.makedirs(out_dir, exist_ok=True)
+    s = open(src_xml).read()
+    s = re.sub(r"<ImageResolution>[^<]*</ImageResolution>", f"<ImageResolution>{width} {height}</ImageResolution>", s)
+    if brdf:
+        s = s.replace("<Materials>", "<BRDFs>\n        <OriginalPhong id=\"1\">\n            <Exponent>25</Exponent>\n"
+                      "        </OriginalPhong>\n    </BRDFs>\n    <Materials>", 1)
+        for mid in ("1", "2", "3", "4"):
+            s = s.replace(f'<Material id="{mid}">', f'<Material id="{mid}" BRDF="1">', 1)
+    return _write(out_dir, "c2_cornell", s)
+
+
+def config_c3(out_dir: str, K: int = 70000, width: int = 1920, height: int = 1080, spp: int = 4) -> str:
+    """C3: ~70k-triangle closed mesh + area light, OriginalBlinnPhong, 4 spp, 1920x1080."""
+    os.makedirs(out_dir, exist_ok=True)
+    v, f = blob_mesh(K, center=(0, 1.0, 0), radius=1.0, seed=7)
+    write_ply(os.path.join(out_dir, "c3_blob.ply"), v, f)
+    gv, gf = _ground(6.0)
+    xml = f"""<Scene>
+    <MaxRecursionDepth>1</MaxRecursionDepth>
+    <BackgroundColor>5 5 10</BackgroundColor>
+    <ShadowRayEpsilon>1e-3</ShadowRayEpsilon>
+{_lookat_camera((0, 1.6, 4.2), (0, 0.9, 0), (0, 1, 0), 38, (width, height), 'c3.png', spp)}
+    <Lights>
+        <AmbientLight>8 8 8</AmbientLight>
+        <AreaLight id="1">
+            <Position>0.5 4 1</Position>
+            <Normal>0 -1 0</Normal>
+            <Radiance>1500 1400 1300</Radiance>
+            <Size>1.5</Size>
+        </AreaLight>
+    </Lights>
+    <BRDFs>
+        <OriginalBlinnPhong id="1">
+            <Exponent>40</Exponent>
+        </OriginalBlinnPhong>
+    </BRDFs>
+    <Materials>
+        <Material id="1" BRDF="1">
+            <AmbientReflectance>0.3 0.3 0.3</AmbientReflectance>
+            <DiffuseReflectance>0.7 0.55 0.4</DiffuseReflectance>
+            <SpecularReflectance>0.4 0.4 0.4</SpecularReflectance>
+        </Material>
+        <Material id="2">
+            <AmbientReflectance>0.3 0.3 0.3</AmbientReflectance>
+            <DiffuseReflectance>0.5 0.5 0.55</DiffuseReflectance>
+            <SpecularReflectance>0 0 0</SpecularReflectance>
+        </Material>
+    </Materials>
+    <VertexData>
+        {gv}
+    </VertexData>
+    <Objects>
+        <Mesh id="1">
+            <Material>1</Material>
+            <Faces plyFile="c3_blob.ply"/>
+        </Mesh>
+        <Mesh id="2">
+            <Material>2</Material>
+            <Faces>
+                {gf}
+            </Faces>
+        </Mesh>
+    </Objects>
+</Scene>
+"""
+    return _write(out_dir, "c3_blob", xml)
+
+
+def tree_mesh(K: int = 10000, seed: int = 11):
+    """Trunk (open cylinder) + crown (displaced sphere) in one mesh, base at y=0."""
+    cv, cf = blob_mesh(K - 256, center=(0, 1.6, 0), radius=0.7, seed=seed, bumps=0.2)
+    m = 64
+    a = np.linspace(0, 2 * np.pi, m, endpoint=False)
+    ring0 = np.stack([0.12 * np.cos(a), np.zeros(m), 0.12 * np.sin(a)], -1)
+    ring1 = np.stack([0.09 * np.cos(a), np.full(m, 1.0), 0.09 * np.sin(a)], -1)
+    tv = np.round(np.concatenate([ring0, ring1]), 6).astype(np.float32)
+    i0 = np.arange(m)
+    i1 = np.roll(i0, -1)
+    tf = np.concatenate([np.stack([i0, i1, i1 + m], -1), np.stack([i0, i1 + m, i0 + m], -1)])
+    verts = np.concatenate([cv, tv])
+    faces = np.concatenate([cf, tf + len(cv)]).astype(np.int32)
+    return verts, faces
+
+
+def config_c4(out_dir: str, n_side: int = 10, K_tree: int = 10000, width: int = 1920, height: int = 1080,
+              spp: int = 16) -> str:
+    """C4: a ~10k-triangle tree x n_side^2 MeshInstances (~1M effective triangles) with
+    placements composed from single-digit transform ids (parser.cpp:663,689,699): x and
+    z offsets are binary sums of t1-t4 / t5-t8, orientation r1-r9, scale s1-s3;
+    SphericalDirectionalLight with a synthetic sky (inputs/c4_sky.ppm), TorranceSparrow
+    with kdfresnel, 16 spp.  The tree is inline VertexData / Faces: the reference crashes
+    on any MeshInstance in a scene that also holds a PLY mesh."""
+    os.makedirs(os.path.join(out_dir, "inputs"), exist_ok=True)
+    v, f = tree_mesh(K_tree)
+    tree_verts = "\n        ".join(_f(p) for p in v)
+    tree_faces = "\n                ".join(" ".join(str(int(k) + 5) for k in tri) for tri in f)
+    # sky: vertical gradient + a sun blob (LDR, 0..255)
+    H, W = 128, 256
+    yy, xx = np.mgrid[0:H, 0:W]
+    sky = np.stack([60 + 120 * (1 - yy / H), 90 + 110 * (1 - yy / H), 140 + 100 * (1 - yy / H)], -1)
+    sun = np.exp(-(((xx - 0.3 * W) / 9.0) ** 2 + ((yy - 0.25 * H) / 9.0) ** 2))[..., None] * 255
+    write_ppm(os.path.join(out_dir, "inputs", "c4_sky.ppm"), sky + sun)
+    step = 2.0
+    trans = "\n".join([f'        <Translation id="{k + 1}">{step * (1 << k)} 0 0</Translation>' for k in range(4)] +
+                      [f'        <Translation id="{k + 5}">0 0 {-step * (1 << k)}</Translation>' for k in range(4)] +
+                      [f'        <Translation id="9">{-step * (n_side - 1) / 2} 0 {step * 2}</Translation>'])
+    rots = "\n".join(f'        <Rotation id="{k + 1}">{40 * k} 0 1 0</Rotation>' for k in range(9))
+    scls = ('        <Scaling id="1">1 1 1</Scaling>\n        <Scaling id="2">1.15 1.25 1.15</Scaling>\n'
+            '        <Scaling id="3">0.85 0.8 0.85</Scaling>')
+    inst = []
+    for i in range(n_side):
+        for j in range(n_side):
+            k = i * n_side + j
+            ts = [f"t{b + 1}" for b in range(4) if (j >> b) & 1] + [f"t{b + 5}" for b in range(4) if (i >> b) & 1]
+            tr = " ".join([f"s{1 + k % 3}", f"r{1 + (7 * k) % 9}"] + ts + ["t9"])
+            inst.append(f'        <MeshInstance id="{100 + k}" baseMeshId="1">\n'
+                        f'            <Material>{1 + k % 2}</Material>\n'
+                        f'            <Transformations>{tr}</Transformations>\n'
+                        f'        </MeshInstance>')
+    gv, gf = _ground(60.0)
+    xml = f"""<Scene>
+    <MaxRecursionDepth>1</MaxRecursionDepth>
+    <BackgroundColor>0 0 0</BackgroundColor>
+    <ShadowRayEpsilon>1e-3</ShadowRayEpsilon>
+{_lookat_camera((0, 6.0, 8.0), (0, 0.5, -8.0), (0, 1, 0), 50, (width, height), 'c4.png', spp)}
+    <Lights>
+        <AmbientLight>10 10 10</AmbientLight>
+        <PointLight id="1">
+            <Position>10 30 10</Position>
+            <Intensity>250000 240000 230000</Intensity>
+        </PointLight>
+        <SphericalDirectionalLight id="1">
+            <ImageId>1</ImageId>
+        </SphericalDirectionalLight>
+    </Lights>
+    <Textures>
+        <Images>
+            <Image id="1">c4_sky.ppm</Image>
+        </Images>
+    </Textures>
+    <BRDFs>
+        <TorranceSparrow id="1" kdfresnel="true">
+            <Exponent>30</Exponent>
+        </TorranceSparrow>
+    </BRDFs>
+    <Materials>
+        <Material id="1" BRDF="1">
+            <AmbientReflectance>0.1 0.1 0.1</AmbientReflectance>
+            <DiffuseReflectance>0.2 0.45 0.15</DiffuseReflectance>
+            <SpecularReflectance>0.2 0.2 0.2</SpecularReflectance>
+            <RefractionIndex>1.4</RefractionIndex>
+        </Material>
+        <Material id="2" BRDF="1">
+            <AmbientReflectance>0.1 0.1 0.1</AmbientReflectance>
+            <DiffuseReflectance>0.35 0.4 0.1</DiffuseReflectance>
+            <SpecularReflectance>0.2 0.2 0.2</SpecularReflectance>
+            <RefractionIndex>1.4</RefractionIndex>
+        </Material>
+        <Material id="3">
+            <AmbientReflectance>0.1 0.1 0.1</AmbientReflectance>
+            <DiffuseReflectance>0.3 0.25 0.2</DiffuseReflectance>
+            <SpecularReflectance>0 0 0</SpecularReflectance>
+        </Material>
+    </Materials>
+    <Transformations>
+{trans}
+{rots}
+{scls}
+    </Transformations>
+    <VertexData>
+        {gv}
+        {tree_verts}
+    </VertexData>
+    <Objects>
+        <Mesh id="1">
+            <Material>1</Material>
+            <Faces>
+                {tree_faces}
+            </Faces>
+        </Mesh>
+        <Mesh id="2">
+            <Material>3</Material>
+            <Faces>
+                {gf}
+            </Faces>
+        </Mesh>
+{chr(10).join(inst)}
+    </Objects>
+</Scene>
+"""
+    return _write(out_dir, "c4_forest", xml)
+
+
+def config_c5(out_dir: str, K: int = 870000, width: int = 3840, height: int = 2160, spp: int = 64,
+              depth: int = 5) -> str:
+    """C5: ~870k-triangle closed mesh ("dragon" stand-in) as a dielectric, a mirror sphere,
+    a Perlin replace_kd ground, reflect/refract depth 5, 3840x2160, 64 spp.  No area light,
+    roughness or DOF: deterministic."""
+    os.makedirs(out_dir, exist_ok=True)
+    v, f = blob_mesh(K, center=(0, 1.0, 0), radius=1.0, seed=5, bumps=0.15)
+    write_ply(os.path.join(out_dir, "c5_dragon.ply"), v, f)
+    gv, gf = _ground(12.0)
+    xml = f"""<Scene>
+    <MaxRecursionDepth>{depth}</MaxRecursionDepth>
+    <BackgroundColor>20 25 40</BackgroundColor>
+    <ShadowRayEpsilon>1e-3</ShadowRayEpsilon>
+{_lookat_camera((0, 2.0, 5.0), (0, 0.9, 0), (0, 1, 0), 40, (width, height), 'c5.png', spp)}
+    <Lights>
+        <AmbientLight>15 15 15</AmbientLight>
+        <PointLight id="1">
+            <Position>3 6 4</Position>
+            <Intensity>3000 2900 2800</Intensity>
+        </PointLight>
+        <PointLight id="2">
+            <Position>-4 5 -2</Position>
+            <Intensity>1500 1600 1800</Intensity>
+        </PointLight>
+    </Lights>
+    <Materials>
+        <Material id="1" type="dielectric">
+            <AmbientReflectance>0 0 0</AmbientReflectance>
+            <DiffuseReflectance>0 0 0</DiffuseReflectance>
+            <SpecularReflectance>0 0 0</SpecularReflectance>
+            <AbsorptionCoefficient>0.01 0.05 0.1</AbsorptionCoefficient>
+            <RefractionIndex>1.5</RefractionIndex>
+        </Material>
+        <Material id="2" type="mirror">
+            <AmbientReflectance>0 0 0</AmbientReflectance>
+            <DiffuseReflectance>0.05 0.05 0.05</DiffuseReflectance>
+            <SpecularReflectance>0 0 0</SpecularReflectance>
+            <MirrorReflectance>0.85 0.85 0.9</MirrorReflectance>
+        </Material>
+        <Material id="3">
+            <AmbientReflectance>0.5 0.5 0.5</AmbientReflectance>
+            <DiffuseReflectance>0.6 0.6 0.6</DiffuseReflectance>
+            <SpecularReflectance>0.2 0.2 0.2</SpecularReflectance>
+            <PhongExponent>10</PhongExponent>
+        </Material>
+    </Materials>
+    <Textures>
+        <TextureMap id="1" type="perlin">
+            <DecalMode>replace_kd</DecalMode>
+            <NoiseConversion>absval</NoiseConversion>
+            <NoiseScale>1.5</NoiseScale>
+        </TextureMap>
+    </Textures>
+    <VertexData>
+        {gv}
+        -2.2 0.8 -1.5
+    </VertexData>
+    <Objects>
+        <Mesh id="1">
+            <Material>1</Material>
+            <Faces plyFile="c5_dragon.ply"/>
+        </Mesh>
+        <Mesh id="2">
+            <Material>3</Material>
+            <Textures>1</Textures>
+            <Faces>
+                {gf}
+            </Faces>
+        </Mesh>
+        <Sphere id="1">
+            <Material>2</Material>
+            <Center>5</Center>
+            <Radius>0.8</Radius>
+        </Sphere>
+    </Objects>
+</Scene>
+"""
+    return _write(out_dir, "c5_dragon", xml)

@@ -41,7 +41,32 @@ def parse():
     p.add_argument("--cpu-threads", type=int, default=8, help="reference THREAD_COUNT (main.cpp:15)")
     p.add_argument("--cpu-reps", type=int, default=3)
     p.add_argument("--sweep", action="store_true", help="also report K in {1k,10k,1M} (extra field)")
+    p.add_argument("--config", default="headline", choices=["headline", "c2", "c3", "c4", "c5"],
+                   help="BASELINE.json configuration (c2-c5: one frame = all camera samples)")
     return p.parse_args()
+
+
+CONFIG_DESC = {
+    "c2": "C2 conductor Cornell box + OriginalPhong BRDF, 800x800, 1 spp, depth 6",
+    "c3": "C3 70k-triangle mesh + area light, OriginalBlinnPhong, 1920x1080, 4 spp",
+    "c4": "C4 10k-triangle tree x 100 MeshInstances (~1M effective) + spherical env light, "
+          "TorranceSparrow kdfresnel, 1920x1080, 16 spp",
+    "c5": "C5 870k-triangle dielectric mesh + mirror sphere + Perlin ground, depth 5, 3840x2160, 64 spp",
+}
+
+
+def make_workload(args, out_dir):
+    import scenes
+    if args.config == "headline":
+        xml = scenes.synthetic_heightfield(out_dir, K=args.K, width=args.width, height=args.height)
+        desc = (f"synthetic height field K={args.K} tris, {args.width}x{args.height}, 1 spp, 1 point light, "
+                "default Blinn-Phong, primary+shadow rays")
+        return xml, desc
+    if args.config == "c2":
+        xml = scenes.config_c2(out_dir, os.path.join(ROOT, "tests", "golden", "scenes", "cornell_conductors.xml"))
+    else:
+        xml = getattr(scenes, "config_" + args.config)(out_dir)
+    return xml, CONFIG_DESC[args.config]
 
 
 def cpu_baseline(xml_dir, xml, rays_per_frame, threads, reps):
@@ -153,7 +178,7 @@ def main():
     tmp = tempfile.mkdtemp(prefix=f"rtg_bench_r{rank}_")
     old = os.getcwd()
     try:
-        xml = scenes.synthetic_heightfield(tmp, K=args.K, width=args.width, height=args.height)
+        xml, desc = make_workload(args, tmp)
         os.chdir(tmp)
         hs = rtgpu.HostScene(xml)
         ds = rtgpu.DeviceScene(hs, local)
@@ -203,10 +228,9 @@ def main():
             "dtype": "f32",
             "data": "synthetic (seeded procedural height field, written as the reference's XML+PLY)",
             "config": {
-                "workload": f"synthetic height field K={args.K} tris, {W}x{H}, 1 spp, 1 point light, "
-                            "default Blinn-Phong, primary+shadow rays",
-                "scene_K": int(args.K),
-                "width": W, "height": H, "spp": 1,
+                "workload": desc,
+                "scene_K": int(args.K) if args.config == "headline" else int(hs.counts()["faces"]),
+                "width": W, "height": H, "spp": int(cam["spp"]),
                 "rays_per_frame": int(rays),
                 "camera_rays": int(st["camera_rays"]), "shadow_rays": int(st["shadow_rays"]),
                 "node_visits_per_extend_ray": round(st["node_visits"] / max(rays - st["shadow_rays"], 1), 2),
@@ -233,7 +257,7 @@ def main():
             },
             "cpu_baseline": None,
         }
-        if args.sweep and rank == 0:
+        if args.sweep and rank == 0 and args.config == "headline":
             sweep = {}
             for K in (1000, 10082, 1002528):
                 sub = tempfile.mkdtemp(prefix="rtg_sweep_")
@@ -254,7 +278,7 @@ def main():
                 h2.close()
                 shutil.rmtree(sub, ignore_errors=True)
             result["sweep_K"] = sweep
-        if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "headline":
             result["cpu_baseline"] = cpu_baseline(tmp, xml, rays, args.cpu_threads, args.cpu_reps)
         if rank == 0:
             print(json.dumps(result), flush=True)
