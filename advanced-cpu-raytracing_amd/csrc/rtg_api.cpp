@@ -206,6 +206,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     // ---- BVH: reference topology -> pre-order with skip links (rtg_device.hpp)
     std::vector<float4> nodes;
     std::vector<int2> next;
+    bool bigleaf = false;
     nodes.reserve(2 * d->num_nodes); next.reserve(d->num_nodes);
     std::vector<int> meshBegin(d->num_meshes), meshEnd(d->num_meshes);
     for (int m = 0; m < d->num_meshes; ++m) {
@@ -237,6 +238,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
             const int first = M.face_offset + n.first;
             int leaf = -1;
             if (n.left < 0) leaf = (first < (1 << 23) && n.count < 255) ? (first << 8) | n.count : rtg::LEAF_EXT;
+            if (n.left < 0 && n.count > rtg::kCoopLeaf) bigleaf = true;
             float4 a, b;
             a.x = n.bmin[0]; a.y = n.bmin[1]; a.z = n.bmin[2]; a.w = n.bmax[0];
             b.x = n.bmax[1]; b.y = n.bmax[2];
@@ -309,7 +311,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
         branching |= (t == RTG_MAT_MIRROR || t == RTG_MAT_DIELECTRIC || t == RTG_MAT_CONDUCTOR);
     }
     for (int i = 0; i < d->num_objects; ++i) blur |= (d->objects[i].flags & RTG_OBJF_MOTION_BLUR) != 0;
-    sc->feat = feat;
+    sc->feat = feat | (bigleaf ? rtg::FEAT_BIGLEAF : 0);
     sc->wave_ok = !blur && (d->max_recursion_depth <= 0 || !branching);
     sc->num_slots = d->num_point_lights + d->num_area_lights + d->num_env_lights + d->num_dir_lights +
                     d->num_spot_lights;

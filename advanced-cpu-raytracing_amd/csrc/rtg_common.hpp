@@ -83,6 +83,7 @@ enum { RP_MOTION = 1, RP_DOF = 2, RP_JITTER = 3, RP_AREA = 4, RP_ENV = 5, RP_ROU
 template <bool STATS> struct Cnt {
     template <bool ANY> DEV void node() {}
     template <bool ANY> DEV void tri() {}
+    template <bool ANY> DEV void tri_n(uint32_t) {}
     DEV void sph() {} DEV void obj() {}
     DEV void cam() {} DEV void sec() {} DEV void shd() {}
 };
@@ -90,6 +91,7 @@ template <> struct Cnt<true> {
     uint32_t nodes = 0, tris = 0, sphs = 0, objs = 0, cams = 0, secs = 0, shds = 0, snodes = 0, stris = 0;
     template <bool ANY> DEV void node() { if (ANY) ++snodes; else ++nodes; }
     template <bool ANY> DEV void tri() { if (ANY) ++stris; else ++tris; }
+    template <bool ANY> DEV void tri_n(uint32_t n) { if (ANY) stris += n; else tris += n; }
     DEV void sph() { ++sphs; } DEV void obj() { ++objs; }
     DEV void cam() { ++cams; } DEV void sec() { ++secs; } DEV void shd() { ++shds; }
 };
@@ -223,11 +225,42 @@ DEV bool tri_test_fast(const DevScene& S, int f, const Ray& r, float minT, float
     return tri_test(S, f, r, minT, tout);
 }
 
-// BVH::IntersectBVH (bvh.cpp:5-30) as a stackless pre-order walk (rtg_device.hpp).
-// ANY: stop at the first accepted face with t < limit (CastShadowRay semantics).
+// 64-bit lexicographic (t, face) key of a candidate hit; t > 0, so the float bits order
+// like the values.  Non-candidates: ~0.
+DEV uint64_t hit_key(float t, int f) { return ((uint64_t)__float_as_uint(t) << 32) | (uint32_t)f; }
+
+// Minimum of `key` over the lanes set in `em` (the wave's active lanes).  A butterfly
+// needs every lane; with a partial exec mask (image-edge tiles, rays that skip an
+// instance, the fused kernel's ray trees) the active lanes' keys are read one by one.
+DEV uint64_t shfl64(uint64_t v, int src) {
+    const uint32_t lo = (uint32_t)__shfl((int)(uint32_t)v, src);
+    const uint32_t hi = (uint32_t)__shfl((int)(uint32_t)(v >> 32), src);
+    return ((uint64_t)hi << 32) | lo;
+}
+DEV uint64_t wave_min_key(uint64_t key, uint64_t em) {
+    if (em == ~0ull) {
+        const int lane = threadIdx.x & 63;
+        for (int m = 1; m < 64; m <<= 1) {
+            const uint64_t other = shfl64(key, lane ^ m);
+            if (other < key) key = other;
+        }
+        return key;
+    }
+    uint64_t acc = ~0ull;
+    while (em) {
+        const int l = __ffsll((long long)em) - 1;
+        em &= em - 1;
+        const uint64_t v = shfl64(key, l);
+        if (v < acc) acc = v;
+    }
+    return acc;
+}
+
+// Sequential form: each lane tests its leaves' faces in order inside the walk (scenes
+// whose leaves are all small: the lean kernels).
 template <bool ANY, bool STATS>
-DEV bool walk_bvh(const DevScene& S, int i, const int end, const Ray& r, float& minT, int& hitFace, float limit,
-                  Cnt<STATS>& c) {
+DEV bool walk_bvh_seq(const DevScene& S, int i, const int end, const Ray& r, float& minT, int& hitFace, float limit,
+                      Cnt<STATS>& c) {
     bool hit = false;
     const RayRcp q = ray_rcp(r);
     while (i < end) {
@@ -260,6 +293,106 @@ DEV bool walk_bvh(const DevScene& S, int i, const int end, const Ray& r, float& 
             }
         } else {
             i = skip;
+        }
+    }
+    return hit;
+}
+
+// BVH::IntersectBVH (bvh.cpp:5-30) as a stackless pre-order walk (rtg_device.hpp).
+// ANY: stop at the first accepted face with t < limit (CastShadowRay semantics).
+//
+// Leaves of up to kCoopLeaf faces are tested by their lane in order.  Larger leaves
+// (the reference's midpoint split keeps faces with equal centroid coordinates
+// together, e.g. fans around a mesh pole, in leaves of hundreds of faces) are tested
+// cooperatively: the walk loop runs while any lane of the wave is active, and every
+// lane that reached such a leaf in this step has it tested by all active lanes of the
+// wave in parallel, followed by a (t, face) minimum reduction.  That is exactly the
+// sequential result: IntersectFace's acceptance is t < minT with minT shrinking over
+// the leaf, so the survivor is the smallest t -- the first face among equal t -- of the
+// faces with t < minT at leaf entry; for ANY, "some face with t < min(minT, limit)".
+template <bool ANY, bool STATS, bool COOP>
+DEV bool walk_bvh(const DevScene& S, int i, const int end, const Ray& r, float& minT, int& hitFace, float limit,
+                  Cnt<STATS>& c) {
+    if constexpr (!COOP) return walk_bvh_seq<ANY, STATS>(S, i, end, r, minT, hitFace, limit, c);
+    bool hit = false;
+    const RayRcp q = ray_rcp(r);
+    bool active = i < end;
+    while (__ballot(active)) {
+        int coopFirst = 0, coopCnt = 0;
+        if (active) {
+            const float4 a = S.nodes[2 * i];
+            const float4 b = S.nodes[2 * i + 1];
+            c.template node<ANY>();
+            const int skip = __float_as_int(b.z);
+            if (box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, r, q, minT)) {
+                const int leaf = __float_as_int(b.w);
+                if (leaf >= 0) {
+                    int first = leaf >> 8, cnt = leaf & 255;
+                    if (leaf == LEAF_EXT) {
+                        const int2 e = S.node_ext[i];
+                        first = e.x;
+                        cnt = e.y;
+                    }
+                    if (cnt > kCoopLeaf) {
+                        coopFirst = first;
+                        coopCnt = cnt;
+                    } else {
+                        for (int f = first; f < first + cnt; ++f) {
+                            c.template tri<ANY>();
+                            float t;
+                            if (tri_test_fast(S, f, r, minT, t)) {
+                                minT = t;
+                                hitFace = f;
+                                hit = true;
+                                if (ANY && t < limit) {
+                                    active = false;
+                                    break;
+                                }
+                            }
+                        }
+                    }
+                    i = skip;
+                } else {
+                    i = i + 1;
+                }
+            } else {
+                i = skip;
+            }
+            if (i >= end) active = false;
+        }
+        uint64_t coop = __ballot(coopCnt > 0);
+        if (coop) {
+            const uint64_t em = __ballot(1);
+            const int lane = threadIdx.x & 63;
+            const int nact = __popcll(em);
+            const int rank = __popcll(em & ((1ull << lane) - 1ull));
+            while (coop) {
+                const int L = __ffsll((long long)coop) - 1;
+                coop &= coop - 1;
+                Ray lr;
+                lr.o = mk(__shfl(r.o.x, L), __shfl(r.o.y, L), __shfl(r.o.z, L));
+                lr.d = mk(__shfl(r.d.x, L), __shfl(r.d.y, L), __shfl(r.d.z, L));
+                const float mt = __shfl(minT, L);
+                const int lf = __shfl(coopFirst, L), lc = __shfl(coopCnt, L);
+                uint64_t best = ~0ull;
+                for (int k = rank; k < lc; k += nact) {
+                    float t;
+                    if (tri_test_fast(S, lf + k, lr, mt, t)) {
+                        const uint64_t key = hit_key(t, lf + k);
+                        if (key < best) best = key;
+                    }
+                }
+                best = wave_min_key(best, em);
+                if (lane == L) {
+                    c.template tri_n<ANY>((uint32_t)lc);
+                    if (best != ~0ull) {
+                        minT = __uint_as_float((uint32_t)(best >> 32));
+                        hitFace = (int)(uint32_t)best;
+                        hit = true;
+                        if (ANY && minT < limit) active = false;
+                    }
+                }
+            }
         }
     }
     return hit;
@@ -348,7 +481,7 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
         Ray lr = (FEAT & FEAT_XFORM) ? trav_ray(ob, r, mbTime) : r;
         int face = -1;
         float t = h.t;
-        if (walk_bvh<ANY, STATS>(S, ob.node_begin, ob.node_end, lr, t, face, limit, c)) {
+        if (walk_bvh<ANY, STATS, (FEAT & FEAT_BIGLEAF) != 0>(S, ob.node_begin, ob.node_end, lr, t, face, limit, c)) {
             h.t = t; h.obj = k; h.face = face; h.o = r.o;
             if (ANY && t < limit) return true;
         }

@@ -71,8 +71,9 @@ struct DevSpotLight {
 enum : int { LEAF_EXT = 0x7FFFFFFF };
 
 // Scene feature bits (kernel specialisation): spheres, mesh instances, any mesh with a
-// non-identity transform or motion blur.
-enum : int { FEAT_SPHERE = 1, FEAT_INSTANCE = 2, FEAT_XFORM = 4, FEAT_ALL = 7 };
+// non-identity transform or motion blur, BVH leaves of more than kCoopLeaf faces.
+enum : int { FEAT_SPHERE = 1, FEAT_INSTANCE = 2, FEAT_XFORM = 4, FEAT_BIGLEAF = 8, FEAT_ALL = 15 };
+constexpr int kCoopLeaf = 8;
 
 struct DevScene {
     const float4* __restrict__ nodes;

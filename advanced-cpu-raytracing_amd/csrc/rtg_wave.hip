@@ -299,15 +299,24 @@ static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const Ren
 
 hipError_t launch_wave(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W, float* hdr,
                        unsigned char* l, DevCounters* cnt, bool stats, int feat, hipStream_t stream, hipEvent_t* ev) {
-    // traversal variants: meshes only (identity transforms) / + spheres / everything
-    if (feat == 0)
-        return stats ? launch_wave_t<true, 0>(S, C, P, W, hdr, l, cnt, stream, ev)
-                     : launch_wave_t<false, 0>(S, C, P, W, hdr, l, cnt, stream, ev);
-    if (feat == FEAT_SPHERE)
-        return stats ? launch_wave_t<true, FEAT_SPHERE>(S, C, P, W, hdr, l, cnt, stream, ev)
-                     : launch_wave_t<false, FEAT_SPHERE>(S, C, P, W, hdr, l, cnt, stream, ev);
-    return stats ? launch_wave_t<true, FEAT_ALL>(S, C, P, W, hdr, l, cnt, stream, ev)
-                 : launch_wave_t<false, FEAT_ALL>(S, C, P, W, hdr, l, cnt, stream, ev);
+    // traversal variants: meshes only (identity transforms) / + spheres / everything,
+    // each with the sequential or the cooperative (large-leaf) BVH walk
+    const bool big = (feat & FEAT_BIGLEAF) != 0;
+    const int base = feat & ~FEAT_BIGLEAF;
+#define RTG_WAVE(F)                                                                    \
+    return stats ? launch_wave_t<true, F>(S, C, P, W, hdr, l, cnt, stream, ev)         \
+                 : launch_wave_t<false, F>(S, C, P, W, hdr, l, cnt, stream, ev)
+    if (base == 0) {
+        if (big) RTG_WAVE(FEAT_BIGLEAF);
+        RTG_WAVE(0);
+    }
+    if (base == FEAT_SPHERE) {
+        if (big) RTG_WAVE(FEAT_SPHERE | FEAT_BIGLEAF);
+        RTG_WAVE(FEAT_SPHERE);
+    }
+    if (big) RTG_WAVE(FEAT_ALL);
+    RTG_WAVE(FEAT_ALL & ~FEAT_BIGLEAF);
+#undef RTG_WAVE
 }
 
 }  // namespace rtg

@@ -98,3 +98,25 @@ def test_c5_dragon_4k_64spp(in_tmp):
     r = ob.compare(a[rows[0]:rows[1]], oacc[rows[0]:rows[1]], REL)
     print("vs oracle", r)
     assert r["rel_pass"] == 1.0, r
+
+
+@pytest.mark.parametrize("cfg", ["c3", "c4"])
+def test_large_leaf_cooperative_walk_small(cfg, in_tmp):
+    """Meshes whose midpoint BVH keeps leaves of hundreds of faces take the wave-cooperative
+    leaf test; with instances the walk runs under partial exec masks.  Whole image vs the
+    oracle, and the wavefront pipeline == the fused kernel bit for bit."""
+    if cfg == "c3":
+        xml = scenes.config_c3(in_tmp, K=20000, width=320, height=180, spp=1)
+    else:
+        xml = scenes.config_c4(in_tmp, n_side=3, K_tree=4000, width=320, height=180, spp=1)
+    hs, ds = _scene(xml)
+    hdr, _ = ds.render(0, seed=3)
+    ohdr, _, _ = ob.render(hs, seed=3)
+    r = ob.compare(hdr, ohdr, REL)
+    print(r)
+    assert r["rel_pass"] >= 0.999, r
+    xml0 = scenes.with_depth(xml, os.path.join(in_tmp, "d0.xml"), 0)
+    hs0, ds0 = _scene(xml0)
+    a, _ = ds0.render(0, seed=3)
+    b, _ = ds0.render(0, seed=3, flags=rtgpu.RTG_RENDER_FUSED)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
