@@ -200,6 +200,34 @@ def blob_mesh(K: int, center=(0.0, 0.0, 0.0), radius: float = 1.0, seed: int = 1
     return verts, np.concatenate(faces).astype(np.int32)
 
 
+def torus_mesh(K: int, center=(0.0, 0.0, 0.0), R: float = 1.0, r: float = 0.45, seed: int = 1234,
+               bumps: float = 0.08):
+    """Displaced torus with ~K triangles, tilted 30 degrees about x: a dense closed mesh with
+    no poles (a UV sphere's pole fans share centroid coordinates, which the reference's
+    midpoint split cannot separate; scanned meshes have no such fans)."""
+    nv = max(3, int(round(np.sqrt(K / 4.0))))
+    nu = max(3, int(round(K / (2.0 * nv))))
+    rng = np.random.default_rng(seed)
+    ph = rng.uniform(0, 2 * np.pi, 4)
+    u = np.linspace(0.0, 2 * np.pi, nu, endpoint=False)
+    v = np.linspace(0.0, 2 * np.pi, nv, endpoint=False)
+    U, Vv = np.meshgrid(u, v, indexing="ij")
+    rr = r * (1 + bumps * (np.sin(7 * U + ph[0]) * np.cos(5 * Vv + ph[1]) + 0.5 * np.sin(23 * U + 3 * Vv + ph[2])
+                           + 0.25 * np.cos(61 * U + 11 * Vv + ph[3])))
+    x = (R + rr * np.cos(Vv)) * np.cos(U)
+    z = (R + rr * np.cos(Vv)) * np.sin(U)
+    y = rr * np.sin(Vv)
+    a = np.radians(30.0)
+    y, z = y * np.cos(a) - z * np.sin(a), y * np.sin(a) + z * np.cos(a)
+    verts = np.round(np.stack([x, y, z], -1).reshape(-1, 3) + np.asarray(center), 6).astype(np.float32)
+    idx = np.arange(nu * nv).reshape(nu, nv)
+    i1 = np.roll(idx, -1, axis=0)
+    j1 = np.roll(idx, -1, axis=1)
+    ij1 = np.roll(i1, -1, axis=1)
+    faces = np.concatenate([np.stack([idx, i1, ij1], -1).reshape(-1, 3), np.stack([idx, ij1, j1], -1).reshape(-1, 3)])
+    return verts, faces.astype(np.int32)
+
+
 def _lookat_camera(pos, gaze_point, up, fovy, res, name, spp=1) -> str:
     extra = f"\n            <NumSamples>{spp}</NumSamples>" if spp > 1 else ""
     return f"""    <Cameras>
@@ -309,17 +337,61 @@ def config_c3(out_dir: str, K: int = 70000, width: int = 1920, height: int = 108
     return _write(out_dir, "c3_blob", xml)
 
 
+def octasphere_mesh(level: int, center=(0.0, 0.0, 0.0), radius: float = 1.0, seed: int = 11,
+                    bumps: float = 0.2):
+    """Displaced sphere from a subdivided octahedron: 8 * 4**level triangles, no pole fans."""
+    n = 1 << level
+    rng = np.random.default_rng(seed)
+    ph = rng.uniform(0, 2 * np.pi, 3)
+    corners = np.array([[1, 0, 0], [0, 1, 0], [0, 0, 1], [-1, 0, 0], [0, -1, 0], [0, 0, -1]], np.float64)
+    octa = [(0, 1, 2), (1, 3, 2), (3, 4, 2), (4, 0, 2), (1, 0, 5), (3, 1, 5), (4, 3, 5), (0, 4, 5)]
+    verts, faces = [], []
+    for a, b, c in octa:
+        A, B, Cc = corners[a], corners[b], corners[c]
+        base = len(verts)
+        idx = {}
+        for i in range(n + 1):
+            for j in range(n + 1 - i):
+                idx[(i, j)] = len(verts)
+                verts.append(A + (B - A) * (i / n) + (Cc - A) * (j / n))
+        for i in range(n):
+            for j in range(n - i):
+                faces.append((idx[(i, j)], idx[(i + 1, j)], idx[(i, j + 1)]))
+                if j < n - i - 1:
+                    faces.append((idx[(i + 1, j)], idx[(i + 1, j + 1)], idx[(i, j + 1)]))
+        del base
+    V = np.array(verts)
+    V /= np.linalg.norm(V, axis=1, keepdims=True)
+    th = np.arccos(np.clip(V[:, 1], -1, 1))
+    lo = np.arctan2(V[:, 2], V[:, 0])
+    rad = radius * (1 + bumps * (np.sin(3 * th + ph[0]) * np.cos(4 * lo + ph[1]) + 0.4 * np.sin(9 * th + 7 * lo + ph[2])))
+    V = V * rad[:, None] + np.asarray(center)
+    return np.round(V, 6).astype(np.float32), np.array(faces, np.int32)
+
+
 def tree_mesh(K: int = 10000, seed: int = 11):
-    """Trunk (open cylinder) + crown (displaced sphere) in one mesh, base at y=0."""
-    cv, cf = blob_mesh(K - 256, center=(0, 1.6, 0), radius=0.7, seed=seed, bumps=0.2)
-    m = 64
+    """Trunk (open cylinder) + crown (displaced octasphere, 8*4^level faces close to K) in
+    one mesh, base at y=0."""
+    level = max(1, int(round(np.log(max(K, 8) / 8.0) / np.log(4.0))))
+    # base geometry in the positive octant (x, z in [0.3, 1.7]); the instances translate it
+    # back.  The reference's node bboxes start from max = FLT_MIN (parser.cpp:1393,
+    # mesh.cpp RecomputeBoundingBox), so a node whose faces all lie at negative
+    # coordinates gets a box reaching 0, its midpoint falls outside every centroid and
+    # the split gives up: leaves of thousands of faces.
+    cv, cf = octasphere_mesh(level, center=(1.0, 1.6, 1.0), radius=0.7, seed=seed)
+    # trunk: 12 rings (short triangles: a long sliver widens its node's box past every
+    # centroid and the reference's midpoint split gives up, mesh.cpp:105-106)
+    m, rings = 48, 12
     a = np.linspace(0, 2 * np.pi, m, endpoint=False)
-    ring0 = np.stack([0.12 * np.cos(a), np.zeros(m), 0.12 * np.sin(a)], -1)
-    ring1 = np.stack([0.09 * np.cos(a), np.full(m, 1.0), 0.09 * np.sin(a)], -1)
-    tv = np.round(np.concatenate([ring0, ring1]), 6).astype(np.float32)
+    hs = np.linspace(0.0, 1.0, rings + 1)
+    rad = 0.12 - 0.03 * hs
+    tv = np.concatenate([np.stack([1.0 + rr * np.cos(a), np.full(m, h), 1.0 + rr * np.sin(a)], -1)
+                         for h, rr in zip(hs, rad)])
+    tv = np.round(tv, 6).astype(np.float32)
     i0 = np.arange(m)
     i1 = np.roll(i0, -1)
-    tf = np.concatenate([np.stack([i0, i1, i1 + m], -1), np.stack([i0, i1 + m, i0 + m], -1)])
+    tf = np.concatenate([np.concatenate([np.stack([i0, i1, i1 + m], -1), np.stack([i0, i1 + m, i0 + m], -1)]) + k * m
+                         for k in range(rings)])
     verts = np.concatenate([cv, tv])
     faces = np.concatenate([cf, tf + len(cv)]).astype(np.int32)
     return verts, faces
@@ -331,12 +403,11 @@ def config_c4(out_dir: str, n_side: int = 10, K_tree: int = 10000, width: int = 
     placements composed from single-digit transform ids (parser.cpp:663,689,699): x and
     z offsets are binary sums of t1-t4 / t5-t8, orientation r1-r9, scale s1-s3;
     SphericalDirectionalLight with a synthetic sky (inputs/c4_sky.ppm), TorranceSparrow
-    with kdfresnel, 16 spp.  The tree is inline VertexData / Faces: the reference crashes
-    on any MeshInstance in a scene that also holds a PLY mesh."""
+    with kdfresnel, 16 spp.  The reference itself cannot render it: CastShadowRay reads the
+    uninitialised Shape::material_id of every InstancedMesh (tests/golden/make_goldens.py)."""
     os.makedirs(os.path.join(out_dir, "inputs"), exist_ok=True)
     v, f = tree_mesh(K_tree)
-    tree_verts = "\n        ".join(_f(p) for p in v)
-    tree_faces = "\n                ".join(" ".join(str(int(k) + 5) for k in tri) for tri in f)
+    write_ply(os.path.join(out_dir, "c4_tree.ply"), v, f)
     # sky: vertical gradient + a sun blob (LDR, 0..255)
     H, W = 128, 256
     yy, xx = np.mgrid[0:H, 0:W]
@@ -346,7 +417,7 @@ def config_c4(out_dir: str, n_side: int = 10, K_tree: int = 10000, width: int = 
     step = 2.0
     trans = "\n".join([f'        <Translation id="{k + 1}">{step * (1 << k)} 0 0</Translation>' for k in range(4)] +
                       [f'        <Translation id="{k + 5}">0 0 {-step * (1 << k)}</Translation>' for k in range(4)] +
-                      [f'        <Translation id="9">{-step * (n_side - 1) / 2} 0 {step * 2}</Translation>'])
+                      [f'        <Translation id="9">{-step * (n_side - 1) / 2 - 1.0} 0 {step * 2 - 1.0}</Translation>'])
     rots = "\n".join(f'        <Rotation id="{k + 1}">{40 * k} 0 1 0</Rotation>' for k in range(9))
     scls = ('        <Scaling id="1">1 1 1</Scaling>\n        <Scaling id="2">1.15 1.25 1.15</Scaling>\n'
             '        <Scaling id="3">0.85 0.8 0.85</Scaling>')
@@ -412,14 +483,11 @@ def config_c4(out_dir: str, n_side: int = 10, K_tree: int = 10000, width: int = 
     </Transformations>
     <VertexData>
         {gv}
-        {tree_verts}
     </VertexData>
     <Objects>
         <Mesh id="1">
             <Material>1</Material>
-            <Faces>
-                {tree_faces}
-            </Faces>
+            <Faces plyFile="c4_tree.ply"/>
         </Mesh>
         <Mesh id="2">
             <Material>3</Material>
@@ -436,11 +504,11 @@ def config_c4(out_dir: str, n_side: int = 10, K_tree: int = 10000, width: int = 
 
 def config_c5(out_dir: str, K: int = 870000, width: int = 3840, height: int = 2160, spp: int = 64,
               depth: int = 5) -> str:
-    """C5: ~870k-triangle closed mesh ("dragon" stand-in) as a dielectric, a mirror sphere,
-    a Perlin replace_kd ground, reflect/refract depth 5, 3840x2160, 64 spp.  No area light,
-    roughness or DOF: deterministic."""
+    """C5: ~870k-triangle closed mesh ("dragon" stand-in: a displaced, tilted torus) as a
+    dielectric, a mirror sphere, a Perlin replace_kd ground, reflect/refract depth 5,
+    3840x2160, 64 spp.  No area light, roughness or DOF: deterministic."""
     os.makedirs(out_dir, exist_ok=True)
-    v, f = blob_mesh(K, center=(0, 1.0, 0), radius=1.0, seed=5, bumps=0.15)
+    v, f = torus_mesh(K, center=(0, 1.1, 0), R=1.0, r=0.42, seed=5)
     write_ply(os.path.join(out_dir, "c5_dragon.ply"), v, f)
     gv, gf = _ground(12.0)
     xml = f"""<Scene>

@@ -98,11 +98,18 @@ def cpu_baseline(xml_dir, xml, rays_per_frame, threads, reps):
             "sample": sample, "seconds_median": round(med, 4)}
 
 
+def log(msg):
+    """Progress on stderr (long configurations: keeps the run visibly alive)."""
+    print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
+
+
 def measure(ds, torch, hdr, ldr, steps, warmup, seed, barrier):
     stream = torch.cuda.current_stream()
     sptr = stream.cuda_stream
-    for _ in range(warmup):
+    for k in range(warmup):
         ds.render_device(hdr.data_ptr(), ldr.data_ptr(), sptr, seed=seed)
+        torch.cuda.synchronize()
+        log(f"warmup {k + 1}/{warmup}")
     torch.cuda.synchronize()
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
@@ -189,6 +196,7 @@ def main():
         seed = 0x5EED + rank
 
         # untimed counting pass: rays / BVH nodes / triangle tests per frame
+        log(f"scene ready: {hs.counts()}, counting pass")
         ds.reset_stats()
         ds.render_device(hdr.data_ptr(), ldr.data_ptr(), torch.cuda.current_stream().cuda_stream, seed=seed,
                          flags=rtgpu.RTG_RENDER_COUNT_STATS)
@@ -196,7 +204,9 @@ def main():
         st = ds.stats()
         rays = st["camera_rays"] + st["secondary_rays"] + st["shadow_rays"]
 
+        log(f"rays/frame {rays}; timing {args.steps} steps")
         elapsed, kern_ms = measure(ds, torch, hdr, ldr, args.steps, args.warmup, seed, barrier)
+        log(f"timed: {elapsed / args.steps * 1e3:.3f} ms/step")
         if dist:
             t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
             dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -19,7 +19,7 @@ def per_kernel(d, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        m = re.search(r"rtg::(k_\w+)(<(\w+)>)?", r["Kernel_Name"])
+        m = re.search(r"rtg::(k_\w+)(<(\w+)[^>]*>)?", r["Kernel_Name"])
         name = m.group(1) + ("" if not m.group(3) else f"<{m.group(3)}>")
         acc[name].append(float(r["Counter_Value"]) * 1024.0)
     return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
