@@ -611,12 +611,50 @@ int rtg_render(rtg_scene* s, const rtg_render_opts* o, float* hdr_rgb, uint8_t* 
     HIP_TRY(hipMemset(s->d_ldr, 0, pixels * 3));
     rc = launch(s, o, C, P, s->d_hdr, s->d_ldr, nullptr, nullptr);
     if (rc) return rc;
+    // tonemapped camera, whole image: the LDR output is the tonemapped image (main.cpp:187-192)
+    const rtg_camera& cam = s->cameras[o->camera];
+    if (cam.has_tonemapper && P.row_begin == 0 && P.row_end == C.height) {
+        rtg_tonemap_params tp = {cam.tm_key, cam.tm_burn, cam.tm_saturation, cam.tm_gamma};
+        rc = rtg_tonemap_device(s->d_hdr, C.width, C.height, &tp, s->d_ldr, s->device, nullptr);
+        if (rc) return rc;
+    }
     HIP_TRY(hipDeviceSynchronize());
     // rows outside [row_begin, row_end) are left untouched in the caller's buffers
     const size_t off = (size_t)P.row_begin * C.width * 3, n = (size_t)(P.row_end - P.row_begin) * C.width * 3;
     if (hdr_rgb) HIP_TRY(hipMemcpy(hdr_rgb + off, s->d_hdr + off, n * sizeof(float), hipMemcpyDeviceToHost));
     if (ldr_rgb) HIP_TRY(hipMemcpy(ldr_rgb + off, s->d_ldr + off, n, hipMemcpyDeviceToHost));
     return RTG_OK;
+}
+
+int rtg_tonemap_device(const float* d_hdr, int32_t w, int32_t h, const rtg_tonemap_params* tp, uint8_t* d_ldr,
+                       int32_t device, void* stream) {
+    if (!d_hdr || !d_ldr || !tp || w <= 0 || h <= 0) return set_err(RTG_ERR_INVALID, "bad tonemap arguments");
+    HIP_TRY(hipSetDevice(device));
+    hipStream_t st = (hipStream_t)stream;
+    void* scratch = nullptr;
+    HIP_TRY(hipMallocAsync(&scratch, rtg::tonemap_scratch_bytes((long long)w * h), st));
+    hipError_t e = rtg::launch_tonemap(d_hdr, w, h, tp->key, tp->burn_percent, tp->saturation, tp->gamma, d_ldr, scratch, st);
+    hipError_t e2 = hipFreeAsync(scratch, st);
+    HIP_TRY(e);
+    HIP_TRY(e2);
+    return RTG_OK;
+}
+
+int rtg_tonemap(const float* hdr, int32_t w, int32_t h, const rtg_tonemap_params* tp, uint8_t* ldr, int32_t device) {
+    if (!hdr || !ldr || !tp || w <= 0 || h <= 0) return set_err(RTG_ERR_INVALID, "bad tonemap arguments");
+    HIP_TRY(hipSetDevice(device));
+    const size_t n = (size_t)w * h * 3;
+    float* dh = nullptr;
+    uint8_t* dl = nullptr;
+    HIP_TRY(hipMalloc(&dh, n * sizeof(float)));
+    if (hipMalloc(&dl, n) != hipSuccess) { (void)hipFree(dh); return set_err(RTG_ERR_NOMEM, "device allocation failed"); }
+    int rc = RTG_OK;
+    if (hipMemcpy(dh, hdr, n * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) rc = set_err(RTG_ERR_HIP, "copy failed");
+    if (!rc) rc = rtg_tonemap_device(dh, w, h, tp, dl, device, nullptr);
+    if (!rc && hipMemcpy(ldr, dl, n, hipMemcpyDeviceToHost) != hipSuccess) rc = set_err(RTG_ERR_HIP, "copy failed");
+    (void)hipFree(dh);
+    (void)hipFree(dl);
+    return rc;
 }
 
 int rtg_resolve_accum(const float* accum, int32_t w, int32_t h, float* hdr, uint8_t* ldr) {

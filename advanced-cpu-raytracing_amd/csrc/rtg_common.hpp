@@ -155,7 +155,7 @@ DEV bool box_hit_fast(float mnx, float mny, float mnz, float mxx, float mxy, flo
     const float atmin = fabsf(tmin), atmax = fabsf(tmax);
     const float slack = 0x1p-20f * (atmin + atmax) + 1e-30f;
     // all three decisions clear of their boundaries (NaN / inf fail these tests)
-    const bool sure = q.fast & (atmax >= 1e-30f) & (atmax <= 1e30f) & (atmin <= 1e30f) &
+    const bool sure = (int)q.fast & (atmax >= 1e-30f) & (atmax <= 1e30f) & (atmin <= 1e30f) &
                       (fabsf(tmax - tmin) > slack) &
                       ((minT == INFINITY) | (fabsf(tmin - minT) > 0x1p-20f * atmin + 1e-30f));
     const bool hit = (tmax > 0) & (tmax >= tmin) & (tmin < minT);

@@ -15,6 +15,10 @@ hipError_t launch_mega(const DevScene& S, const DevCamera& C, const RenderParams
 hipError_t launch_wave(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W, float* hdr,
                        unsigned char* ldr, DevCounters* counters, bool stats, int feat, hipStream_t stream,
                        hipEvent_t* ev);
+// photographic tonemapper (rtg_tonemap.hip); scratch of tonemap_scratch_bytes()
+size_t tonemap_scratch_bytes(long long pixels);
+hipError_t launch_tonemap(const float* hdr, int width, int height, float key, float burn, float saturation,
+                          float gamma, unsigned char* ldr, void* scratch, hipStream_t stream);
 enum { WAVE_STAGES = 4, MEGA_STAGES = 1, MAX_STAGES = 4 };
 
 }  // namespace rtg

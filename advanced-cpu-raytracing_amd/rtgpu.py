@@ -35,6 +35,11 @@ class RTGError(RuntimeError):
         self.code = code
 
 
+class TonemapParams(ctypes.Structure):
+    _fields_ = [("key", ctypes.c_float), ("burn_percent", ctypes.c_float), ("saturation", ctypes.c_float),
+                ("gamma", ctypes.c_float)]
+
+
 class RenderOpts(ctypes.Structure):
     _fields_ = [
         ("camera", ctypes.c_int32),
@@ -61,7 +66,8 @@ EXPORTED = [
     "rtg_host_scene_load_xml", "rtg_host_scene_desc", "rtg_host_scene_free",
     "rtg_desc_camera_info", "rtg_desc_counts", "rtg_scene_create", "rtg_scene_destroy",
     "rtg_device_count", "rtg_render", "rtg_render_device", "rtg_resolve_accum",
-    "rtg_scene_stats", "rtg_scene_reset_stats", "rtg_scene_timings", "rtg_write_png", "rtg_write_hdr",
+    "rtg_scene_stats", "rtg_scene_reset_stats", "rtg_scene_timings", "rtg_tonemap_device", "rtg_tonemap",
+    "rtg_write_png", "rtg_write_hdr",
     "rtg_last_error", "rtg_abi_version",
 ]
 
@@ -103,6 +109,8 @@ def lib() -> ctypes.CDLL:
     L.rtg_scene_stats.argtypes = [vp, P(Stats)]
     L.rtg_scene_reset_stats.argtypes = [vp]
     L.rtg_scene_timings.argtypes = [vp, P(ctypes.c_float), P(ctypes.c_char_p), i32, P(i32)]
+    L.rtg_tonemap_device.argtypes = [vp, i32, i32, P(TonemapParams), vp, i32, vp]
+    L.rtg_tonemap.argtypes = [vp, i32, i32, P(TonemapParams), vp, i32]
     L.rtg_write_png.argtypes = [ctypes.c_char_p, i32, i32, vp]
     L.rtg_write_hdr.argtypes = [ctypes.c_char_p, i32, i32, vp]
     _lib = L
@@ -230,6 +238,16 @@ def resolve_accum(accum: np.ndarray):
     ldr = np.zeros((h, w, 3), np.uint8)
     _check(lib().rtg_resolve_accum(accum.ctypes.data, w, h, hdr.ctypes.data, ldr.ctypes.data))
     return hdr, ldr
+
+
+def tonemap(hdr: np.ndarray, key=0.18, burn=1.0, saturation=1.0, gamma=2.2, device: int = 0) -> np.ndarray:
+    """Photographic tonemapper (Tonemapper::Tonemap, tonemapper.h:28-60) on the GPU."""
+    hdr = np.ascontiguousarray(hdr, np.float32)
+    h, w, _ = hdr.shape
+    ldr = np.zeros((h, w, 3), np.uint8)
+    p = TonemapParams(key, burn, saturation, gamma)
+    _check(lib().rtg_tonemap(hdr.ctypes.data, w, h, ctypes.byref(p), ldr.ctypes.data, device))
+    return ldr
 
 
 def write_png(path: str, ldr: np.ndarray):

@@ -290,8 +290,10 @@ typedef struct {
 /* One call per camera, replacing main.cpp:164-185 (threads -> renderThreadMain ->
  * RenderPixel).  Host buffers of width*height*3, layout 3*(x + y*width)
  * (main.cpp:109).  hdr_rgb receives the float colour (what main.cpp:114-116
- * stores for tonemapped cameras); ldr_rgb receives clamp((int)c) (main.cpp:121).
- * Either may be NULL. */
+ * stores for tonemapped cameras); ldr_rgb receives clamp((int)c) (main.cpp:121), or,
+ * for a camera with a <Tonemap> rendered over all its rows, the tonemapped image
+ * main.cpp:187-192 produces (a row band gets the clamp: tonemap the gathered image
+ * with rtg_tonemap).  Either may be NULL. */
 int rtg_render(rtg_scene* scene, const rtg_render_opts* opts, float* hdr_rgb, uint8_t* ldr_rgb);
 
 /* Same on device-resident buffers (hipMalloc'd / torch tensors) on `stream`
@@ -314,6 +316,22 @@ int rtg_scene_reset_stats(rtg_scene* scene);
  * Wavefront pipeline: names "k_primary", "k_shade", "k_shadow", "k_resolve"; fused
  * kernel: "k_render".  Writes up to `cap` entries; *count = number of stages. */
 int rtg_scene_timings(rtg_scene* scene, float* ms, const char** names, int32_t cap, int32_t* count);
+
+/* ------------------------------------------------------------------------- */
+/* Tonemapping (tonemapper.h, main.cpp:187-192)                               */
+/* ------------------------------------------------------------------------- */
+/* Tonemapper(opType, keyValue, burnPerct, saturation, gamma) (tonemapper.h:18-25);
+ * the parser's defaults are 0.18, 1, 1, 2.2 (parser.cpp:845-863). */
+typedef struct { float key, burn_percent, saturation, gamma; } rtg_tonemap_params;
+
+/* Replaces Camera::GetTonemappedImage -> Tonemapper::Tonemap (tonemapper.h:28-60):
+ * photographic operator over a whole width*height float RGB image in device memory,
+ * writing the 8-bit image main.cpp:195 saves.  Asynchronous on `stream`. */
+int rtg_tonemap_device(const float* d_hdr_rgb, int32_t width, int32_t height, const rtg_tonemap_params* params,
+                       uint8_t* d_ldr_rgb, int32_t device, void* stream);
+/* Same on host buffers (copies through device `device`; synchronous). */
+int rtg_tonemap(const float* hdr_rgb, int32_t width, int32_t height, const rtg_tonemap_params* params,
+                uint8_t* ldr_rgb, int32_t device);
 
 /* ------------------------------------------------------------------------- */
 /* Output (main.cpp:187-195)                                                  */

@@ -29,6 +29,7 @@
 // pinned bit-for-bit against the reference itself (oracle/_ref, tests/golden).
 //
 // Build: g++ -O2 -ffp-contract=off (no FMA contraction, like the reference binary).
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
@@ -965,6 +966,60 @@ int oracle_render(const rtg_scene_desc* desc, int camera, int row_begin, int row
             stats[4] += c.tris; stats[5] += c.spheres; stats[6] += c.objects; stats[7] += c.snodes;
             stats[8] += c.stris;
         }
+    }
+    return 0;
+}
+
+// Tonemapper::Tonemap (tonemapper.h:28-60, photographic operator): the log-average
+// luminance as one sequential double sum, the burn threshold from the sorted list of all
+// channel values (float), and TonemapPixel's double math with its float round trips
+// (Reinhard returns float, clip takes and returns float, gammaInv = 1.0f / gamma).
+static float TmClip(float n, float lower, float upper) { return std::max(lower, std::min(n, upper)); }
+
+int oracle_tonemap(const float* hdr, int width, int height, float key, float burn, float saturation, float gamma,
+                   uint8_t* ldr) {
+    if (!hdr || !ldr || width <= 0 || height <= 0) return 1;
+    const float delta = 0.01f;
+    const size_t n = (size_t)width * height;
+    std::vector<float> sorted(3 * n);
+    double logSum = 0.0f;
+    for (size_t i = 0; i < n; i++) {
+        double r = sorted[3 * i + 0] = hdr[3 * i + 0];
+        double g = sorted[3 * i + 1] = hdr[3 * i + 1];
+        double b = sorted[3 * i + 2] = hdr[3 * i + 2];
+        double lum = 0.2126 * r + 0.7152 * g + 0.0722 * b;
+        logSum += std::log(delta + lum);
+    }
+    long pixelCount = width * height;
+    const double avg = std::exp(logSum / (double)pixelCount);
+    std::sort(sorted.begin(), sorted.end());
+    auto reinhard = [&](double Y) -> float {
+        double Lxy = (key * Y) / avg;
+        if (burn > 0.01) {
+            float thresholdPerct = (100.0f - burn) / 100;
+            int lastIdx = (int)sorted.size() - 1;
+            int idx = std::min(lastIdx, (int)(thresholdPerct * lastIdx));
+            double thr = sorted[idx];
+            thr = thr * key / avg;
+            double LwhiteSqr = thr * thr;
+            return (Lxy * (1 + (Lxy / LwhiteSqr))) / (1.0f + Lxy);
+        }
+        return Lxy / (1 + Lxy);
+    };
+    for (size_t i = 0; i < n; i++) {
+        double R = hdr[3 * i], G = hdr[3 * i + 1], B = hdr[3 * i + 2];
+        double y_i = 0.2126 * R + 0.7152 * G + 0.0722 * B;
+        double y_o = reinhard(y_i);
+        double r_o = TmClip(y_o * std::pow((R / y_i), saturation), 0.0f, 1.0f);
+        double g_o = TmClip(y_o * std::pow((G / y_i), saturation), 0.0f, 1.0f);
+        double b_o = TmClip(y_o * std::pow((B / y_i), saturation), 0.0f, 1.0f);
+        double gammaInv = 1.0f / gamma;
+        int cx = std::floor(std::min(255.0, 255 * std::pow(r_o, gammaInv)));
+        int cy = std::floor(std::min(255.0, 255 * std::pow(g_o, gammaInv)));
+        int cz = std::floor(std::min(255.0, 255 * std::pow(b_o, gammaInv)));
+        ldr[3 * i] = (uint8_t)cx;
+        ldr[3 * i + 1] = (uint8_t)cy;
+        ldr[3 * i + 2] = (uint8_t)cz;
     }
     return 0;
 }

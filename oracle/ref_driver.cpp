@@ -12,6 +12,10 @@
 //       Times the reference's row-band render exactly as main.cpp:164-185 partitions it
 //       (rows [t*(H/T), (t+1)*(H/T)) per thread; spawn -> join), spp==1 per pixel via
 //       RenderPixel, and prints one JSON line with the per-rep seconds.
+//   refdriver tonemap <in.bin> <key> <burn%> <saturation> <gamma> <out.bin>
+//       The reference's own Tonemapper::Tonemap (tonemapper.h:28-60) on an "RTGF" float
+//       image (as dump writes); writes "RTGL" int32 w, int32 h, w*h*3 uint8 (the LDR
+//       image main.cpp:187-195 saves for a tonemapped camera).
 #define STB_IMAGE_WRITE_IMPLEMENTATION
 #include "stb_image_write.h"
 #define STB_IMAGE_IMPLEMENTATION
@@ -87,7 +91,30 @@ static int bench(const char* xml, int threads, int reps, int ci) {
     return 0;
 }
 
+static int tonemap(const char* in, float key, float burn, float sat, float gamma, const char* out) {
+    FILE* f = std::fopen(in, "rb");
+    if (!f) { std::perror(in); return 1; }
+    char magic[4];
+    int32_t wh[2];
+    if (std::fread(magic, 1, 4, f) != 4 || std::memcmp(magic, "RTGF", 4) || std::fread(wh, 4, 2, f) != 2) return 1;
+    std::vector<float> hdr((size_t)wh[0] * wh[1] * 3);
+    if (std::fread(hdr.data(), 4, hdr.size(), f) != hdr.size()) return 1;
+    std::fclose(f);
+    std::vector<unsigned char> ldr(hdr.size());
+    Tonemapper tm("Photographic", key, burn, sat, gamma);
+    tm.Tonemap(wh[0], wh[1], hdr.data(), ldr.data());
+    f = std::fopen(out, "wb");
+    if (!f) { std::perror(out); return 1; }
+    std::fwrite("RTGL", 1, 4, f);
+    std::fwrite(wh, 4, 2, f);
+    std::fwrite(ldr.data(), 1, ldr.size(), f);
+    std::fclose(f);
+    return 0;
+}
+
 int main(int argc, char** argv) {
+    if (argc >= 8 && !std::strcmp(argv[1], "tonemap"))
+        return tonemap(argv[2], std::atof(argv[3]), std::atof(argv[4]), std::atof(argv[5]), std::atof(argv[6]), argv[7]);
     if (argc >= 4 && !std::strcmp(argv[1], "dump")) return dump(argv[2], argv[3], argc > 4 ? std::atoi(argv[4]) : 0);
     if (argc >= 5 && !std::strcmp(argv[1], "bench"))
         return bench(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), argc > 5 ? std::atoi(argv[5]) : 0);

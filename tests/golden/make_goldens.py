@@ -161,11 +161,43 @@ def dump(name):
     return np.frombuffer(raw[12:], np.float32).reshape(h, w, 3).copy()
 
 
+# Tonemapper goldens: the reference's own Tonemapper::Tonemap (refdriver tonemap) applied
+# to golden float images, (key, burn %, saturation, gamma) per case.
+TONEMAP_SOURCES = ("env_light", "brdf_lights", "c3_blob", "cornell_conductors")
+TONEMAP_PARAMS = ((0.18, 1.0, 1.0, 2.2), (0.36, 0.0, 0.8, 2.0), (0.09, 5.0, 1.2, 1.8))
+
+
+def make_tonemap_goldens():
+    out = {}
+    for name in TONEMAP_SOURCES:
+        hdr = np.load(os.path.join(HERE, name + ".npz"), allow_pickle=False)["hdr"].astype(np.float32)
+        h, w, _ = hdr.shape
+        src = os.path.join(HERE, "_tm_in.bin")
+        with open(src, "wb") as f:
+            f.write(b"RTGF" + np.array([w, h], np.int32).tobytes() + hdr.tobytes())
+        for k, (key, burn, sat, gamma) in enumerate(TONEMAP_PARAMS):
+            dst = os.path.join(HERE, "_tm_out.bin")
+            subprocess.run([DRIVER, "tonemap", src, str(key), str(burn), str(sat), str(gamma), dst], check=True,
+                           stdout=subprocess.DEVNULL)
+            raw = open(dst, "rb").read()
+            assert raw[:4] == b"RTGL"
+            out[f"{name}__{k}"] = np.frombuffer(raw[12:], np.uint8).reshape(h, w, 3).copy()
+            os.remove(dst)
+        os.remove(src)
+    np.savez_compressed(os.path.join(HERE, "tonemap.npz"), **out)
+    with open(os.path.join(HERE, "tonemap.json"), "w") as f:
+        json.dump({"sources": list(TONEMAP_SOURCES), "params": [list(p) for p in TONEMAP_PARAMS]}, f, indent=1)
+    print("tonemap goldens", len(out))
+
+
 def main():
     if not os.path.exists(DRIVER):
         sys.exit(f"{DRIVER} missing: build it with `make -C {os.path.join(ROOT, 'oracle')}` (needs /root/reference)")
     man = {}
     only = set(sys.argv[1:])
+    if only == {"tonemap"}:
+        make_tonemap_goldens()
+        return
     for name, (src, w, h, kind, edits) in FIXTURES.items():
         if only and name not in only:
             continue

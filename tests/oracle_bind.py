@@ -58,6 +58,26 @@ def render(host_scene, camera=0, rows=(0, 0), seed=0x5EED, threads=None, sample_
     return hdr, ldr, dict(zip(STAT_NAMES, map(int, st)))
 
 
+def tonemap(hdr, key=0.18, burn=1.0, saturation=1.0, gamma=2.2):
+    """CPU restatement of Tonemapper::Tonemap (tonemapper.h:28-60)."""
+    hdr = np.ascontiguousarray(hdr, np.float32)
+    h, w, _ = hdr.shape
+    out = np.zeros((h, w, 3), np.uint8)
+    f = ctypes.c_float
+    L = lib()
+    L.oracle_tonemap.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, f, f, f, f, ctypes.c_void_p]
+    if L.oracle_tonemap(hdr.ctypes.data, w, h, key, burn, saturation, gamma, out.ctypes.data):
+        raise RuntimeError("oracle_tonemap failed")
+    return out
+
+
+def tonemap_goldens():
+    """[(source name, params, reference LDR)] from tests/golden/tonemap.npz."""
+    meta = json.load(open(os.path.join(GOLDEN, "tonemap.json")))
+    d = np.load(os.path.join(GOLDEN, "tonemap.npz"), allow_pickle=False)
+    return [(n, tuple(p), d[f"{n}__{k}"]) for n in meta["sources"] for k, p in enumerate(meta["params"])]
+
+
 def clamp_ldr(hdr):
     """x86 (int) conversion + clamp to [0,255] (helperMath.cpp:140-152)."""
     x = np.asarray(hdr, np.float64)

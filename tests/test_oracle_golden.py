@@ -97,3 +97,12 @@ def test_oracle_traversal_counts_match_survey():
     per_ray = (st["tri_tests"] + st["shadow_tri_tests"]) / (st["camera_rays"] + st["secondary_rays"] + st["shadow_rays"])
     # 108023024 tests / (1036800 + 1073849 + 793976) rays at full size
     assert 30 < per_ray < 45, per_ray
+
+
+@pytest.mark.parametrize("case", range(12))
+def test_oracle_tonemap_matches_reference(case):
+    """The restated photographic tonemapper == the reference's Tonemapper::Tonemap
+    (tests/golden/tonemap.npz, made by refdriver tonemap), byte for byte."""
+    name, (key, burn, sat, gamma), ref = ob.tonemap_goldens()[case]
+    got = ob.tonemap(ob.load_golden(name), key, burn, sat, gamma)
+    assert np.array_equal(got, ref), (name, key, burn, np.mean(got != ref))
