@@ -97,6 +97,8 @@ struct rtg_scene {
     DevBuf<int> perm;
     DevBuf<float> grad;
     bool wave_ok = false;             // scene renders on the wavefront pipeline
+    bool tree_ok = false;             // scene may render on the wavefront ray-tree pipeline
+    rtg::TreeState* tree = nullptr;   // its buffers
     int feat = rtg::FEAT_ALL;         // scene feature bits (traversal specialisation)
     int num_slots = 0;                // lights per pixel (wavefront light slots)
     // wavefront buffers, grown on demand
@@ -115,6 +117,7 @@ struct rtg_scene {
     hipEvent_t ev[rtg::MAX_STAGES + 1] = {};
     int timed_stages = 0;             // stages recorded by the last timed render
     ~rtg_scene() {
+        if (tree) rtg::tree_destroy(tree);
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
         if (d_hdr) (void)hipFree(d_hdr);
@@ -312,6 +315,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     }
     for (int i = 0; i < d->num_objects; ++i) blur |= (d->objects[i].flags & RTG_OBJF_MOTION_BLUR) != 0;
     sc->feat = feat | (bigleaf ? rtg::FEAT_BIGLEAF : 0);
+    sc->tree_ok = !blur && d->max_recursion_depth > 0 && branching;
     sc->wave_ok = !blur && (d->max_recursion_depth <= 0 || !branching);
     sc->num_slots = d->num_point_lights + d->num_area_lights + d->num_env_lights + d->num_dir_lights +
                     d->num_spot_lights;
@@ -553,6 +557,22 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
             if (!e) HIP_TRY(hipEventCreate(&e));
         ev = s->ev;
     }
+    // ray trees: the wavefront tree pipeline for large frames (it synchronises once per tree
+    // level), the fused kernel otherwise; RTG_RENDER_TREE / RTG_RENDER_FUSED force either
+    const long long work = (long long)(P.row_end - P.row_begin) * C.width * P.sample_count;
+    const bool use_tree = s->tree_ok && !(o->flags & RTG_RENDER_FUSED) &&
+                          ((o->flags & RTG_RENDER_TREE) || work >= (1ll << 21));
+    if (use_tree) {
+        float4* acc = (float4*)d_accum;
+        if (!P.accum_only && C.spp > 1) {   // internal accumulator indexed by absolute pixel
+            int rc = ensure_wave(s, (size_t)C.width * C.height, s->num_slots, (size_t)P.num_tiles);
+            if (rc) return rc;
+            acc = s->wave.accum;
+        }
+        HIP_TRY(rtg::launch_tree(s->tree, s->ds, C, P, d_hdr, d_ldr, acc, s->counters.p, stats, s->feat, stream, ev));
+        if (ev) s->timed_stages = rtg::TREE_STAGES;
+        return RTG_OK;
+    }
     if (s->wave_ok && !(o->flags & RTG_RENDER_FUSED)) {
         const size_t rows = (size_t)(P.row_end - P.row_begin);
         int rc = ensure_wave(s, rows * C.width, s->num_slots, (size_t)P.num_tiles);
@@ -702,12 +722,13 @@ int rtg_scene_reset_stats(rtg_scene* s) {
 int rtg_scene_timings(rtg_scene* s, float* ms, const char** names, int32_t cap, int32_t* count) {
     static const char* kWave[rtg::WAVE_STAGES] = {"k_primary", "k_shade", "k_shadow", "k_resolve"};
     static const char* kMega[rtg::MEGA_STAGES] = {"k_render"};
+    static const char* kTree[rtg::TREE_STAGES] = {"tree_levels", "tree_resolve"};
     if (!s || !count) return set_err(RTG_ERR_INVALID, "null argument");
     if (!s->timed_stages) return set_err(RTG_ERR_INVALID, "no render was issued with RTG_RENDER_TIMING");
     HIP_TRY(hipSetDevice(s->device));
     const int n = s->timed_stages;
     HIP_TRY(hipEventSynchronize(s->ev[n]));
-    const char** nm = n == rtg::WAVE_STAGES ? kWave : kMega;
+    const char** nm = n == rtg::WAVE_STAGES ? kWave : (n == rtg::TREE_STAGES ? kTree : kMega);
     for (int k = 0; k < n && k < cap; ++k) {
         float t = 0.f;
         HIP_TRY(hipEventElapsedTime(&t, s->ev[k], s->ev[k + 1]));

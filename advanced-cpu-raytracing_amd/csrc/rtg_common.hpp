@@ -778,49 +778,62 @@ DEV bool in_shadow_dir(const DevScene& S, f3 p, f3 n, f3 lightDir, float mbTime,
     return trace<true, STATS>(S, sr, mbTime, INFINITY, INFINITY, h, c);
 }
 
-// SampleDirectLighting (raytracer.cpp:701-805): type order point, area, env, dir, spot
-template <bool STATS>
-DEV f3 direct(const DevScene& S, const ShadeCtx& c, f3 w_o, float mbTime, uint64_t key, Cnt<STATS>& cn) {
-    f3 color = mk(0, 0, 0);
-    const f3 p = c.s.p, n = c.s.n;
-    for (int i = 0; i < S.num_point; ++i) {
+// One light of SampleDirectLighting (raytracer.cpp:701-805), slots in the reference's
+// type order point, area, env, dir, spot: the incident direction, the irradiance and,
+// where the reference casts one, the shadow ray (IsInShadow :567-584 /
+// IsInShadowDirectional :555-566).
+struct LightSample {
+    f3 w_i, E;
+    bool shadow;
+    Ray sr;
+    float minT, limit;
+};
+DEV LightSample light_sample(const DevScene& S, int slot, f3 p, f3 n, uint64_t key) {
+    LightSample ls;
+    ls.shadow = true;
+    ls.sr.o = add(p, muls(n, S.eps));
+    f3 lpos = mk(0, 0, 0);
+    bool positional = true;
+    int i = slot;
+    if (i < S.num_point) {
         const f3 lp = ld3(S.point_lights[i].pos);
-        if (in_shadow<STATS>(S, p, n, lp, mbTime, cn)) continue;
-        f3 w_i = makeUnit(sub(lp, p));
+        lpos = lp;
+        ls.w_i = makeUnit(sub(lp, p));
         float dist = len(sub(lp, p));
-        f3 E = divs(ld3(S.point_lights[i].intensity), dist * dist);
-        color = add(color, shade(S, c, w_i, w_o, E));
-    }
-    for (int i = 0; i < S.num_area; ++i) {
+        ls.E = divs(ld3(S.point_lights[i].intensity), dist * dist);
+    } else if ((i -= S.num_point) < S.num_area) {
         const DevAreaLight& L = S.area_lights[i];
         float offU = rnd(key, RP_AREA, 2 * i) - 0.5f;                     // areaLight.h:34-41
         float offV = rnd(key, RP_AREA, 2 * i + 1) - 0.5f;
         f3 sp = add(add(ld3(L.pos), muls(ld3(L.u), L.extent * offU)), muls(ld3(L.v), L.extent * offV));
-        if (in_shadow<STATS>(S, p, n, sp, mbTime, cn)) continue;
+        lpos = sp;
         f3 w_i = sub(sp, p);
         float dist = len(w_i);
         float dSqr = dist * dist;
         w_i = divs(w_i, dist);
         float lc = dot(ld3(L.normal), neg(w_i));
         if (lc < 0) lc = dot(ld3(L.normal), w_i);
-        f3 E = muls(ld3(L.radiance), L.area * lc / dSqr);
-        color = add(color, shade(S, c, w_i, w_o, E));
-    }
-    for (int i = 0; i < S.num_env; ++i) {
+        ls.w_i = w_i;
+        ls.E = muls(ld3(L.radiance), L.area * lc / dSqr);
+    } else if ((i -= S.num_area) < S.num_env) {                           // no shadow ray (:741-755)
         f3 sd = env_direction(n, key, i);
-        f3 E = env_sample(S, i, sd);
-        color = add(color, shade(S, c, n, w_o, E));
-    }
-    for (int i = 0; i < S.num_dir; ++i) {
+        ls.E = env_sample(S, i, sd);
+        ls.w_i = n;
+        ls.shadow = false;
+    } else if ((i -= S.num_env) < S.num_dir) {
         const f3 ldir = ld3(S.dir_lights[i].dir);
-        if (in_shadow_dir<STATS>(S, p, n, ldir, mbTime, cn)) continue;
-        color = add(color, shade(S, c, neg(ldir), w_o, ld3(S.dir_lights[i].radiance)));
-    }
-    for (int i = 0; i < S.num_spot; ++i) {
+        ls.w_i = neg(ldir);
+        ls.E = ld3(S.dir_lights[i].radiance);
+        ls.sr.d = neg(ldir);
+        ls.minT = INFINITY;
+        ls.limit = INFINITY;
+        positional = false;
+    } else {
+        i -= S.num_dir;
         const DevSpotLight& L = S.spot_lights[i];
         const f3 lp = ld3(L.pos);
-        if (in_shadow<STATS>(S, p, n, lp, mbTime, cn)) continue;
-        f3 w_i = makeUnit(sub(lp, p));
+        lpos = lp;
+        ls.w_i = makeUnit(sub(lp, p));
         // SpotLight::GetIrradiance (spotLight.h:33-57)
         float distToPoint = len(sub(p, lp));
         f3 toPoint = divs(sub(p, lp), distToPoint);
@@ -833,11 +846,38 @@ DEV f3 direct(const DevScene& S, const ShadeCtx& c, f3 w_o, float mbTime, uint64
             E = divs(ld3(L.intensity), distSqr);
             if (alpha > (L.falloff_deg / 2.0f)) {
                 double cosAlpha = cos(alpha * (RT_PI / 180.0f));
-                double s = pow((cosAlpha - L.cos_half_coverage) / (L.cos_half_falloff - L.cos_half_coverage), (double)4.0f);
-                E = muls(E, (float)s);
+                double sv = pow((cosAlpha - L.cos_half_coverage) / (L.cos_half_falloff - L.cos_half_coverage), (double)4.0f);
+                E = muls(E, (float)sv);
             }
         }
-        color = add(color, shade(S, c, w_i, w_o, E));
+        ls.E = E;
+    }
+    if (ls.shadow && positional) {
+        f3 dir = sub(lpos, p);
+        float lightT = len(dir);
+        ls.sr.d = divs(dir, lightT);
+        ls.minT = lightT + 0.01f;
+        ls.limit = lightT;
+    }
+    return ls;
+}
+
+// SampleDirectLighting (raytracer.cpp:701-805): the unshadowed lights' Shade terms summed in
+// slot order.  One trace and one Shade call site for all light types (the BRDF code and the
+// traversal are inlined once).
+template <bool STATS>
+DEV f3 direct(const DevScene& S, const ShadeCtx& c, f3 w_o, float mbTime, uint64_t key, Cnt<STATS>& cn) {
+    f3 color = mk(0, 0, 0);
+    const f3 p = c.s.p, n = c.s.n;
+    const int nslots = S.num_point + S.num_area + S.num_env + S.num_dir + S.num_spot;
+    for (int l = 0; l < nslots; ++l) {
+        LightSample ls = light_sample(S, l, p, n, key);
+        if (ls.shadow) {
+            Hit h;
+            cn.shd();
+            if (trace<true, STATS>(S, ls.sr, mbTime, ls.minT, ls.limit, h, cn)) continue;
+        }
+        color = add(color, shade(S, c, ls.w_i, w_o, ls.E));
     }
     return color;
 }
@@ -946,6 +986,25 @@ DEV void flush_counters(Cnt<STATS>& cn, DevCounters* counters) {
             if ((threadIdx.x & 63) == 0 && x) atomicAdd(&((unsigned long long*)counters)[k], x);
         }
     }
+}
+
+// Shadow queue in per-block segments (rtg_wave.hip k_shade, rtg_tree.hip k_tree_shade):
+// one thread per queued shadow ray, CastShadowRay as early-exit any-hit (raytracer.cpp:585-623).
+template <bool STATS, int FEAT>
+// grid (shade blocks, slots): block (b, c) takes entries [256c, 256c+256) of segment b
+__global__ __launch_bounds__(256) void k_shadow(const DevScene S, const WaveBufs W, DevCounters* counters) {
+    const int k = blockIdx.y * 256 + threadIdx.x;
+    const size_t q = ((size_t)blockIdx.x * W.num_slots) * 256 + k;
+    Cnt<STATS> cn;
+    if (k < W.q_count[blockIdx.x]) {
+        const float4 o = W.q_o[q], d = W.q_d[q];
+        Ray r;
+        r.o = mk(o.x, o.y, o.z);
+        r.d = mk(d.x, d.y, d.z);
+        Hit h;
+        if (trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn)) W.occ[W.q_slot[q]] = 1;
+    }
+    flush_counters<STATS>(cn, counters);
 }
 
 }  // namespace rtg

@@ -138,6 +138,40 @@ struct WaveBufs {
     int pixel_base;                     // row_begin * width
 };
 
+// One level of the wavefront ray tree (rtg_tree.hip): rays, their hits, the shading node
+// each hit becomes and its final value.
+struct TreeLevel {
+    float4* o;                          // origin, medium
+    float4* d;                          // direction, tree level (int bits)
+    unsigned long long* key;            // RNG key of the ray-tree node
+    float4* miss;                       // miss lookup: env direction, mode (int bits)
+    float* t;
+    int* obj;
+    int* face;
+    float4* base;                       // ambient colour, kind | lit flag (int bits)
+    float4* coef;                       // mirror reflectance, ratio (conductor / Fresnel reflect)
+    float4* ext;                        // refract ratio, material, child 0, child 1 (int bits)
+    float4* value;                      // node value (rgb), ray hit something (int bits)
+    float4* term;                       // per light slot: Shade term
+    unsigned char* occ;                 // per light slot: 1 = in shadow
+    int n;
+};
+// Per-block output segments of k_tree_shade: shadow rays (256 x slots per block, the
+// k_shadow layout) and child rays (512 per block).
+struct TreeSegs {
+    float4* q_o;
+    float4* q_d;
+    int* q_slot;
+    int* q_count;
+    float4* c_o;
+    float4* c_d;
+    unsigned long long* c_key;
+    float4* c_miss;
+    int* c_parent;                      // parent node | slot << 30
+    int* c_count;
+    int num_slots;
+};
+
 // Per-launch ray/traversal counters (RTG_RENDER_COUNT_STATS).
 struct DevCounters {
     unsigned long long camera_rays, secondary_rays, shadow_rays, node_visits, tri_tests, sphere_tests,

@@ -15,10 +15,17 @@ hipError_t launch_mega(const DevScene& S, const DevCamera& C, const RenderParams
 hipError_t launch_wave(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W, float* hdr,
                        unsigned char* ldr, DevCounters* counters, bool stats, int feat, hipStream_t stream,
                        hipEvent_t* ev);
+// wavefront ray trees (rtg_tree.hip): scenes with mirror / conductor / dielectric materials;
+// host-synchronous per tree level (the next level's size); state (buffers) kept in `tree`
+struct TreeState;
+void tree_destroy(TreeState* tree);
+hipError_t launch_tree(TreeState*& tree, const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr,
+                       unsigned char* ldr, float4* accum, DevCounters* counters, bool stats, int feat,
+                       hipStream_t stream, hipEvent_t* ev);
 // photographic tonemapper (rtg_tonemap.hip); scratch of tonemap_scratch_bytes()
 size_t tonemap_scratch_bytes(long long pixels);
 hipError_t launch_tonemap(const float* hdr, int width, int height, float key, float burn, float saturation,
                           float gamma, unsigned char* ldr, void* scratch, hipStream_t stream);
-enum { WAVE_STAGES = 4, MEGA_STAGES = 1, MAX_STAGES = 4 };
+enum { WAVE_STAGES = 4, MEGA_STAGES = 1, TREE_STAGES = 2, MAX_STAGES = 4 };
 
 }  // namespace rtg

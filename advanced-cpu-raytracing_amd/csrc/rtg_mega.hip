@@ -156,21 +156,19 @@ DEV f3 env_or_zero(const DevScene& S, f3 dir) {
 }
 
 // Whole ray tree of one pixel sample; returns RenderPixel's colour
-// (raytracer.cpp:38-63).
+// (raytracer.cpp:38-63).  A single trace call site: the loop holds one pending ray
+// (camera ray, a frame's first child, or a dielectric frame's refracted child).
 template <int MAXD, bool STATS>
 DEV f3 render_sample(const DevScene& S, const DevCamera& C, int px, int py, uint64_t key, Cnt<STATS>& cn) {
     float mbTime;
-    Ray ray = camera_ray(C, px, py, key, mbTime);
+    Ray R = camera_ray(C, px, py, key, mbTime);
     const f3 cpos = ld3(C.pos);
     cn.cam();
-    Node cur;
-    if (!trace<false, STATS>(S, ray, mbTime, INFINITY, INFINITY, cur.h, cn)) return miss_color(S, C, px, py, ray.d);
-    cur.r = ray;
-    cur.eye = cpos;
-    cur.medium = 1.0f;
-    cur.mbTime = mbTime;
-    cur.depth = S.max_depth;
-    cur.key = key;
+    // pending ray: medium, remaining depth, RNG key; pend: 0 camera, 1 first child, 2 refracted
+    float rMedium = 1.0f;
+    int rDepth = S.max_depth;
+    uint64_t rKey = key;
+    int pend = 0;
 
     Frame stack[MAXD > 0 ? MAXD : 1];
     int sp = 0;
@@ -178,28 +176,40 @@ DEV f3 render_sample(const DevScene& S, const DevCamera& C, int px, int py, uint
     bool vHit;
     float vT = 0.f, vMedium = 1.f;
     for (;;) {
-        // ---- shade the current node; a node with children pushes a frame
-        Child ch;
-        const bool spawn = shade_node<STATS>(S, cur, value, stack[MAXD > 0 ? sp : 0], ch, cn);
-        if (MAXD > 0 && spawn) {
-            ++sp;
-            const Frame& f = stack[sp - 1];
-            cn.sec();
-            Node nx;
-            if (trace<false, STATS>(S, ch.r, cur.mbTime, INFINITY, INFINITY, nx.h, cn)) {
-                nx.r = ch.r; nx.eye = ch.r.o; nx.medium = ch.medium; nx.mbTime = cur.mbTime;
-                nx.depth = f.depth - 1;
-                nx.key = child_key(f.key, 0);
-                cur = nx;
+        Node cur;
+        const bool hit = trace<false, STATS>(S, R, mbTime, INFINITY, INFINITY, cur.h, cn);
+        if (pend == 0 && !hit) return miss_color(S, C, px, py, R.d);
+        if (hit) {
+            cur.r = R;
+            cur.eye = pend == 0 ? cpos : R.o;
+            cur.medium = rMedium;
+            cur.mbTime = mbTime;
+            cur.depth = rDepth;
+            cur.key = rKey;
+            // ---- shade; a node with children pushes a frame and continues with its first child
+            Child ch;
+            const bool spawn = shade_node<STATS>(S, cur, value, stack[MAXD > 0 ? sp : 0], ch, cn);
+            if (MAXD > 0 && spawn) {
+                const Frame& f = stack[sp];
+                ++sp;
+                cn.sec();
+                R = ch.r;
+                rMedium = ch.medium;
+                rDepth = f.depth - 1;
+                rKey = child_key(f.key, 0);
+                pend = 1;
                 continue;
             }
-            // miss (ComputeMirrorReflection :461-470, dielectric reflected :351-356)
-            if (f.kind == FK_MIRROR) value = env_or_zero(S, ch.r.d);
-            else if (f.kind == FK_DIEL) value = env_or_zero(S, f.reflDir);
+            vHit = true;
+            vT = cur.h.t;
+            vMedium = cur.medium;
+        } else {
+            // a child missed (ComputeMirrorReflection :461-470, dielectric :351-356, :408 --
+            // the refracted miss looks the environment up in the reflected direction)
+            const Frame& f = stack[MAXD > 0 ? sp - 1 : 0];
+            if (f.kind == FK_MIRROR || f.kind == FK_DIEL) value = env_or_zero(S, f.kind == FK_MIRROR ? R.d : f.reflDir);
             else value = mk(0, 0, 0);
             vHit = false;
-        } else {
-            vHit = true; vT = cur.h.t; vMedium = cur.medium;
         }
         // ---- propagate finished values up the stack
         bool descended = false;
@@ -220,22 +230,15 @@ DEV f3 render_sample(const DevScene& S, const DevCamera& C, int px, int py, uint
                 } else {
                     wr = makeUnit(wr);
                 }
-                Ray rr;
-                rr.o = f.rOrigin;
-                rr.d = wr;
+                R.o = f.rOrigin;
+                R.d = wr;
+                rMedium = f.rMedium;
+                rDepth = f.depth - 1;
+                rKey = child_key(f.key, 1);
+                pend = 2;
                 cn.sec();
-                Node nx;
-                if (trace<false, STATS>(S, rr, cur.mbTime, INFINITY, INFINITY, nx.h, cn)) {
-                    nx.r = rr; nx.eye = rr.o; nx.medium = f.rMedium; nx.mbTime = cur.mbTime;
-                    nx.depth = f.depth - 1;
-                    nx.key = child_key(f.key, 1);
-                    cur = nx;
-                    descended = true;
-                    break;
-                }
-                value = env_or_zero(S, f.reflDir);      // refracted miss uses the reflected dir (:408)
-                vHit = false;
-                continue;
+                descended = true;
+                break;
             }
             f3 term;
             if (f.kind == FK_MIRROR) {

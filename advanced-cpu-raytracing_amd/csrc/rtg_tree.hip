@@ -1,0 +1,599 @@
+// Wavefront ray trees: the mirror / conductor / dielectric recursion of PerformShading
+// (raytracer.cpp:65-134, 208-472) as levels of compacted ray queues, for scenes whose
+// materials spawn secondary rays (the fused kernel keeps one thread per pixel walking
+// the whole tree with a per-thread stack; that costs 256 VGPRs and scratch).
+//
+// Per sample pass, level L = 0, 1, ... holds every ray of depth L of every pixel's tree:
+//
+//   k_tree_gen      level 0: the camera rays (GenerateRay, raytracer.cpp:661-699)
+//   k_tree_trace    closest hit of every ray of the level (lean traversal kernel)
+//   k_tree_shade    one node per hit: surface, ambient, per-light Shade terms and their
+//                   shadow rays (queued per block), the node's kind and its child rays
+//                   (queued per block, two slots per node); misses get their value here
+//   k_shadow        the level's shadow rays (the pipeline's any-hit kernel)
+//   k_tree_scan     prefix over the per-block child counts -> next level size
+//   k_tree_compact  child rays into the next level's dense arrays, child links
+//   ...
+//   k_tree_resolve  levels deepest first: colour = base + unoccluded terms in light order,
+//                   then the reference's combine with the children's values (mirror,
+//                   conductor, total internal reflection, Fresnel reflect + refract with
+//                   Beer's law); level 0 writes the pixel (or its spp accumulation)
+//
+// Every value is computed by the same expressions in the same order as the recursion
+// (rtg_mega.hip / the reference), so the result is bit-identical to the fused kernel.
+#include <vector>
+
+#include "rtg_common.hpp"
+#include "rtg_kernels.hpp"
+
+namespace rtg {
+
+enum : int { TK_FINAL = 0, TK_LEAF = 1, TK_ADDZERO = 2, TK_MIRROR = 3, TK_CONDUCTOR = 4, TK_TIR = 5, TK_DIEL = 6 };
+enum : int { TK_LIT = 16 };
+enum : int { TM_ZERO = 0, TM_ENV = 1 };
+
+__global__ __launch_bounds__(256) void k_tree_gen(const DevCamera C, const RenderParams P, const int sample,
+                                                  const TreeLevel L0, const int pixel_base) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= L0.n) return;
+    const int pixel = pixel_base + i;
+    const int px = pixel % C.width, py = pixel / C.width;
+    const uint64_t key = root_key(P.seed, pixel, sample);
+    float mbTime;
+    Ray r = camera_ray(C, px, py, key, mbTime);
+    L0.o[i] = make_float4(r.o.x, r.o.y, r.o.z, 1.0f);
+    L0.d[i] = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(0));
+    L0.key[i] = key;
+}
+
+template <bool STATS, int FEAT>
+__global__ __launch_bounds__(256) void k_tree_trace(const DevScene S, const TreeLevel L, const int level,
+                                                    DevCounters* counters) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    Cnt<STATS> cn;
+    if (i < L.n) {
+        const float4 o = L.o[i], d = L.d[i];
+        Ray r;
+        r.o = mk(o.x, o.y, o.z);
+        r.d = mk(d.x, d.y, d.z);
+        if (level == 0) cn.cam();
+        else cn.sec();
+        Hit h;
+        trace<false, STATS, FEAT>(S, r, 0.f, INFINITY, INFINITY, h, cn);
+        L.t[i] = h.t;
+        L.obj[i] = h.obj;
+        L.face[i] = h.face;
+    }
+    flush_counters<STATS>(cn, counters);
+}
+
+// wave-aggregated append into a block segment (ballot + mbcnt rank + one LDS atomic)
+DEV int seg_append(bool want, int* lds_count) {
+    const unsigned long long mask = __ballot(want);
+    if (!mask) return -1;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)mask) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(lds_count, __popcll(mask));
+    base = __shfl(base, leader);
+    return want ? base + __popcll(mask & ((1ull << lane) - 1ull)) : -1;
+}
+
+template <bool STATS>
+__global__ __launch_bounds__(256) void k_tree_shade(const DevScene S, const DevCamera C, const TreeLevel L,
+                                                    const int level, const int pixel_base, const TreeSegs G,
+                                                    DevCounters* counters) {
+    __shared__ int nShadow, nChild;
+    if (threadIdx.x == 0) { nShadow = 0; nChild = 0; }
+    __syncthreads();
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const bool valid = i < L.n;
+    Cnt<STATS> cn;
+    ShadeCtx c;
+    bool lit = false;
+    f3 w_o = mk(0, 0, 0);
+    uint64_t key = 0;
+    // children to spawn: count (0..2), rays
+    int nch = 0;
+    Ray ch0, ch1;
+    float med0 = 1.0f, med1 = 1.0f;
+    f3 miss0 = mk(0, 0, 0), miss1 = mk(0, 0, 0);
+    int mm0 = TM_ZERO, mm1 = TM_ZERO;
+    int depth = 0;
+    if (valid) {
+        const float4 o = L.o[i], d = L.d[i];
+        Ray r;
+        r.o = mk(o.x, o.y, o.z);
+        r.d = mk(d.x, d.y, d.z);
+        const float medium = o.w;
+        depth = S.max_depth - __float_as_int(d.w);
+        key = L.key[i];
+        const int obj = L.obj[i];
+        if (obj < 0) {
+            f3 v;
+            if (level == 0) {
+                const int pixel = pixel_base + i;
+                v = miss_color(S, C, pixel % C.width, pixel / C.width, r.d);
+            } else {
+                const float4 m = L.miss[i];
+                v = __float_as_int(m.w) == TM_ENV
+                        ? (S.num_env > 0 ? env_sample(S, 0, mk(m.x, m.y, m.z)) : mk(0, 0, 0))
+                        : mk(0, 0, 0);
+            }
+            L.base[i] = make_float4(0, 0, 0, __int_as_float(TK_FINAL));
+            L.value[i] = make_float4(v.x, v.y, v.z, __int_as_float(0));
+        } else {
+            const DevObject& ob = S.objects[obj];
+            Hit h;
+            h.t = L.t[i];
+            h.obj = obj;
+            h.face = L.face[i];
+            h.o = r.o;
+            c.ob = &ob;
+            c.mat = &S.materials[ob.material];
+            c.s = surface<STATS>(S, r, 0.f, h, cn);
+            const f3 eye = level == 0 ? ld3(C.pos) : r.o;
+            w_o = makeUnit(sub(eye, c.s.p));
+            const DevMaterial& mat = *c.mat;
+            const bool inside = medium > 1.00001f;
+            if (mat.type == 3) {                                        // Emissive (raytracer.cpp:81-84)
+                const f3 e = muls(muls(ld3(mat.radiance), 2.0f), (float)RT_PI);
+                L.base[i] = make_float4(0, 0, 0, __int_as_float(TK_FINAL));
+                L.value[i] = make_float4(e.x, e.y, e.z, __int_as_float(1));
+            } else if (ob.tex_replace_all >= 0) {                       // replace_all (:87-89)
+                const f3 e = tex_rgb(S, S.textures[ob.tex_replace_all], c.s.u, c.s.v);
+                L.base[i] = make_float4(0, 0, 0, __int_as_float(TK_FINAL));
+                L.value[i] = make_float4(e.x, e.y, e.z, __int_as_float(1));
+            } else {
+                f3 color = mk(0, 0, 0);
+                if (!inside) {
+                    color = add(color, mulv(mk(S.ambient[0], S.ambient[1], S.ambient[2]), ld3(mat.ambient)));
+                    lit = true;
+                }
+                const f3 n = c.s.n, hp = c.s.p;
+                int kind = TK_LEAF;
+                float4 coef = make_float4(0, 0, 0, 0);
+                float rT = 0.f;
+                if (mat.type == 0) {                                    // Mirror (raytracer.cpp:442-472)
+                    if (depth <= 0) {
+                        kind = TK_ADDZERO;
+                    } else {
+                        kind = TK_MIRROR;
+                        coef = make_float4(mat.mirror[0], mat.mirror[1], mat.mirror[2], 0.f);
+                        ch0.d = reflect(n, w_o, mat.roughness, key, RP_ROUGH_REFL);
+                        ch0.o = add(hp, muls(n, S.eps));
+                        med0 = 1.0f;
+                        miss0 = ch0.d;
+                        mm0 = TM_ENV;
+                        nch = 1;
+                    }
+                } else if (mat.type == 2) {                             // Conductor (raytracer.cpp:208-254)
+                    if (depth <= 0) {
+                        kind = TK_ADDZERO;
+                    } else {
+                        f3 dd = neg(w_o);
+                        float cosTheta = -dot(dd, n);
+                        float n2 = mat.refractive_index, k2 = mat.absorption_index;
+                        float n2k2 = n2 * n2 + k2 * k2;
+                        float n2cosTheta2 = 2 * n2 * cosTheta;
+                        float cosThetaSqr = cosTheta * cosTheta;
+                        float rs = (n2k2 - n2cosTheta2 + cosThetaSqr) / (n2k2 + n2cosTheta2 + cosThetaSqr);
+                        float rp = (n2k2 * cosThetaSqr - n2cosTheta2 + 1) / (n2k2 * cosThetaSqr + n2cosTheta2 + 1);
+                        float reflectRatio = (float)(0.5 * (rs + rp));
+                        if (!(reflectRatio > 0.0001)) {
+                            kind = TK_ADDZERO;
+                        } else {
+                            kind = TK_CONDUCTOR;
+                            coef = make_float4(mat.mirror[0], mat.mirror[1], mat.mirror[2], reflectRatio);
+                            ch0.d = reflect(n, w_o, mat.roughness, key, RP_ROUGH_REFL);
+                            ch0.o = add(hp, muls(n, S.eps));
+                            med0 = 1.0f;
+                            mm0 = TM_ZERO;
+                            nch = 1;
+                        }
+                    }
+                } else if (mat.type == 1) {                             // Dielectric (raytracer.cpp:261-415)
+                    if (depth <= 0) {
+                        kind = TK_ADDZERO;
+                    } else {
+                        float n1 = medium, n2 = mat.refractive_index;
+                        f3 dd = neg(w_o);
+                        f3 modN = n;
+                        float cosTheta = -dot(dd, modN);
+                        bool isEntering = cosTheta > 0.f;
+                        float objN = n2;
+                        if (!isEntering) {
+                            n1 = n2; n2 = 1.0f; objN = 1.0f;
+                            cosTheta = fabsf(cosTheta);
+                            modN = neg(modN);
+                        }
+                        float rr = n1 / n2;
+                        float sinThetaSqr = 1 - (cosTheta * cosTheta);
+                        float criticalTerm = rr * rr * sinThetaSqr;
+                        if (criticalTerm > 1) {
+                            kind = TK_TIR;
+                            ch0.d = reflect(modN, w_o, mat.roughness, key, RP_ROUGH_REFL);
+                            ch0.o = add(hp, muls(modN, S.eps));
+                            med0 = medium;
+                            mm0 = TM_ZERO;
+                            nch = 1;
+                        } else {
+                            float cosPhi = sqrtf(1 - criticalTerm);
+                            float n2cosTheta = n2 * cosTheta;
+                            float n1cosPhi = n1 * cosPhi;
+                            float rpar = (n2cosTheta - n1cosPhi) / (n2cosTheta + n1cosPhi);
+                            float rperp = (n1 * cosTheta - n2 * cosPhi) / (n1 * cosTheta + n2 * cosPhi);
+                            float rReflect = (rpar * rpar + rperp * rperp) / 2;
+                            kind = TK_DIEL;
+                            coef = make_float4(0, 0, 0, rReflect);
+                            rT = 1 - rReflect;
+                            ch0.d = reflect(modN, w_o, mat.roughness, key, RP_ROUGH_REFL);
+                            ch0.o = add(hp, muls(modN, S.eps));
+                            med0 = isEntering ? objN : 1.0f;
+                            miss0 = ch0.d;
+                            mm0 = TM_ENV;
+                            // refracted ray (raytracer.cpp:362-392)
+                            f3 wr = sub(muls(add(dd, muls(modN, cosTheta)), rr), muls(modN, cosPhi));
+                            if (mat.roughness > 0.001) {
+                                f3 u, v;
+                                onb(wr, u, v);
+                                float psi1 = rnd(key, RP_ROUGH_REFR, 0) - 0.5f;
+                                float psi2 = rnd(key, RP_ROUGH_REFR, 1) - 0.5f;
+                                wr = makeUnit(add(wr, muls(add(muls(u, psi1), muls(v, psi2)), mat.roughness)));
+                            } else {
+                                wr = makeUnit(wr);
+                            }
+                            ch1.o = add(hp, muls(neg(modN), S.eps));
+                            ch1.d = wr;
+                            med1 = isEntering ? objN : 1.0f;
+                            miss1 = ch0.d;                  // refracted miss: reflected dir (:408)
+                            mm1 = TM_ENV;
+                            nch = 2;
+                        }
+                    }
+                }
+                L.base[i] = make_float4(color.x, color.y, color.z, __int_as_float(kind | (lit ? TK_LIT : 0)));
+                L.coef[i] = coef;
+                L.ext[i] = make_float4(rT, __int_as_float(ob.material), __int_as_float(-1), __int_as_float(-1));
+            }
+        }
+    }
+    // ---- light slots of lit nodes: Shade terms + shadow rays (SampleDirectLighting order)
+    const int ns = G.num_slots;
+    for (int l = 0; l < ns; ++l) {
+        LightSample ls;
+        if (lit) {
+            ls = light_sample(S, l, c.s.p, c.s.n, key);
+            const f3 t = shade(S, c, ls.w_i, w_o, ls.E);
+            L.term[(size_t)i * ns + l] = make_float4(t.x, t.y, t.z, 0.f);
+            L.occ[(size_t)i * ns + l] = 0;
+        }
+        const bool want = lit && ls.shadow;
+        const int qi = seg_append(want, &nShadow);
+        if (want) {
+            cn.shd();
+            const size_t q = (size_t)blockIdx.x * 256 * ns + qi;
+            G.q_o[q] = make_float4(ls.sr.o.x, ls.sr.o.y, ls.sr.o.z, ls.minT);
+            G.q_d[q] = make_float4(ls.sr.d.x, ls.sr.d.y, ls.sr.d.z, ls.limit);
+            G.q_slot[q] = i * ns + l;
+        }
+    }
+    // ---- child rays (slot 0, slot 1)
+    for (int s = 0; s < 2; ++s) {
+        const bool want = nch > s;
+        const int ci = seg_append(want, &nChild);
+        if (want) {
+            const size_t q = (size_t)blockIdx.x * 512 + ci;
+            const Ray& r = s == 0 ? ch0 : ch1;
+            const f3 m = s == 0 ? miss0 : miss1;
+            G.c_o[q] = make_float4(r.o.x, r.o.y, r.o.z, s == 0 ? med0 : med1);
+            G.c_d[q] = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(S.max_depth - depth + 1));
+            G.c_key[q] = child_key(key, s);
+            G.c_miss[q] = make_float4(m.x, m.y, m.z, __int_as_float(s == 0 ? mm0 : mm1));
+            G.c_parent[q] = i | (s << 30);
+        }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        G.q_count[blockIdx.x] = nShadow;
+        G.c_count[blockIdx.x] = nChild;
+    }
+    flush_counters<STATS>(cn, counters);
+}
+
+// exclusive prefix over the per-block child counts (one block); total -> offs[nb]
+__global__ __launch_bounds__(1024) void k_tree_scan(const int* __restrict__ cnt, int nb, int* __restrict__ offs) {
+    __shared__ int part[1024];
+    const int t = threadIdx.x;
+    const int per = (nb + 1023) / 1024;
+    const int b0 = t * per, b1 = min(nb, b0 + per);
+    int s = 0;
+    for (int b = b0; b < b1; ++b) s += cnt[b];
+    part[t] = s;
+    __syncthreads();
+    for (int w = 1; w < 1024; w <<= 1) {
+        const int v = t >= w ? part[t - w] : 0;
+        __syncthreads();
+        part[t] += v;
+        __syncthreads();
+    }
+    int run = part[t] - s;
+    for (int b = b0; b < b1; ++b) {
+        offs[b] = run;
+        run += cnt[b];
+    }
+    if (t == 1023) offs[nb] = part[1023];
+}
+
+__global__ __launch_bounds__(256) void k_tree_compact(const TreeSegs G, const int* __restrict__ offs,
+                                                      const TreeLevel cur, const TreeLevel nxt) {
+    const int b = blockIdx.x;
+    const int n = G.c_count[b], base = offs[b];
+    for (int k = threadIdx.x; k < n; k += 256) {
+        const size_t q = (size_t)b * 512 + k;
+        const int dst = base + k;
+        nxt.o[dst] = G.c_o[q];
+        nxt.d[dst] = G.c_d[q];
+        nxt.key[dst] = G.c_key[q];
+        nxt.miss[dst] = G.c_miss[q];
+        const int p = G.c_parent[q];
+        const int parent = p & 0x3FFFFFFF, slot = p >> 30;
+        int* ext = reinterpret_cast<int*>(&cur.ext[parent]);
+        ext[2 + slot] = dst;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_tree_resolve(const DevScene S, const DevCamera C, const RenderParams P,
+                                                      const int sample, const int first, const int last,
+                                                      const TreeLevel L, const TreeLevel Lc, const int level,
+                                                      const int num_slots, const int pixel_base,
+                                                      float* __restrict__ hdr, unsigned char* __restrict__ ldrOut,
+                                                      float4* __restrict__ accum) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= L.n) return;
+    const float4 b = L.base[i];
+    const int kb = __float_as_int(b.w);
+    const int kind = kb & 15;
+    f3 value;
+    if (kind == TK_FINAL) {
+        const float4 v = L.value[i];
+        value = mk(v.x, v.y, v.z);
+    } else {
+        f3 color = mk(b.x, b.y, b.z);
+        if (kb & TK_LIT) {
+            f3 sum = mk(0, 0, 0);
+            const size_t s0 = (size_t)i * num_slots;
+            for (int l = 0; l < num_slots; ++l)
+                if (!L.occ[s0 + l]) {
+                    const float4 t = L.term[s0 + l];
+                    sum = add(sum, mk(t.x, t.y, t.z));
+                }
+            color = add(color, sum);
+        }
+        if (kind == TK_LEAF) {
+            value = color;
+        } else if (kind == TK_ADDZERO) {
+            value = add(color, mk(0, 0, 0));
+        } else {
+            const float4 cf = L.coef[i];
+            const float4 ex = L.ext[i];
+            const f3 coef = mk(cf.x, cf.y, cf.z);
+            const DevMaterial& pm = S.materials[__float_as_int(ex.y)];
+            auto child = [&](int slot, f3& v, bool& vHit, float& vT, float& vMed) {
+                const int ci = __float_as_int(slot == 0 ? ex.z : ex.w);
+                const float4 cv = Lc.value[ci];
+                v = mk(cv.x, cv.y, cv.z);
+                vHit = __float_as_int(cv.w) != 0;
+                vT = Lc.t[ci];
+                vMed = Lc.o[ci].w;
+            };
+            f3 v0;
+            bool h0;
+            float t0, m0;
+            child(0, v0, h0, t0, m0);
+            f3 term;
+            if (kind == TK_MIRROR) {
+                term = mulv(coef, v0);
+            } else if (kind == TK_CONDUCTOR) {
+                term = muls(h0 ? mulv(coef, v0) : mk(0, 0, 0), cf.w);
+            } else if (kind == TK_TIR) {
+                term = h0 ? ((m0 > 1.0001) ? beer(t0, pm.absorption, v0) : v0) : mk(0, 0, 0);
+            } else {
+                const f3 refl = (h0 && m0 > 1.00001f) ? beer(t0, pm.absorption, v0) : v0;
+                f3 v1;
+                bool h1;
+                float t1, m1;
+                child(1, v1, h1, t1, m1);
+                const f3 refr = (h1 && m1 > 1.001f) ? beer(t1, pm.absorption, v1) : v1;
+                term = add(muls(refl, cf.w), muls(refr, ex.x));
+            }
+            value = add(color, term);
+        }
+    }
+    if (level > 0) {
+        L.value[i] = make_float4(value.x, value.y, value.z, __int_as_float(L.obj[i] >= 0 ? 1 : 0));
+        return;
+    }
+    // level 0: the pixel (RenderPixel's colour), spp accumulation as k_resolve
+    const int pixel = pixel_base + i;
+    if (C.spp <= 1 && !P.accum_only) {
+        const size_t idx = 3 * (size_t)pixel;
+        if (hdr) { hdr[idx] = value.x; hdr[idx + 1] = value.y; hdr[idx + 2] = value.z; }
+        if (ldrOut) { ldrOut[idx] = ldr(value.x); ldrOut[idx + 1] = ldr(value.y); ldrOut[idx + 2] = ldr(value.z); }
+        return;
+    }
+    const float gw = sample_weight(C.spp, sample, root_key(P.seed, pixel, sample));
+    float4 a = first ? make_float4(0.f, 0.f, 0.f, 0.f) : accum[pixel];
+    a.x += value.x * gw;
+    a.y += value.y * gw;
+    a.z += value.z * gw;
+    a.w += gw;
+    accum[pixel] = a;
+    if (last && !P.accum_only) {
+        const f3 cc = mk(a.x / a.w, a.y / a.w, a.z / a.w);
+        const size_t idx = 3 * (size_t)pixel;
+        if (hdr) { hdr[idx] = cc.x; hdr[idx + 1] = cc.y; hdr[idx + 2] = cc.z; }
+        if (ldrOut) { ldrOut[idx] = ldr(cc.x); ldrOut[idx + 1] = ldr(cc.y); ldrOut[idx + 2] = ldr(cc.z); }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Host side
+// ---------------------------------------------------------------------------
+namespace {
+
+template <typename T>
+hipError_t grow(T*& p, size_t& cap, size_t n) {
+    if (n <= cap) return hipSuccess;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    cap = 0;
+    const size_t want = n + n / 4 + 1024;
+    hipError_t e = hipMalloc(&p, want * sizeof(T));
+    if (e == hipSuccess) cap = want;
+    return e;
+}
+
+}  // namespace
+
+struct TreeState {
+    struct Level {
+        TreeLevel L{};
+        size_t cap = 0, cap_slots = 0;
+        // separate capacities per array (grown together)
+        size_t co = 0, cd = 0, ck = 0, cm = 0, ct = 0, cob = 0, cf = 0, cb = 0, cc = 0, ce = 0, cv = 0, cte = 0, coc = 0;
+    };
+    std::vector<Level> levels;
+    TreeSegs G{};
+    size_t c_qo = 0, c_qd = 0, c_qs = 0, c_qc = 0, c_o = 0, c_d = 0, c_k = 0, c_m = 0, c_p = 0, c_cc = 0, c_off = 0;
+    int* offs = nullptr;
+    int* h_total = nullptr;     // pinned host word
+    ~TreeState() {
+        auto f = [](void* p) { if (p) (void)hipFree(p); };
+        for (auto& lv : levels) {
+            TreeLevel& L = lv.L;
+            f(L.o); f(L.d); f(L.key); f(L.miss); f(L.t); f(L.obj); f(L.face); f(L.base); f(L.coef); f(L.ext);
+            f(L.value); f(L.term); f(L.occ);
+        }
+        f(G.q_o); f(G.q_d); f(G.q_slot); f(G.q_count); f(G.c_o); f(G.c_d); f(G.c_key); f(G.c_miss); f(G.c_parent);
+        f(G.c_count); f(offs);
+        if (h_total) (void)hipHostFree(h_total);
+    }
+};
+
+static hipError_t ensure_level(TreeState::Level& lv, size_t n, int ns) {
+    TreeLevel& L = lv.L;
+    hipError_t e;
+#define G_(ptr, c, cnt) if ((e = grow(ptr, lv.c, cnt)) != hipSuccess) return e
+    G_(L.o, co, n); G_(L.d, cd, n); G_(L.key, ck, n); G_(L.miss, cm, n); G_(L.t, ct, n); G_(L.obj, cob, n);
+    G_(L.face, cf, n); G_(L.base, cb, n); G_(L.coef, cc, n); G_(L.ext, ce, n); G_(L.value, cv, n);
+    G_(L.term, cte, n * (size_t)(ns > 0 ? ns : 1)); G_(L.occ, coc, n * (size_t)(ns > 0 ? ns : 1));
+#undef G_
+    L.n = (int)n;
+    return hipSuccess;
+}
+
+static hipError_t ensure_segs(TreeState& T, size_t blocks, int ns) {
+    TreeSegs& G = T.G;
+    hipError_t e;
+    const size_t nq = blocks * 256 * (size_t)(ns > 0 ? ns : 1), nc = blocks * 512;
+#define G_(ptr, c, cnt) if ((e = grow(ptr, T.c, cnt)) != hipSuccess) return e
+    G_(G.q_o, c_qo, nq); G_(G.q_d, c_qd, nq); G_(G.q_slot, c_qs, nq); G_(G.q_count, c_qc, blocks);
+    G_(G.c_o, c_o, nc); G_(G.c_d, c_d, nc); G_(G.c_key, c_k, nc); G_(G.c_miss, c_m, nc); G_(G.c_parent, c_p, nc);
+    G_(G.c_count, c_cc, blocks); G_(T.offs, c_off, blocks + 1);
+#undef G_
+    G.num_slots = ns;
+    return hipSuccess;
+}
+
+void tree_destroy(TreeState* t) { delete t; }
+
+template <bool STATS, int FEAT>
+static hipError_t tree_pass(TreeState& T, const DevScene& S, const DevCamera& C, const RenderParams& P, int s,
+                            bool first, bool last, float* hdr, unsigned char* l, float4* accum, DevCounters* cnt,
+                            hipStream_t st, hipEvent_t* ev) {
+    const int ns = S.num_point + S.num_area + S.num_env + S.num_dir + S.num_spot;
+    const int npix = (P.row_end - P.row_begin) * C.width;
+    const int pixel_base = P.row_begin * C.width;
+    hipError_t e;
+    size_t n = (size_t)npix;
+    int level = 0;
+    if (ev) (void)hipEventRecord(ev[0], st);
+    for (;; ++level) {
+        if ((int)T.levels.size() <= level) T.levels.emplace_back();
+        if ((e = ensure_level(T.levels[level], n, ns)) != hipSuccess) return e;
+        TreeLevel& L = T.levels[level].L;
+        const int blocks = (int)((n + 255) / 256);
+        if ((e = ensure_segs(T, (size_t)blocks, ns)) != hipSuccess) return e;
+        if (level == 0) hipLaunchKernelGGL(k_tree_gen, dim3(blocks), dim3(256), 0, st, C, P, s, L, pixel_base);
+        hipLaunchKernelGGL((k_tree_trace<STATS, FEAT>), dim3(blocks), dim3(256), 0, st, S, L, level, cnt);
+        hipLaunchKernelGGL((k_tree_shade<STATS>), dim3(blocks), dim3(256), 0, st, S, C, L, level, pixel_base, T.G, cnt);
+        if (ns > 0) {
+            WaveBufs W{};
+            W.q_o = T.G.q_o; W.q_d = T.G.q_d; W.q_slot = T.G.q_slot; W.q_count = T.G.q_count;
+            W.occ = L.occ;
+            W.num_slots = ns;
+            hipLaunchKernelGGL((k_shadow<STATS, FEAT>), dim3(blocks, ns), dim3(256), 0, st, S, W, cnt);
+        }
+        hipLaunchKernelGGL(k_tree_scan, dim3(1), dim3(1024), 0, st, T.G.c_count, blocks, T.offs);
+        if ((e = hipMemcpyAsync(T.h_total, T.offs + blocks, sizeof(int), hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return e;
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+        const size_t nn = (size_t)*T.h_total;
+        if (nn == 0) break;
+        if ((int)T.levels.size() <= level + 1) T.levels.emplace_back();
+        if ((e = ensure_level(T.levels[level + 1], nn, ns)) != hipSuccess) return e;
+        hipLaunchKernelGGL(k_tree_compact, dim3(blocks), dim3(256), 0, st, T.G, T.offs, T.levels[level].L,
+                           T.levels[level + 1].L);
+        n = nn;
+    }
+    if (ev) (void)hipEventRecord(ev[1], st);
+    for (int lv = level; lv >= 0; --lv) {
+        const TreeLevel& L = T.levels[lv].L;
+        const TreeLevel& Lc = lv < level ? T.levels[lv + 1].L : L;
+        const int blocks = (int)((L.n + 255) / 256);
+        hipLaunchKernelGGL(k_tree_resolve, dim3(blocks), dim3(256), 0, st, S, C, P, s, (int)first, (int)last, L,
+                           Lc, lv, ns, pixel_base, hdr, l, accum);
+    }
+    if (ev) (void)hipEventRecord(ev[2], st);
+    return hipGetLastError();
+}
+
+template <bool STATS, int FEAT>
+static hipError_t tree_run(TreeState& T, const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr,
+                           unsigned char* l, float4* accum, DevCounters* cnt, hipStream_t st, hipEvent_t* ev) {
+    if (!T.h_total) {
+        hipError_t e = hipHostMalloc(&T.h_total, sizeof(int));
+        if (e != hipSuccess) return e;
+    }
+    for (int s = P.sample_begin; s < P.sample_begin + P.sample_count; ++s) {
+        const bool first = s == P.sample_begin, last = s == P.sample_begin + P.sample_count - 1;
+        hipError_t e = tree_pass<STATS, FEAT>(T, S, C, P, s, first, last, hdr, l, accum, cnt, st, last ? ev : nullptr);
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
+
+hipError_t launch_tree(TreeState*& T, const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr,
+                       unsigned char* l, float4* accum, DevCounters* cnt, bool stats, int feat, hipStream_t st,
+                       hipEvent_t* ev) {
+    if (!T) T = new TreeState();
+    const bool big = (feat & FEAT_BIGLEAF) != 0;
+    const int base = feat & ~FEAT_BIGLEAF;
+#define RTG_TREE(F)                                                                     \
+    return stats ? tree_run<true, F>(*T, S, C, P, hdr, l, accum, cnt, st, ev)           \
+                 : tree_run<false, F>(*T, S, C, P, hdr, l, accum, cnt, st, ev)
+    if (base == 0) {
+        if (big) RTG_TREE(FEAT_BIGLEAF);
+        RTG_TREE(0);
+    }
+    if (base == FEAT_SPHERE) {
+        if (big) RTG_TREE(FEAT_SPHERE | FEAT_BIGLEAF);
+        RTG_TREE(FEAT_SPHERE);
+    }
+    if (big) RTG_TREE(FEAT_ALL);
+    RTG_TREE(FEAT_ALL & ~FEAT_BIGLEAF);
+#undef RTG_TREE
+}
+
+}  // namespace rtg

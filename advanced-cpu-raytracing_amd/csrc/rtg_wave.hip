@@ -209,23 +209,6 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene S, const DevCamera
     flush_counters<STATS>(cn, counters);
 }
 
-template <bool STATS, int FEAT>
-// grid (shade blocks, slots): block (b, c) takes entries [256c, 256c+256) of segment b
-__global__ __launch_bounds__(256) void k_shadow(const DevScene S, const WaveBufs W, DevCounters* counters) {
-    const int k = blockIdx.y * 256 + threadIdx.x;
-    const size_t q = ((size_t)blockIdx.x * W.num_slots) * 256 + k;
-    Cnt<STATS> cn;
-    if (k < W.q_count[blockIdx.x]) {
-        const float4 o = W.q_o[q], d = W.q_d[q];
-        Ray r;
-        r.o = mk(o.x, o.y, o.z);
-        r.d = mk(d.x, d.y, d.z);
-        Hit h;
-        if (trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn)) W.occ[W.q_slot[q]] = 1;
-    }
-    flush_counters<STATS>(cn, counters);
-}
-
 __global__ __launch_bounds__(256) void k_resolve(const DevCamera C, const RenderParams P, const int sample,
                                                  const int first, const int last, const WaveBufs W,
                                                  float* __restrict__ hdr, unsigned char* __restrict__ ldrOut,

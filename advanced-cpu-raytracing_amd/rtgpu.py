@@ -27,6 +27,7 @@ RTG_RENDER_COUNT_STATS = 1
 RTG_RENDER_ACCUM_ONLY = 2
 RTG_RENDER_FUSED = 4
 RTG_RENDER_TIMING = 8
+RTG_RENDER_TREE = 16
 
 
 class RTGError(RuntimeError):

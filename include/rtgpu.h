@@ -260,8 +260,12 @@ enum rtg_render_flags {
                                      when samples are split across devices            */
     RTG_RENDER_FUSED = 4,         /* force the fused per-pixel kernel even where the
                                      wavefront pipeline applies (for cross-checks)     */
-    RTG_RENDER_TIMING = 8         /* record HIP events around every kernel of the
+    RTG_RENDER_TIMING = 8,        /* record HIP events around every kernel of the
                                      render (last sample pass); see rtg_scene_timings */
+    RTG_RENDER_TREE = 16          /* force the wavefront ray-tree pipeline for scenes with
+                                     mirror / conductor / dielectric materials (default:
+                                     frames of >= 2^21 pixel-samples; it synchronises the
+                                     stream once per tree level)                       */
 };
 
 typedef struct {
@@ -314,7 +318,8 @@ int rtg_scene_reset_stats(rtg_scene* scene);
 /* Kernel durations (ms, HIP events on the render's stream) of the last render issued
  * with RTG_RENDER_TIMING, for its last sample pass; synchronises on that render.
  * Wavefront pipeline: names "k_primary", "k_shade", "k_shadow", "k_resolve"; fused
- * kernel: "k_render".  Writes up to `cap` entries; *count = number of stages. */
+ * kernel: "k_render"; ray-tree pipeline: "tree_levels" (all levels' trace / shade /
+ * shadow kernels), "tree_resolve".  Writes up to `cap` entries; *count = number of stages. */
 int rtg_scene_timings(rtg_scene* scene, float* ms, const char** names, int32_t cap, int32_t* count);
 
 /* ------------------------------------------------------------------------- */
