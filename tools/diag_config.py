@@ -26,7 +26,7 @@ os.chdir(d)
 hs = rtgpu.HostScene(xml)
 ds = rtgpu.DeviceScene(hs, 0)
 print(cfg, hs.counts(), hs.camera(0), flush=True)
-for flags, name in ((0, "default"), (rtgpu.RTG_RENDER_FUSED, "fused")):
+for flags, name in ((0, "default"), (rtgpu.RTG_RENDER_FUSED, "fused"), (rtgpu.RTG_RENDER_TREE, "tree")):
     ds.reset_stats()
     ds.render(0, flags=flags | rtgpu.RTG_RENDER_COUNT_STATS)
     st = ds.stats()
