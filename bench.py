@@ -160,7 +160,7 @@ def kernel_bytes(st, W, H):
     ext = 32 * st["node_visits"] + 36 * st["tri_tests"] + 64 * ext_rays
     shd = 32 * st["shadow_node_visits"] + 36 * st["shadow_tri_tests"] + 64 * st["shadow_rays"]
     return {"k_primary": ext, "k_shadow": shd, "k_render": ext + shd + 15 * W * H,
-            "frame": ext + shd + 15 * W * H}
+            "tree_levels": ext + shd, "frame": ext + shd + 15 * W * H}
 
 
 def main():
@@ -217,13 +217,14 @@ def main():
 
         value = world * rays * args.steps / elapsed / 1e6
         ktimes = kernel_times(ds, torch, hdr, ldr, args.steps, seed)
-        kbytes = kernel_bytes(st, W, H)
+        # the library times the kernels of the last sample pass: bytes of one pass
+        kbytes = {k: v / max(1, cam["spp"]) for k, v in kernel_bytes(st, W, H).items()}
         # the dominant traversal kernel: k_primary (wavefront) or k_render (fused)
         dom = max((k for k in ktimes if k in kbytes), key=lambda k: ktimes[k])
         algo_bytes = kbytes[dom]
         achieved = algo_bytes / (ktimes[dom] * 1e-3) / 1e9
-        frame_gbs = kbytes["frame"] / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic(dom)
+        frame_gbs = kbytes["frame"] * max(1, cam["spp"]) / (kern_ms * 1e-3) / 1e9
+        traffic, traffic_src = pmc_traffic(dom) if args.config == "headline" else (None, None)
         result = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -262,7 +263,7 @@ def main():
                 "algo_bytes_per_launch": int(algo_bytes),
                 "kernels_ms": {k: round(v, 4) for k, v in ktimes.items()},
                 "frame_ms": round(kern_ms, 4),
-                "frame_algo_bytes": int(kbytes["frame"]),
+                "frame_algo_bytes": int(kbytes["frame"] * max(1, cam["spp"])),
                 "frame_frac": round(frame_gbs / HBM_PEAK_GBS, 4),
             },
             "cpu_baseline": None,
