@@ -1020,8 +1020,12 @@ void Loader::flatten() {
         if (S.materials[o.material].type == RTG_MAT_EMISSIVE) o.flags |= RTG_OBJF_SHADOW_SKIP;
         if (!S.meshes[o.mesh].has_uv) o.flags |= RTG_OBJF_NORMAL_TWICE;
         if (sh.motionBlur) o.flags |= RTG_OBJF_MOTION_BLUR;
-        o.tex_diffuse = sh.tex[0]; o.tex_specular = sh.tex[1]; o.tex_normal = sh.tex[2];
-        o.tex_bump = sh.tex[3]; o.tex_replace_all = sh.tex[4];
+        o.tex_diffuse = sh.tex[0]; o.tex_specular = sh.tex[1]; o.tex_replace_all = sh.tex[4];
+        // normal / bump maps are read by IntersectFace of the BASE mesh (mesh.cpp:263-358,
+        // `this` is the base Mesh for an instance): an instance takes its base mesh's maps
+        const ShapeRec& geoOwner = sh.isInstance ? shapes[sh.parentShape] : sh;
+        o.tex_normal = geoOwner.tex[2];
+        o.tex_bump = geoOwner.tex[3];
         sh.xf.inverse.to(o.inv_transform);
         sh.xf.invTranspose.to(o.inv_transpose);
         sh.xf.transform.to(o.transform);

@@ -83,6 +83,7 @@ struct rtg_scene {
     DevBuf<int2> node_ext;
     DevBuf<int> env_images;
     DevBuf<float2> face_uv;
+    DevBuf<float4> face_v12;
     DevBuf<rtg::DevObject> objects;
     DevBuf<rtg::DevMaterial> materials;
     DevBuf<rtg::DevBrdf> brdfs;
@@ -186,8 +187,17 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
         return set_err(RTG_ERR_UNSUPPORTED, "MaxRecursionDepth %d > %d", d->max_recursion_depth, rtg::max_supported_depth());
     for (int i = 0; i < d->num_objects; ++i) {
         const rtg_object& o = d->objects[i];
-        if (o.tex_normal >= 0 || o.tex_bump >= 0)
-            return set_err(RTG_ERR_UNSUPPORTED, "normal / bump mapping is not implemented on the GPU path yet");
+        if (o.kind == RTG_OBJ_SPHERE && o.tex_normal >= 0)
+            return set_err(RTG_ERR_UNSUPPORTED, "sphere %d: normal map (the reference leaves the normal unset, "
+                           "sphere.cpp:95-113)", i);
+        if ((o.tex_normal >= d->num_textures) || (o.tex_bump >= d->num_textures))
+            return set_err(RTG_ERR_INVALID, "object %d: bad normal / bump texture", i);
+        if (o.tex_normal >= 0 && d->textures[o.tex_normal].kind == RTG_TEX_IMAGE &&
+            (d->textures[o.tex_normal].image < 0 || d->textures[o.tex_normal].image >= d->num_images))
+            return set_err(RTG_ERR_INVALID, "object %d: normal map without an image", i);
+        if (o.tex_bump >= 0 && d->textures[o.tex_bump].kind == RTG_TEX_IMAGE &&
+            (d->textures[o.tex_bump].image < 0 || d->textures[o.tex_bump].image >= d->num_images))
+            return set_err(RTG_ERR_INVALID, "object %d: bump map without an image", i);
         if (o.material < 0 || o.material >= d->num_materials) return set_err(RTG_ERR_INVALID, "object %d: bad material", i);
         if (o.kind != RTG_OBJ_SPHERE && (o.mesh < 0 || o.mesh >= d->num_meshes))
             return set_err(RTG_ERR_INVALID, "object %d: bad mesh", i);
@@ -277,6 +287,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     // ---- objects
     std::vector<rtg::DevObject> objs(d->num_objects);
     int feat = 0;
+    bool anyMapped = false;
     for (int i = 0; i < d->num_objects; ++i) {
         const rtg_object& o = d->objects[i];
         rtg::DevObject& D = objs[i];
@@ -292,6 +303,12 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
         D.tex_diffuse = o.tex_diffuse;
         D.tex_specular = o.tex_specular;
         D.tex_replace_all = o.tex_replace_all;
+        // maps only act where the reference reads them: mesh faces with UVs (mesh.cpp:245-358)
+        // and sphere bump maps (sphere.cpp:116-170)
+        const bool uvmesh = o.kind != RTG_OBJ_SPHERE && d->meshes[o.mesh].has_uv;
+        D.tex_normal = uvmesh ? o.tex_normal : -1;
+        D.tex_bump = (uvmesh && o.tex_normal < 0) || o.kind == RTG_OBJ_SPHERE ? o.tex_bump : -1;
+        if (D.tex_normal >= 0 || D.tex_bump >= 0) { D.flags |= rtg::OBJF_MAPPED; anyMapped = true; }
         for (int k = 0; k < 3; ++k) { D.bmin[k] = o.bbox_min[k]; D.bmax[k] = o.bbox_max[k]; }
         f4(D.mbv, o.motion_blur);
         f4(D.center, o.center, o.radius);
@@ -400,6 +417,15 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
 
     HIP_TRY(sc->nodes.upload(nodes)); HIP_TRY(sc->node_ext.upload(next)); HIP_TRY(sc->tris.upload(tris));
     HIP_TRY(sc->face_n.upload(fn)); HIP_TRY(sc->face_uv.upload(fuv));
+    if (anyMapped) {
+        std::vector<float4> v12(2 * d->num_faces);
+        for (int64_t f = 0; f < d->num_faces; ++f) {
+            const rtg_face& F = d->faces[f];
+            v12[2 * f] = make_float4(F.v1.x, F.v1.y, F.v1.z, 0.f);
+            v12[2 * f + 1] = make_float4(F.v2.x, F.v2.y, F.v2.z, 0.f);
+        }
+        HIP_TRY(sc->face_v12.upload(v12));
+    }
     HIP_TRY(sc->objects.upload(objs)); HIP_TRY(sc->materials.upload(mats)); HIP_TRY(sc->brdfs.upload(brdfs));
     HIP_TRY(sc->textures.upload(texs)); HIP_TRY(sc->images.upload(imgs)); HIP_TRY(sc->texels.upload(pool));
     HIP_TRY(sc->point_lights.upload(pls)); HIP_TRY(sc->area_lights.upload(als)); HIP_TRY(sc->dir_lights.upload(dls));
@@ -418,6 +444,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     std::memset(&S, 0, sizeof(S));
     S.nodes = sc->nodes.p; S.node_ext = sc->node_ext.p; S.tris = sc->tris.p; S.face_n = sc->face_n.p;
     S.face_uv = sc->face_uv.p;
+    S.face_v12 = sc->face_v12.p;
     S.objects = sc->objects.p; S.materials = sc->materials.p; S.brdfs = sc->brdfs.p;
     S.textures = sc->textures.p; S.images = sc->images.p; S.texels = sc->texels.p;
     S.point_lights = sc->point_lights.p; S.area_lights = sc->area_lights.p; S.dir_lights = sc->dir_lights.p;

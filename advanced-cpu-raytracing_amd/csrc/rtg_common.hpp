@@ -505,6 +505,9 @@ struct Surf {
     float u, v;
 };
 
+DEV f3 mesh_mapped_normal(const DevScene& S, const DevObject& ob, int face, f3 lp, float u, float v);
+DEV f3 sphere_bumped_normal(const DevScene& S, const DevObject& ob, f3 p, float phi, float theta, float u, float v);
+
 template <bool STATS>
 DEV Surf surface(const DevScene& S, const Ray& r, float mbTime, const Hit& h, Cnt<STATS>& c) {
     const DevObject& ob = S.objects[h.obj];
@@ -523,13 +526,13 @@ DEV Surf surface(const DevScene& S, const Ray& r, float mbTime, const Hit& h, Cn
         float theta = acosf(p.y / ob.center[3]);
         s.u = (float)((-phi + RT_PI) / (2.0f * RT_PI));
         s.v = (float)(theta / RT_PI);
-        f3 n = makeUnit(sub(lp, center));
+        f3 n = (ob.flags & OBJF_MAPPED) ? sphere_bumped_normal(S, ob, p, phi, theta, s.u, s.v)
+                                        : makeUnit(sub(lp, center));
         s.n = makeUnit(xform(ob.invT, n, 0.0f));
         return s;
     }
     f3 n = ld3(&S.face_n[h.face].x);
     if (ob.flags & OBJF_NORMAL_TWICE) n = makeUnit(xform(ob.baseInvT, n, 0.0f));   // mesh.cpp:363
-    s.n = makeUnit(xform(ob.invT, n, 0.0f));                                          // mesh.cpp:179 / instancedMesh.cpp:57
     if (ob.flags & OBJF_HAS_UV) {                                                     // mesh.cpp:245-262
         float bg[2], t;
         tri_test(S, h.face, lr, INFINITY, t, bg);
@@ -538,7 +541,13 @@ DEV Surf surface(const DevScene& S, const Ray& r, float mbTime, const Hit& h, Cn
         float v = a.y + bg[0] * (b.y - a.y) + bg[1] * (cc.y - a.y);
         s.u = tiledUV(u);
         s.v = tiledUV(v);
+        if (ob.flags & OBJF_MAPPED) {
+            // IntersectFace's local hit point (mesh.cpp:242), then the base mesh's transform
+            const f3 lp = add(lr.o, muls(lr.d, h.t));
+            n = makeUnit(xform(ob.baseInvT, mesh_mapped_normal(S, ob, h.face, lp, s.u, s.v), 0.0f));
+        }
     }
+    s.n = makeUnit(xform(ob.invT, n, 0.0f));                                          // mesh.cpp:179 / instancedMesh.cpp:57
     return s;
 }
 
@@ -617,6 +626,108 @@ DEV float perlin(const DevScene& S, const DevTexture& tx, float x, float y, floa
 DEV f3 tex_rgb(const DevScene& S, const DevTexture& tx, float u, float v) {
     if (tx.kind == 1) return mk(180.f, 30.f, 180.f);                    // PerlinTexture::GetRGBSample
     return image_rgb(S, tx, u, v);
+}
+
+// ---------------------------------------------------------------------------
+// Normal / bump mapping (mesh.cpp:263-358, sphere.cpp:116-193)
+// ---------------------------------------------------------------------------
+// GetTangentAndBitangentForTriangle (mesh.cpp:390-422)
+DEV void tri_tangents(f3 vert0, f3 vert1, f3 vert2, float2 v0_uv, float2 v1_uv, float2 v2_uv, f3& tan, f3& bitan) {
+    f3 e1 = makeUnit(sub(vert1, vert0));
+    f3 e2 = makeUnit(sub(vert2, vert1));
+    float v0u = tiledUV(v0_uv.x), v0v = tiledUV(v0_uv.y);
+    float v1u = tiledUV(v1_uv.x), v1v = tiledUV(v1_uv.y);
+    float v2u = tiledUV(v2_uv.x), v2v = tiledUV(v2_uv.y);
+    float u1 = v1u - v0u, v1 = v1v - v0v;
+    float u2 = v2u - v1u, v2 = v2v - v1v;
+    float det = 1.0f / (u1 * v2 - v1 * u2);
+    tan = mk(det * (v2 * e1.x - v1 * e2.x), det * (v2 * e1.y - v1 * e2.y), det * (v2 * e1.z - v1 * e2.z));
+    const float nd = -det;
+    bitan = mk(nd * u2 * e1.x + det * u1 * e2.x, nd * u2 * e1.y + det * u1 * e2.y, nd * u2 * e1.z + det * u1 * e2.z);
+    tan = makeUnit(tan);
+    bitan = makeUnit(bitan);
+}
+// GetTransformedNormal (helperMath.cpp:86-109): 3x3 double Matrix product, row by row
+DEV f3 tbn_normal(f3 tan, f3 bitan, f3 normal, f3 sn) {
+    double r0 = 0.0f, r1 = 0.0f, r2 = 0.0f;
+    r0 += (double)tan.x * (double)sn.x; r0 += (double)bitan.x * (double)sn.y; r0 += (double)normal.x * (double)sn.z;
+    r1 += (double)tan.y * (double)sn.x; r1 += (double)bitan.y * (double)sn.y; r1 += (double)normal.y * (double)sn.z;
+    r2 += (double)tan.z * (double)sn.x; r2 += (double)bitan.z * (double)sn.y; r2 += (double)normal.z * (double)sn.z;
+    return makeUnit(mk((float)r0, (float)r1, (float)r2));
+}
+// perlin bump: N minus the surface part of the height gradient (mesh.cpp:290-309, sphere.cpp:123-138)
+DEV f3 perlin_bump(const DevScene& S, const DevTexture& bm, f3 N, f3 p, float bf, bool scaled) {
+    const float eps = 0.001;
+    float h0 = perlin(S, bm, p.x, p.y, p.z);
+    float hxyz = scaled ? h0 * bf : h0;
+    float gx = perlin(S, bm, p.x + eps, p.y, p.z), gy = perlin(S, bm, p.x, p.y + eps, p.z),
+          gz = perlin(S, bm, p.x, p.y, p.z + eps);
+    if (scaled) { gx = gx * bf; gy = gy * bf; gz = gz * bf; }
+    f3 gradient = mk((gx - hxyz) / eps, (gy - hxyz) / eps, (gz - hxyz) / eps);
+    f3 gParallel = muls(N, dot(gradient, N));
+    f3 surfaceGradient = sub(gradient, gParallel);
+    return makeUnit(sub(N, surfaceGradient));
+}
+// Normal of a mapped mesh face in the base mesh's object space, before its transform.
+DEV f3 mesh_mapped_normal(const DevScene& S, const DevObject& ob, int face, f3 lp, float u, float v) {
+    const f3 N = ld3(&S.face_n[face].x);
+    const float4 a = S.tris[3 * face], b = S.face_v12[2 * face], c = S.face_v12[2 * face + 1];
+    f3 tan, bitan;
+    tri_tangents(mk(a.x, a.y, a.z), mk(b.x, b.y, b.z), mk(c.x, c.y, c.z), S.face_uv[3 * face],
+                 S.face_uv[3 * face + 1], S.face_uv[3 * face + 2], tan, bitan);
+    if (ob.tex_normal >= 0) {                                            // mesh.cpp:263-272
+        f3 sn = tex_rgb(S, S.textures[ob.tex_normal], u, v);
+        sn = sub(divs(sn, 127.5f), mk(1, 1, 1));
+        sn = makeUnit(sn);
+        return tbn_normal(tan, bitan, N, sn);
+    }
+    const DevTexture& bm = S.textures[ob.tex_bump];
+    if (bm.kind == 1) return perlin_bump(S, bm, N, lp, bm.bump_factor, true);
+    // image bump map, forward differences (mesh.cpp:310-352)
+    const DevImage im = S.images[bm.image];
+    const float width = (float)im.width, height = (float)im.height;
+    int i = (int)(u * (width - 1));
+    int j = (int)(v * (height - 1));
+    int nextI = i + 1, nextJ = j + 1;
+    if ((float)i == width - 1) nextI = i;
+    if ((float)j == height - 1) nextJ = j;
+    f3 t0 = texel(S, im, i, j), tu = texel(S, im, nextI, j), tv = texel(S, im, i, nextJ);
+    float h_uv = (t0.x + t0.y + t0.z) / 3.0f;                            // MakeGreyscale (mesh.cpp:195-197)
+    float hDeltaU = (tu.x + tu.y + tu.z) / 3.0f;
+    float hDeltaV = (tv.x + tv.y + tv.z) / 3.0f;
+    const float bumpFactor = bm.bump_factor;
+    f3 q_u = add(tan, muls(N, (hDeltaU - h_uv) * bumpFactor));
+    f3 q_v = add(bitan, muls(N, (hDeltaV - h_uv) * bumpFactor));
+    f3 nn = cross(q_v, q_u);
+    f3 n = makeUnit(nn);
+    if (nn.x * N.x <= 0 && nn.y * N.y <= 0 && nn.z * N.z <= 0) n = muls(n, -1.0f);
+    else if (fabsf(nn.y - N.y) > 0.9f || fabsf(nn.x - N.x) > 0.9f || fabsf(nn.z - N.z) > 0.9f) n = muls(n, -1.0f);
+    return n;
+}
+// Bumped sphere normal in local space (sphere.cpp:116-170, tangents sphere.cpp:181-193).
+DEV f3 sphere_bumped_normal(const DevScene& S, const DevObject& ob, f3 p, float phi, float theta, float u, float v) {
+    const float radius = ob.center[3];
+    f3 tan = mk((float)(2 * RT_PI * (double)p.z), 0.0f, (float)(-2 * RT_PI * (double)p.x));
+    f3 bitan = mk((float)(RT_PI * (double)p.y * (double)cosf(phi)),
+                  (float)((double)(-radius) * RT_PI * (double)sinf(theta)),
+                  (float)(RT_PI * (double)p.y * (double)sinf(phi)));
+    tan = makeUnit(tan);
+    bitan = makeUnit(bitan);
+    const f3 N = makeUnit(cross(bitan, tan));
+    const DevTexture& bm = S.textures[ob.tex_bump];
+    if (bm.kind == 1) return perlin_bump(S, bm, N, p, 1.0f, false);
+    const DevImage im = S.images[bm.image];
+    int i = (int)(u * (float)im.width);
+    int j = (int)(v * (float)im.height);
+    const float normalizer = bm.normalizer, bumpFactor = bm.bump_factor;
+    f3 c1 = divs(texel(S, im, i + 1, j), normalizer), c0 = divs(texel(S, im, i, j), normalizer),
+       c2 = divs(texel(S, im, i, j + 1), normalizer);
+    float h1 = (c1.x + c1.y + c1.z) * bumpFactor;                        // MakeGreyscale (sphere.cpp:9-11)
+    float h_uv = (c0.x + c0.y + c0.z) * bumpFactor;
+    float h2 = (c2.x + c2.y + c2.z) * bumpFactor;
+    f3 q_u = add(tan, muls(N, h1 - h_uv));
+    f3 q_v = add(bitan, muls(N, h2 - h_uv));
+    return makeUnit(cross(q_v, q_u));
 }
 
 // SphericalEnvironmentLight::GetSample (sphericalEnvironmentLight.h:22-34)

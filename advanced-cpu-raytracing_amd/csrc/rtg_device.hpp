@@ -13,6 +13,8 @@
 //     (matrixA columns of mesh.cpp:208-210)
 //   face_n[f]  float4 {n.xyz, 0}   (read once per hit)
 //   face_uv[f] 3 x float2 (meshes with UVs only)
+//   face_v12[2f..2f+1] float4 {v1}, {v2} (scenes with normal / bump maps only: the
+//     tangent frame of mesh.cpp:390-422 needs v2 - v1 exactly)
 // Faces are in the BVH-permuted order, so a leaf is a contiguous, coalescable
 // range.  Objects, materials, BRDFs, lights, textures are small tables.
 #pragma once
@@ -23,12 +25,13 @@ namespace rtg {
 
 enum { OBJ_MESH = 0, OBJ_INSTANCE = 1, OBJ_SPHERE = 2 };
 enum { OBJF_SHADOW_SKIP = 1, OBJF_NORMAL_TWICE = 2, OBJF_MOTION_BLUR = 4, OBJF_HAS_UV = 8,
-       OBJF_IDENTITY = 16 };   // inverse transform is exactly the identity: traversal skips it
+       OBJF_IDENTITY = 16,     // inverse transform is exactly the identity: traversal skips it
+       OBJF_MAPPED = 32 };     // normal or bump map in effect (mesh with UVs, or sphere bump map)
 
 struct DevObject {
-    int kind, material, flags, pad0;
+    int kind, material, flags, tex_normal;
     int node_begin, node_end;       // global node range of the (base) mesh's BVH
-    int tex_diffuse, tex_specular, tex_replace_all, pad1;
+    int tex_diffuse, tex_specular, tex_replace_all, tex_bump;
     float bmin[4], bmax[4];         // mesh: local bbox, instance: world bbox
     float mbv[4];                   // motion blur vector
     float center[4];                // sphere center (xyz) + radius (w)
@@ -81,6 +84,7 @@ struct DevScene {
     const float4* __restrict__ tris;
     const float4* __restrict__ face_n;
     const float2* __restrict__ face_uv;
+    const float4* __restrict__ face_v12;   // raw v1, v2 per face (scenes with normal / bump maps only)
     const DevObject* __restrict__ objects;
     const DevMaterial* __restrict__ materials;
     const DevBrdf* __restrict__ brdfs;

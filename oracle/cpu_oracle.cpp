@@ -237,7 +237,7 @@ private:
         return x;
     }
 
-    // ---- mesh.cpp:201-372 (normal/bump maps are not part of this restatement)
+    // ---- mesh.cpp:201-372
     bool IntersectFace(Ray& ray, const rtg_mesh& M, int faceIdx, const rtg_object& ob) {
         const rtg_face& face = S.faces[M.face_offset + faceIdx];
         cnt.tri();
@@ -269,13 +269,114 @@ private:
         if (M.has_uv) {
             float u = face.uv0[0] + beta * (face.uv1[0] - face.uv0[0]) + gama * (face.uv2[0] - face.uv0[0]);
             float v = face.uv0[1] + beta * (face.uv1[1] - face.uv0[1]) + gama * (face.uv2[1] - face.uv0[1]);
-            ray.hitInfo.u = TiledUV(u);
-            ray.hitInfo.v = TiledUV(v);
+            u = TiledUV(u);
+            v = TiledUV(v);
+            ray.hitInfo.u = u;
+            ray.hitInfo.v = v;
+            // normal or bump map of the base mesh (mesh.cpp:263-358), then the base mesh's
+            // inverse transpose; Mesh::Intersect / InstancedMesh::Intersect apply the
+            // object's once more (mesh.cpp:179, instancedMesh.cpp:57)
+            if (ob.tex_normal >= 0) {
+                Vec3f sampledNormal = TexRGB(S.textures[ob.tex_normal], u, v);
+                sampledNormal = sampledNormal / (127.5f) - V(1, 1, 1);
+                sampledNormal = makeUnit(sampledNormal);
+                Vec3f tan, bitan;
+                TangentBitangentForTriangle(v0, v1, v2, face.uv0, face.uv1, face.uv2, tan, bitan);
+                ray.hitInfo.normal = TransformedNormal(tan, bitan, V(face.n), sampledNormal);
+                ray.hitInfo.normal = makeUnit(applyT(ob.base_inv_transpose, ray.hitInfo.normal, 0.0f));
+            } else if (ob.tex_bump >= 0) {
+                const rtg_texture& bm = S.textures[ob.tex_bump];
+                Vec3f tan, bitan;
+                TangentBitangentForTriangle(v0, v1, v2, face.uv0, face.uv1, face.uv2, tan, bitan);
+                Vec3f N = V(face.n);
+                if (bm.kind == RTG_TEX_PERLIN) {
+                    Vec3f gradient;
+                    float eps = 0.001;
+                    const Vec3f& p = ray.hitInfo.hitPoint;
+                    float bf = bm.bump_factor;
+                    float hxyz = Perlin(bm, p.x, p.y, p.z) * bf;
+                    gradient.x = (Perlin(bm, p.x + eps, p.y, p.z) * bf - hxyz) / eps;
+                    gradient.y = (Perlin(bm, p.x, p.y + eps, p.z) * bf - hxyz) / eps;
+                    gradient.z = (Perlin(bm, p.x, p.y, p.z + eps) * bf - hxyz) / eps;
+                    Vec3f gParallel = N * dot(gradient, N);
+                    Vec3f surfaceGradient = gradient - gParallel;
+                    Vec3f newNormal = N - surfaceGradient;
+                    ray.hitInfo.normal = makeUnit(newNormal);
+                } else {
+                    const rtg_image& im = S.images[bm.image];
+                    float width = im.width, height = im.height;
+                    int i = (int)(u * (width - 1));
+                    int j = (int)(v * (height - 1));
+                    int nextI = i + 1, nextJ = j + 1;
+                    if (i == width - 1) nextI = i;
+                    if (j == height - 1) nextJ = j;
+                    Vec3f c = Texel(im, i, j);
+                    float h_uv = (c.x + c.y + c.z) / 3.0f;                  // MakeGreyscale, mesh.cpp:195-197
+                    c = Texel(im, nextI, j);
+                    float hDeltaU = (c.x + c.y + c.z) / 3.0f;
+                    c = Texel(im, i, nextJ);
+                    float hDeltaV = (c.x + c.y + c.z) / 3.0f;
+                    float bumpFactor = bm.bump_factor;
+                    Vec3f q_u = tan + N * ((hDeltaU - h_uv) * bumpFactor);
+                    Vec3f q_v = bitan + N * ((hDeltaV - h_uv) * bumpFactor);
+                    Vec3f newNormal = cross(q_v, q_u);
+                    ray.hitInfo.normal = makeUnit(newNormal);
+                    if (newNormal.x * N.x <= 0 && newNormal.y * N.y <= 0 && newNormal.z * N.z <= 0)
+                        ray.hitInfo.normal = ray.hitInfo.normal * -1;
+                    else if (std::abs(newNormal.y - N.y) > 0.9f || std::abs(newNormal.x - N.x) > 0.9f ||
+                             std::abs(newNormal.z - N.z) > 0.9f)
+                        ray.hitInfo.normal = ray.hitInfo.normal * -1;
+                }
+                ray.hitInfo.normal = makeUnit(applyT(ob.base_inv_transpose, ray.hitInfo.normal, 0.0f));
+            }
         } else {
             // base mesh's own inverse transpose (for instances: the base mesh's)
             ray.hitInfo.normal = makeUnit(applyT(ob.base_inv_transpose, ray.hitInfo.normal, 0.0f));
         }
         return true;
+    }
+
+    // ---- mesh.cpp:390-422
+    static void TangentBitangentForTriangle(Vec3f vert0, Vec3f vert1, Vec3f vert2, const float* v0_uv,
+                                            const float* v1_uv, const float* v2_uv, Vec3f& tan, Vec3f& bitan) {
+        Vec3f e1 = makeUnit(vert1 - vert0);
+        Vec3f e2 = makeUnit(vert2 - vert1);
+        float v0u = TiledUV(v0_uv[0]), v0v = TiledUV(v0_uv[1]);
+        float v1u = TiledUV(v1_uv[0]), v1v = TiledUV(v1_uv[1]);
+        float v2u = TiledUV(v2_uv[0]), v2v = TiledUV(v2_uv[1]);
+        float u1 = v1u - v0u, v1 = v1v - v0v;
+        float u2 = v2u - v1u, v2 = v2v - v1v;
+        float det = 1.0f / (u1 * v2 - v1 * u2);
+        tan.x = det * (v2 * e1.x - v1 * e2.x);
+        tan.y = det * (v2 * e1.y - v1 * e2.y);
+        tan.z = det * (v2 * e1.z - v1 * e2.z);
+        bitan.x = -det * u2 * e1.x + det * u1 * e2.x;
+        bitan.y = -det * u2 * e1.y + det * u1 * e2.y;
+        bitan.z = -det * u2 * e1.z + det * u1 * e2.z;
+        tan = makeUnit(tan);
+        bitan = makeUnit(bitan);
+    }
+    // ---- helperMath.cpp:86-109: TBN (double Matrix) x sampled normal
+    static Vec3f TransformedNormal(Vec3f tan, Vec3f bitan, Vec3f normal, Vec3f s) {
+        const double m[3][3] = {{tan.x, bitan.x, normal.x}, {tan.y, bitan.y, normal.y}, {tan.z, bitan.z, normal.z}};
+        const double vec[3] = {s.x, s.y, s.z};
+        double r[3];
+        for (int i = 0; i < 3; ++i) {
+            r[i] = 0.0f;
+            for (int k = 0; k < 3; ++k) r[i] += m[i][k] * vec[k];
+        }
+        return makeUnit(V((float)r[0], (float)r[1], (float)r[2]));
+    }
+    // ---- sphere.cpp:181-193
+    static void TangentBitangentAroundPoint(Vec3f p, float radius, float phi, float theta, Vec3f& tan, Vec3f& bitan) {
+        tan.x = 2 * M_PI * p.z;
+        tan.y = 0;
+        tan.z = -2 * M_PI * p.x;
+        bitan.x = M_PI * p.y * std::cos(phi);
+        bitan.y = -radius * M_PI * std::sin(theta);
+        bitan.z = M_PI * p.y * std::sin(phi);
+        tan = makeUnit(tan);
+        bitan = makeUnit(bitan);
     }
 
     // ---- bvh.cpp:5-30
@@ -348,7 +449,7 @@ private:
         return hasHit;
     }
 
-    // ---- sphere.cpp:13-180 (no normal / bump maps)
+    // ---- sphere.cpp:13-180 (a sphere normal map leaves the normal unset in the reference: rejected)
     bool SphereIntersect(Ray& r, const rtg_object& ob, int objIdx) {
         cnt.spheres++;
         cnt.objects++;
@@ -384,9 +485,47 @@ private:
             Vec3f p = localhitPoint - center;
             float phi = std::atan2(p.z, p.x);
             float theta = std::acos(p.y / radius);
-            r.hitInfo.u = (-phi + M_PI) / (2.0f * M_PI);
-            r.hitInfo.v = theta / M_PI;
-            r.hitInfo.normal = makeUnit(localhitPoint - center);
+            float u = (-phi + M_PI) / (2.0f * M_PI);
+            float v = theta / M_PI;
+            r.hitInfo.u = u;
+            r.hitInfo.v = v;
+            if (ob.tex_bump >= 0) {                                         // sphere.cpp:116-170
+                const rtg_texture& bm = S.textures[ob.tex_bump];
+                Vec3f tan, bitan;
+                TangentBitangentAroundPoint(p, radius, phi, theta, tan, bitan);
+                Vec3f N = makeUnit(cross(bitan, tan));
+                if (bm.kind == RTG_TEX_PERLIN) {
+                    Vec3f gradient;
+                    float eps = 0.001;
+                    float hxyz = Perlin(bm, p.x, p.y, p.z);
+                    gradient.x = (Perlin(bm, p.x + eps, p.y, p.z) - hxyz) / eps;
+                    gradient.y = (Perlin(bm, p.x, p.y + eps, p.z) - hxyz) / eps;
+                    gradient.z = (Perlin(bm, p.x, p.y, p.z + eps) - hxyz) / eps;
+                    Vec3f gParallel = N * dot(gradient, N);
+                    Vec3f surfaceGradient = gradient - gParallel;
+                    Vec3f newNormal = N - surfaceGradient;
+                    r.hitInfo.normal = makeUnit(newNormal);
+                } else {
+                    const rtg_image& im = S.images[bm.image];
+                    float width = im.width, height = im.height;
+                    int i = (int)(u * width);
+                    int j = (int)(v * height);
+                    float normalizer = bm.normalizer;
+                    float bumpFactor = bm.bump_factor;
+                    Vec3f c = Texel(im, i + 1, j) / normalizer;
+                    float h1 = (c.x + c.y + c.z) * bumpFactor;                // MakeGreyscale, sphere.cpp:9-11
+                    c = Texel(im, i, j) / normalizer;
+                    float h_uv = (c.x + c.y + c.z) * bumpFactor;
+                    c = Texel(im, i, j + 1) / normalizer;
+                    float h2 = (c.x + c.y + c.z) * bumpFactor;
+                    Vec3f q_u = tan + N * (h1 - h_uv);
+                    Vec3f q_v = bitan + N * (h2 - h_uv);
+                    Vec3f newNormal = cross(q_v, q_u);
+                    r.hitInfo.normal = makeUnit(newNormal);
+                }
+            } else {
+                r.hitInfo.normal = makeUnit(localhitPoint - center);
+            }
             r.hitInfo.normal = makeUnit(applyT(ob.inv_transpose, r.hitInfo.normal, 0.0f));
             return true;
         }

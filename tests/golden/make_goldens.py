@@ -46,6 +46,7 @@ FIXTURES = {
     "transforms_textures": ("authored", 200, 150, "exact", None),
     "synth_10k": ("generated", 256, 144, "exact", None),
     "ply_quads": ("generated", 160, 120, "exact", None),
+    "bump_normal": ("generated", 200, 150, "exact", None),
     "area_light": ("authored", 160, 160, "stochastic", None),
     "env_light": ("authored", 160, 120, "stochastic", None),
     "dof_motion": ("authored", 160, 120, "stochastic", None),
@@ -124,6 +125,234 @@ def make_ply_quads():
         f.write(xml)
 
 
+def write_ppm(path, img):
+    h, w, _ = img.shape
+    with open(path, "wb") as f:
+        f.write(b"P6\n%d %d\n255\n" % (w, h) + np.ascontiguousarray(img, np.uint8).tobytes())
+
+
+def make_bump_normal():
+    """Normal maps (mesh), image and Perlin bump maps (mesh, instance of a bumped mesh,
+    sphere): mesh.cpp:263-358, sphere.cpp:116-193.  Images are seeded patterns written as
+    PPM under scenes/inputs/ (parser.cpp:110 prefixes "inputs/")."""
+    n = 64
+    y, x = np.mgrid[0:n, 0:n].astype(np.float64) / n
+    # normal map: tangent-space normals of a sum of bumps, encoded (n + 1) * 127.5
+    hx = 0.6 * np.cos(2 * np.pi * 3 * x) * np.sin(2 * np.pi * 2 * y)
+    hy = 0.6 * np.sin(2 * np.pi * 3 * x) * np.cos(2 * np.pi * 2 * y)
+    nrm = np.stack([-hx, -hy, np.ones_like(hx)], -1)
+    nrm /= np.linalg.norm(nrm, axis=-1, keepdims=True)
+    write_ppm(os.path.join(SCENES, "inputs", "normalmap.ppm"), np.clip(np.round((nrm + 1) * 127.5), 0, 255))
+    # bump map: rings + a seeded speckle, grey in all three channels with a colour tint
+    rng = np.random.default_rng(1234)
+    r = np.hypot(x - 0.5, y - 0.5)
+    hgt = 128 + 90 * np.sin(2 * np.pi * 6 * r) + rng.integers(-20, 21, size=(n, n))
+    bump = np.stack([hgt, hgt * 0.9, hgt * 1.1], -1)
+    write_ppm(os.path.join(SCENES, "inputs", "bumpmap.ppm"), np.clip(np.round(bump), 0, 255))
+    xml = """<Scene>
+    <MaxRecursionDepth>1</MaxRecursionDepth>
+    <BackgroundColor>20 20 30</BackgroundColor>
+    <ShadowRayEpsilon>1e-3</ShadowRayEpsilon>
+    <Cameras>
+        <Camera id="1">
+            <Position>0 4 10</Position>
+            <Gaze>0 -0.35 -1</Gaze>
+            <Up>0 1 0</Up>
+            <NearPlane>-0.8 0.8 -0.6 0.6</NearPlane>
+            <NearDistance>1.2</NearDistance>
+            <ImageResolution>200 150</ImageResolution>
+            <ImageName>bump_normal.png</ImageName>
+        </Camera>
+    </Cameras>
+    <Lights>
+        <AmbientLight>20 20 20</AmbientLight>
+        <PointLight id="1">
+            <Position>3 7 6</Position>
+            <Intensity>2000 2000 2000</Intensity>
+        </PointLight>
+        <PointLight id="2">
+            <Position>-5 3 2</Position>
+            <Intensity>600 500 400</Intensity>
+        </PointLight>
+    </Lights>
+    <Materials>
+        <Material id="1">
+            <AmbientReflectance>0.3 0.3 0.3</AmbientReflectance>
+            <DiffuseReflectance>0.7 0.7 0.7</DiffuseReflectance>
+            <SpecularReflectance>0.5 0.5 0.5</SpecularReflectance>
+            <PhongExponent>30</PhongExponent>
+        </Material>
+        <Material id="2">
+            <AmbientReflectance>0.2 0.2 0.3</AmbientReflectance>
+            <DiffuseReflectance>0.3 0.5 0.9</DiffuseReflectance>
+            <SpecularReflectance>0.6 0.6 0.6</SpecularReflectance>
+            <PhongExponent>40</PhongExponent>
+        </Material>
+        <Material id="3" type="mirror">
+            <AmbientReflectance>0.05 0.05 0.05</AmbientReflectance>
+            <DiffuseReflectance>0.2 0.1 0.1</DiffuseReflectance>
+            <SpecularReflectance>0.2 0.2 0.2</SpecularReflectance>
+            <MirrorReflectance>0.6 0.6 0.6</MirrorReflectance>
+        </Material>
+    </Materials>
+    <Textures>
+        <Images>
+            <Image id="1">normalmap.ppm</Image>
+            <Image id="2">bumpmap.ppm</Image>
+        </Images>
+        <TextureMap id="1" type="image">
+            <ImageId>1</ImageId>
+            <DecalMode>replace_normal</DecalMode>
+            <Interpolation>nearest</Interpolation>
+        </TextureMap>
+        <TextureMap id="2" type="image">
+            <ImageId>2</ImageId>
+            <DecalMode>bump_normal</DecalMode>
+            <BumpFactor>0.02</BumpFactor>
+        </TextureMap>
+        <TextureMap id="3" type="perlin">
+            <DecalMode>bump_normal</DecalMode>
+            <NoiseConversion>absval</NoiseConversion>
+            <NoiseScale>3</NoiseScale>
+            <BumpFactor>0.4</BumpFactor>
+        </TextureMap>
+        <TextureMap id="4" type="image">
+            <ImageId>2</ImageId>
+            <DecalMode>bump_normal</DecalMode>
+            <Normalizer>200</Normalizer>
+            <BumpFactor>3</BumpFactor>
+        </TextureMap>
+        <TextureMap id="5" type="perlin">
+            <DecalMode>bump_normal</DecalMode>
+            <NoiseConversion>linear</NoiseConversion>
+            <NoiseScale>4</NoiseScale>
+        </TextureMap>
+        <TextureMap id="6" type="image">
+            <ImageId>1</ImageId>
+            <DecalMode>replace_normal</DecalMode>
+            <Interpolation>bilinear</Interpolation>
+        </TextureMap>
+    </Textures>
+    <VertexData>
+        -6 0 -6
+        6 0 -6
+        6 0 6
+        -6 0 6
+        -0.5 -0.5 -0.5
+        0.5 -0.5 -0.5
+        0.5 0.5 -0.5
+        -0.5 0.5 -0.5
+        -0.5 -0.5 0.5
+        0.5 -0.5 0.5
+        0.5 0.5 0.5
+        -0.5 0.5 0.5
+        2.5 0.2 2.0
+        4.0 0.2 2.5
+        3.2 2.0 2.2
+        0 1 0
+    </VertexData>
+    <TexCoordData>
+        0 0
+        3 0
+        3 3
+        0 3
+        0 0
+        1 0
+        1 1
+        0 1
+        0.1 0.1
+        0.9 0.1
+        0.9 0.9
+        0.1 0.9
+        0 0
+        1 0
+        0.5 1
+        0 0
+    </TexCoordData>
+    <Transformations>
+        <Translation id="1">0 0.01 0</Translation>
+        <Translation id="2">-2.5 0.9 0</Translation>
+        <Translation id="3">2.2 0.9 -1.5</Translation>
+        <Translation id="4">0 0.2 1.8</Translation>
+        <Scaling id="1">1.2 1 1.2</Scaling>
+        <Scaling id="2">0.8 1.3 0.8</Scaling>
+        <Scaling id="3">1.5 1.5 1.5</Scaling>
+        <Rotation id="1">30 0 1 0</Rotation>
+        <Rotation id="2">-25 1 0 0</Rotation>
+        <Rotation id="3">40 0 0 1</Rotation>
+    </Transformations>
+    <Objects>
+        <Mesh id="1">
+            <Material>1</Material>
+            <Textures>1</Textures>
+            <Transformations>s1 t1</Transformations>
+            <Faces>
+                1 3 2
+                1 4 3
+            </Faces>
+        </Mesh>
+        <Mesh id="2">
+            <Material>2</Material>
+            <Textures>2</Textures>
+            <Transformations>s3 r1 t2</Transformations>
+            <Faces>
+                5 7 6
+                5 8 7
+                9 10 11
+                9 11 12
+                5 6 10
+                5 10 9
+                8 12 11
+                8 11 7
+                5 9 12
+                5 12 8
+                6 7 11
+                6 11 10
+            </Faces>
+        </Mesh>
+        <MeshInstance id="10" baseMeshId="2">
+            <Material>1</Material>
+            <Transformations>r2 t3</Transformations>
+        </MeshInstance>
+        <MeshInstance id="11" baseMeshId="2" resetTransform="true">
+            <Material>3</Material>
+            <Transformations>s2 r3 t4</Transformations>
+        </MeshInstance>
+        <Mesh id="3">
+            <Material>2</Material>
+            <Textures>6</Textures>
+            <Transformations>r3 t4</Transformations>
+            <Faces>
+                9 10 11
+                9 11 12
+            </Faces>
+        </Mesh>
+        <Triangle id="1">
+            <Material>1</Material>
+            <Textures>3</Textures>
+            <Indices>13 14 15</Indices>
+        </Triangle>
+        <Sphere id="1">
+            <Material>1</Material>
+            <Textures>4</Textures>
+            <Center>16</Center>
+            <Radius>0.8</Radius>
+            <Transformations>s2 t3</Transformations>
+        </Sphere>
+        <Sphere id="2">
+            <Material>2</Material>
+            <Textures>5</Textures>
+            <Center>16</Center>
+            <Radius>0.6</Radius>
+            <Transformations>t2 t1</Transformations>
+        </Sphere>
+    </Objects>
+</Scene>
+"""
+    with open(os.path.join(SCENES, "bump_normal.xml"), "w") as f:
+        f.write(xml)
+
+
 def prepare(name, src, w, h, edits):
     dst = os.path.join(SCENES, name + ".xml")
     if src == "generated":
@@ -131,6 +360,8 @@ def prepare(name, src, w, h, edits):
             gen.synthetic_heightfield(SCENES, K=10082, width=w, height=h, name="synth_10k")
         elif name == "ply_quads":
             make_ply_quads()
+        elif name == "bump_normal":
+            make_bump_normal()
         elif name == "c2_cornell":
             gen.config_c2(SCENES, os.path.join(SCENES, "cornell_conductors.xml"), w, h)
         elif name == "c3_blob":

@@ -152,3 +152,32 @@ def test_comments_entities_and_whitespace(tmp_path):
     _, a, _ = render(s)
     _, b, _ = render(_scene(tmp_path, t, "ws.xml"))
     assert np.array_equal(a, b)
+
+
+def test_sphere_normal_map_is_rejected(tmp_path, monkeypatch):
+    """A sphere normal map leaves the hit normal unset in the reference (sphere.cpp:95-113):
+    the device scene refuses it instead of inventing a normal (checked before any GPU call)."""
+    monkeypatch.chdir(SCENES)
+    s = open(os.path.join(SCENES, "bump_normal.xml")).read().replace(
+        "<Textures>4</Textures>", "<Textures>1</Textures>")
+    hs = rtgpu.HostScene(_scene(tmp_path, s))
+    with pytest.raises(rtgpu.RTGError) as e:
+        rtgpu.DeviceScene(hs, 0)
+    assert e.value.code == -6
+
+
+def test_instances_take_base_mesh_bump_map(tmp_path, monkeypatch):
+    """IntersectFace reads the BASE mesh's bump map for an instance (mesh.cpp:263-358 with
+    `this` = baseMesh): dropping the instance's own (ignored) texture list changes nothing,
+    dropping the base mesh's bump map changes the instance's pixels."""
+    monkeypatch.chdir(SCENES)
+    s = open(os.path.join(SCENES, "bump_normal.xml")).read()
+    _, ref, _ = render("bump_normal.xml")
+    inst = s.replace('<MeshInstance id="10" baseMeshId="2">\n            <Material>1</Material>',
+                     '<MeshInstance id="10" baseMeshId="2">\n            <Material>1</Material>\n'
+                     '            <Textures>3</Textures>')
+    _, a, _ = render(_scene(tmp_path, inst, "a.xml"))
+    assert np.array_equal(a.view(np.uint32), ref.view(np.uint32))
+    nob = s.replace("<Textures>2</Textures>", "")
+    _, b, _ = render(_scene(tmp_path, nob, "b.xml"))
+    assert (np.abs(b - ref).max(-1) > 1e-3).mean() > 0.01
