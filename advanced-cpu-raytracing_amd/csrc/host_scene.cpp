@@ -899,7 +899,10 @@ void Loader::parseMeshes(XmlNode* root, const char* elemName) {   // parser.cpp:
             rtg_material& mat = S.materials[sh.material - 1];   // parser.cpp:1484-1487
             mat.type = RTG_MAT_EMISSIVE;
             mat.radiance = to_f3(radiance);
-            S.numMeshLights++;
+            rtg_mesh_light ml;
+            ml.object = (int32_t)shapes.size();     // objects[] follow scene.meshes order
+            ml.radiance = to_f3(radiance);
+            S.mesh_lights.push_back(ml);
         }
         shapes.push_back(sh);
     }
@@ -1114,7 +1117,7 @@ void HostScene::finalize() {
     desc.meshes = meshes.data(); desc.num_meshes = (int32_t)meshes.size();
     desc.faces = faces.data(); desc.num_faces = (int64_t)faces.size();
     desc.nodes = nodes.data(); desc.num_nodes = (int64_t)nodes.size();
-    desc.num_mesh_lights = numMeshLights;
+    desc.mesh_lights = mesh_lights.data(); desc.num_mesh_lights = (int32_t)mesh_lights.size();
 }
 
 }  // namespace rtg

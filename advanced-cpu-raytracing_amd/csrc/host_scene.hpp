@@ -19,7 +19,7 @@ struct HostScene {
     int maxDepth = 0;
     int bgTexture = -1;
     bool motionBlurEnabled = false;
-    int numMeshLights = 0;
+    std::vector<rtg_mesh_light> mesh_lights;
     V3 ambient;
     std::vector<rtg_camera> cameras;
     std::vector<rtg_material> materials;

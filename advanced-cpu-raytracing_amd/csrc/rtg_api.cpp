@@ -84,6 +84,8 @@ struct rtg_scene {
     DevBuf<int> env_images;
     DevBuf<float2> face_uv;
     DevBuf<float4> face_v12;
+    DevBuf<rtg::DevMeshLight> mesh_lights;
+    DevBuf<rtg::DevLightFace> light_faces;
     DevBuf<rtg::DevObject> objects;
     DevBuf<rtg::DevMaterial> materials;
     DevBuf<rtg::DevBrdf> brdfs;
@@ -181,8 +183,12 @@ int rtg_device_count(int32_t* count) {
 int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     if (!d || !out) return set_err(RTG_ERR_INVALID, "null argument");
     *out = nullptr;
-    if (d->num_mesh_lights > 0)
-        return set_err(RTG_ERR_UNSUPPORTED, "LightMesh (mesh light sampling) is not implemented on the GPU path yet");
+    for (int i = 0; i < d->num_mesh_lights; ++i) {
+        const int o = d->mesh_lights ? d->mesh_lights[i].object : -1;
+        if (o < 0 || o >= d->num_objects || d->objects[o].kind != RTG_OBJ_MESH ||
+            d->meshes[d->objects[o].mesh].face_count <= 0)
+            return set_err(RTG_ERR_INVALID, "mesh light %d: bad object", i);
+    }
     if (d->max_recursion_depth > rtg::max_supported_depth())
         return set_err(RTG_ERR_UNSUPPORTED, "MaxRecursionDepth %d > %d", d->max_recursion_depth, rtg::max_supported_depth());
     for (int i = 0; i < d->num_objects; ++i) {
@@ -320,6 +326,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
             ident &= o.inv_transform[k] == ((k % 5 == 0) ? 1.0 : 0.0);
         }
         if (ident) D.flags |= rtg::OBJF_IDENTITY;
+        D.id = o.kind == RTG_OBJ_SPHERE ? INT32_MIN : o.id;   // spheres never carry a light's id
         if (o.kind == RTG_OBJ_SPHERE) feat |= rtg::FEAT_SPHERE;
         else if (o.kind == RTG_OBJ_INSTANCE) feat |= rtg::FEAT_INSTANCE;
         else if (!ident || (o.flags & RTG_OBJF_MOTION_BLUR)) feat |= rtg::FEAT_XFORM;
@@ -335,7 +342,30 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     sc->tree_ok = !blur && d->max_recursion_depth > 0 && branching;
     sc->wave_ok = !blur && (d->max_recursion_depth <= 0 || !branching);
     sc->num_slots = d->num_point_lights + d->num_area_lights + d->num_env_lights + d->num_dir_lights +
-                    d->num_spot_lights;
+                    d->num_spot_lights + d->num_mesh_lights;
+    // mesh lights (meshLight.h): their faces in MeshLight::faces order (the BVH-permuted one)
+    std::vector<rtg::DevMeshLight> mls(d->num_mesh_lights);
+    std::vector<rtg::DevLightFace> lfs;
+    for (int i = 0; i < d->num_mesh_lights; ++i) {
+        const rtg_object& o = d->objects[d->mesh_lights[i].object];
+        const rtg_mesh& M = d->meshes[o.mesh];
+        rtg::DevMeshLight& L = mls[i];
+        std::memset(&L, 0, sizeof(L));
+        L.id = o.id;
+        L.face_begin = (int)lfs.size();
+        L.face_count = M.face_count;
+        f4(L.radiance, d->mesh_lights[i].radiance);
+        L.surface_area = M.surface_area;
+        for (int k = 0; k < 12; ++k) L.xf[k] = o.transform[k];
+        for (int f = 0; f < M.face_count; ++f) {
+            const rtg_face& F = d->faces[M.face_offset + f];
+            rtg::DevLightFace lf;
+            std::memset(&lf, 0, sizeof(lf));
+            f4(lf.v0, F.v0); f4(lf.v1, F.v1); f4(lf.v2, F.v2);
+            lf.area = F.area;
+            lfs.push_back(lf);
+        }
+    }
     std::vector<rtg::DevMaterial> mats(d->num_materials);
     for (int i = 0; i < d->num_materials; ++i) {
         const rtg_material& m = d->materials[i];
@@ -430,6 +460,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     HIP_TRY(sc->textures.upload(texs)); HIP_TRY(sc->images.upload(imgs)); HIP_TRY(sc->texels.upload(pool));
     HIP_TRY(sc->point_lights.upload(pls)); HIP_TRY(sc->area_lights.upload(als)); HIP_TRY(sc->dir_lights.upload(dls));
     HIP_TRY(sc->spot_lights.upload(sls)); HIP_TRY(sc->env_images.upload(envs));
+    HIP_TRY(sc->mesh_lights.upload(mls)); HIP_TRY(sc->light_faces.upload(lfs));
     std::vector<rtg::DevCounters> zero(1);
     std::memset(zero.data(), 0, sizeof(rtg::DevCounters));
     HIP_TRY(sc->counters.upload(zero));
@@ -445,6 +476,9 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     S.nodes = sc->nodes.p; S.node_ext = sc->node_ext.p; S.tris = sc->tris.p; S.face_n = sc->face_n.p;
     S.face_uv = sc->face_uv.p;
     S.face_v12 = sc->face_v12.p;
+    S.mesh_lights = sc->mesh_lights.p;
+    S.light_faces = sc->light_faces.p;
+    S.num_mesh = d->num_mesh_lights;
     S.objects = sc->objects.p; S.materials = sc->materials.p; S.brdfs = sc->brdfs.p;
     S.textures = sc->textures.p; S.images = sc->images.p; S.texels = sc->texels.p;
     S.point_lights = sc->point_lights.p; S.area_lights = sc->area_lights.p; S.dir_lights = sc->dir_lights.p;
@@ -521,7 +555,6 @@ static int prepare(rtg_scene* s, const rtg_render_opts* o, rtg::DevCamera& C, rt
     if (!s || !o) return set_err(RTG_ERR_INVALID, "null argument");
     if (o->camera < 0 || o->camera >= (int)s->cameras.size()) return set_err(RTG_ERR_INVALID, "bad camera %d", o->camera);
     const rtg_camera& c = s->cameras[o->camera];
-    if (c.path_tracing) return set_err(RTG_ERR_UNSUPPORTED, "path tracing (<Renderer>PathTracing) is not implemented yet");
     if (c.width <= 0 || c.height <= 0) return set_err(RTG_ERR_INVALID, "camera %d has an empty image", o->camera);
     std::memset(&C, 0, sizeof(C));
     auto cp = [](float* d, const rtg_float3& v) { d[0] = v.x; d[1] = v.y; d[2] = v.z; };
@@ -529,6 +562,8 @@ static int prepare(rtg_scene* s, const rtg_render_opts* o, rtg::DevCamera& C, rt
     C.left = c.left; C.right_ext = c.right_ext; C.bottom = c.bottom; C.top = c.top;
     C.focus_distance = c.focus_distance; C.aperture = c.aperture;
     C.width = c.width; C.height = c.height; C.spp = c.spp < 1 ? 1 : c.spp;
+    C.path_tracing = c.path_tracing; C.next_event = c.next_event;
+    C.importance_sampling = c.importance_sampling; C.russian_roulette = c.russian_roulette;
     std::memset(&P, 0, sizeof(P));
     P.row_begin = o->row_begin < 0 ? 0 : o->row_begin;
     P.row_end = (o->row_end <= 0 || o->row_end > c.height) ? c.height : o->row_end;
@@ -587,7 +622,9 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
     // ray trees: the wavefront tree pipeline for large frames (it synchronises once per tree
     // level), the fused kernel otherwise; RTG_RENDER_TREE / RTG_RENDER_FUSED force either
     const long long work = (long long)(P.row_end - P.row_begin) * C.width * P.sample_count;
-    const bool use_tree = s->tree_ok && !(o->flags & RTG_RENDER_FUSED) &&
+    // path tracing runs in the fused kernel only (its GI chains live on the per-thread stack)
+    const bool fused_only = (o->flags & RTG_RENDER_FUSED) || C.path_tracing;
+    const bool use_tree = s->tree_ok && !fused_only &&
                           ((o->flags & RTG_RENDER_TREE) || work >= (1ll << 21));
     if (use_tree) {
         float4* acc = (float4*)d_accum;
@@ -600,7 +637,7 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
         if (ev) s->timed_stages = rtg::TREE_STAGES;
         return RTG_OK;
     }
-    if (s->wave_ok && !(o->flags & RTG_RENDER_FUSED)) {
+    if (s->wave_ok && !fused_only) {
         const size_t rows = (size_t)(P.row_end - P.row_begin);
         int rc = ensure_wave(s, rows * C.width, s->num_slots, (size_t)P.num_tiles);
         if (rc) return rc;

@@ -75,7 +75,13 @@ DEV uint64_t root_key(uint64_t seed, int pixel, int sample) {
     return mix64(mix64(seed ^ 0xD1B54A32D192ED03ULL) ^ ((uint64_t)(uint32_t)pixel * 0x9E3779B97F4A7C15ULL) ^
                  ((uint64_t)(uint32_t)sample << 1));
 }
-enum { RP_MOTION = 1, RP_DOF = 2, RP_JITTER = 3, RP_AREA = 4, RP_ENV = 5, RP_ROUGH_REFL = 6, RP_ROUGH_REFR = 7 };
+// double draw (std::uniform_real_distribution<> of MeshLight::getSample, meshLight.h:31-36)
+DEV double rndd(uint64_t key, uint32_t purpose, uint32_t idx) {
+    uint64_t h = mix64(key ^ mix64(((uint64_t)purpose << 32) | idx));
+    return (double)(h >> 11) * (1.0 / 9007199254740992.0);
+}
+enum { RP_MOTION = 1, RP_DOF = 2, RP_JITTER = 3, RP_AREA = 4, RP_ENV = 5, RP_ROUGH_REFL = 6, RP_ROUGH_REFR = 7,
+       RP_GI = 8, RP_MESHLIGHT = 9 };
 
 // ---------------------------------------------------------------------------
 // Counters
@@ -850,11 +856,15 @@ DEV f3 ks_coeff(const DevScene& S, const ShadeCtx& c) {                // raytra
     return refl;
 }
 
-DEV f3 shade(const DevScene& S, const ShadeCtx& c, f3 w_i, f3 w_o, f3 Li) {
+// Shade (raytracer.cpp:192-206).  TP: also ray.throughput *= brdf (:202), which Russian
+// roulette reads (path tracing only).
+template <bool TP = false>
+DEV f3 shade(const DevScene& S, const ShadeCtx& c, f3 w_i, f3 w_o, f3 Li, f3* tp = nullptr) {
     if (c.mat->brdf >= 0) {
         float costheta_i = fmax0(dot(w_i, c.s.n));
         f3 kd = kd_coeff(S, c), ks = ks_coeff(S, c);
         f3 res = brdf_apply(S.brdfs[c.mat->brdf], c.mat->refractive_index, kd, ks, w_i, w_o, c.s.n);
+        if (TP) *tp = mulv(*tp, res);
         return muls(mulv(res, Li), costheta_i);
     }
     f3 kd = kd_coeff(S, c);                                             // GetDiffuse
@@ -893,15 +903,37 @@ DEV bool in_shadow_dir(const DevScene& S, f3 p, f3 n, f3 lightDir, float mbTime,
 // type order point, area, env, dir, spot: the incident direction, the irradiance and,
 // where the reference casts one, the shadow ray (IsInShadow :567-584 /
 // IsInShadowDirectional :555-566).
+// MeshLight::getSample (meshLight.h:27-47) and the irradiance of SampleDirectLighting's
+// mesh-light branch (raytracer.cpp:780-803: radiance * weight * 2 * M_PI, no distance
+// term).  The reference draws the face from uniform_int_distribution(0, faceCount) --
+// inclusive, so 1 draw in faceCount+1 indexes past the face vector (undefined); here the
+// face is uniform over the faceCount faces.
+DEV void mesh_light_sample(const DevScene& S, int l, uint64_t key, f3& pos, f3& E) {
+    const DevMeshLight& L = S.mesh_lights[l];
+    int k = (int)(rndd(key, RP_MESHLIGHT, 3 * l) * L.face_count);
+    k = k < L.face_count ? k : L.face_count - 1;
+    const DevLightFace& F = S.light_faces[L.face_begin + k];
+    const double selectionWeight = F.area / L.surface_area;
+    const double rand1 = rndd(key, RP_MESHLIGHT, 3 * l + 1);
+    const double rand2 = rndd(key, RP_MESHLIGHT, 3 * l + 2);
+    const f3 a = ld3(F.v0), b = ld3(F.v1), c = ld3(F.v2);
+    f3 q = add(muls(b, (float)(1 - rand2)), muls(c, (float)rand2));
+    pos = add(muls(a, (float)(1 - sqrt(rand1))), muls(q, (float)sqrt(rand1)));
+    pos = xform(L.xf, pos, 1.0f);                                      // ApplyTransformToPoint(transform)
+    E = muls(muls(muls(ld3(L.radiance), (float)selectionWeight), 2.0f), (float)RT_PI);
+}
+
 struct LightSample {
     f3 w_i, E;
     bool shadow;
+    bool skip;         // mesh light hit by this node's GI ray (raytracer.cpp:784): no term
     Ray sr;
     float minT, limit;
 };
-DEV LightSample light_sample(const DevScene& S, int slot, f3 p, f3 n, uint64_t key) {
+DEV LightSample light_sample(const DevScene& S, int slot, f3 p, f3 n, uint64_t key, int skipId = -1) {
     LightSample ls;
     ls.shadow = true;
+    ls.skip = false;
     ls.sr.o = add(p, muls(n, S.eps));
     f3 lpos = mk(0, 0, 0);
     bool positional = true;
@@ -939,8 +971,17 @@ DEV LightSample light_sample(const DevScene& S, int slot, f3 p, f3 n, uint64_t k
         ls.minT = INFINITY;
         ls.limit = INFINITY;
         positional = false;
+    } else if ((i -= S.num_dir) >= S.num_spot) {
+        i -= S.num_spot;                                                // mesh lights (:780-803)
+        ls.skip = S.mesh_lights[i].id == skipId;
+        f3 sp, E;
+        mesh_light_sample(S, i, key, sp, E);
+        lpos = sp;
+        f3 w_i = sub(sp, p);
+        float dist = len(w_i);
+        ls.w_i = divs(w_i, dist);
+        ls.E = E;
     } else {
-        i -= S.num_dir;
         const DevSpotLight& L = S.spot_lights[i];
         const f3 lp = ld3(L.pos);
         lpos = lp;
@@ -976,19 +1017,23 @@ DEV LightSample light_sample(const DevScene& S, int slot, f3 p, f3 n, uint64_t k
 // SampleDirectLighting (raytracer.cpp:701-805): the unshadowed lights' Shade terms summed in
 // slot order.  One trace and one Shade call site for all light types (the BRDF code and the
 // traversal are inlined once).
-template <bool STATS>
-DEV f3 direct(const DevScene& S, const ShadeCtx& c, f3 w_o, float mbTime, uint64_t key, Cnt<STATS>& cn) {
+// TP / skipId: path tracing -- throughput update per Shade, and the mesh light the node's
+// GI ray hit is not sampled (raytracer.cpp:92,784).
+template <bool STATS, bool TP = false>
+DEV f3 direct(const DevScene& S, const ShadeCtx& c, f3 w_o, float mbTime, uint64_t key, Cnt<STATS>& cn,
+              int skipId = -1, f3* tp = nullptr) {
     f3 color = mk(0, 0, 0);
     const f3 p = c.s.p, n = c.s.n;
-    const int nslots = S.num_point + S.num_area + S.num_env + S.num_dir + S.num_spot;
+    const int nslots = S.num_point + S.num_area + S.num_env + S.num_dir + S.num_spot + S.num_mesh;
     for (int l = 0; l < nslots; ++l) {
-        LightSample ls = light_sample(S, l, p, n, key);
+        LightSample ls = light_sample(S, l, p, n, key, skipId);
+        if (ls.skip) continue;
         if (ls.shadow) {
             Hit h;
             cn.shd();
             if (trace<true, STATS>(S, ls.sr, mbTime, ls.minT, ls.limit, h, cn)) continue;
         }
-        color = add(color, shade(S, c, ls.w_i, w_o, ls.E));
+        color = add(color, shade<TP>(S, c, ls.w_i, w_o, ls.E, tp));
     }
     return color;
 }

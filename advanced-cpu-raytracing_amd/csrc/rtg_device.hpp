@@ -38,6 +38,7 @@ struct DevObject {
     double inv[12];                 // rows 0..2 of inverseTransform
     double invT[12];                // rows 0..2 of inverseTransposeTransform
     double baseInvT[12];            // base mesh's inverseTransposeTransform
+    int id, pad2, pad3, pad4;       // Shape::id (XML id; spheres: never a light's id)
 };
 
 struct DevMaterial {
@@ -71,6 +72,20 @@ struct DevSpotLight {
     double cos_half_coverage, cos_half_falloff;
 };
 
+// MeshLight (meshLight.h:9-47): a LightMesh object sampled by SampleDirectLighting
+// (raytracer.cpp:780-803).  Its faces (BVH-permuted order, as MeshLight::faces is after
+// the in-place BVH build) are copied to light_faces[face_begin, +face_count).
+struct DevMeshLight {
+    int id, face_begin, face_count, pad0;
+    float radiance[4];
+    double surface_area, pad1;
+    double xf[12];                  // rows 0..2 of Mesh::transform (ApplyTransformToPoint)
+};
+struct DevLightFace {
+    float v0[4], v1[4], v2[4];      // object-space vertices
+    double area, pad0;
+};
+
 enum : int { LEAF_EXT = 0x7FFFFFFF };
 
 // Scene feature bits (kernel specialisation): spheres, mesh instances, any mesh with a
@@ -96,9 +111,11 @@ struct DevScene {
     const DevDirLight* __restrict__ dir_lights;
     const DevSpotLight* __restrict__ spot_lights;
     const int* __restrict__ env_images;
+    const DevMeshLight* __restrict__ mesh_lights;
+    const DevLightFace* __restrict__ light_faces;
     const int* __restrict__ perm;    // Perlin permutation (512) and gradients (12x3)
     const float* __restrict__ grad;
-    int num_objects, num_point, num_area, num_dir, num_spot, num_env;
+    int num_objects, num_point, num_area, num_dir, num_spot, num_env, num_mesh;
     int max_depth, bg_texture;
     float eps;
     float ambient[3];
@@ -110,7 +127,7 @@ struct DevCamera {
     float left, right_ext, bottom, top;
     float focus_distance, aperture;
     int width, height, spp;
-    int path_tracing, next_event;
+    int path_tracing, next_event, importance_sampling, russian_roulette;   // RendererParams (rendererParams.h)
 };
 
 struct RenderParams {

@@ -512,7 +512,7 @@ template <bool STATS, int FEAT>
 static hipError_t tree_pass(TreeState& T, const DevScene& S, const DevCamera& C, const RenderParams& P, int s,
                             bool first, bool last, float* hdr, unsigned char* l, float4* accum, DevCounters* cnt,
                             hipStream_t st, hipEvent_t* ev) {
-    const int ns = S.num_point + S.num_area + S.num_env + S.num_dir + S.num_spot;
+    const int ns = S.num_point + S.num_area + S.num_env + S.num_dir + S.num_spot + S.num_mesh;
     const int npix = (P.row_end - P.row_begin) * C.width;
     const int pixel_base = P.row_begin * C.width;
     hipError_t e;

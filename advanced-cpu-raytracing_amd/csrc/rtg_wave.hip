@@ -204,6 +204,18 @@ __global__ __launch_bounds__(256) void k_shade(const DevScene S, const DevCamera
         }
         push(lit, lp, false);
     }
+    for (int l = 0; l < S.num_mesh; ++l, ++slot) {                  // mesh lights (:780-803)
+        f3 sp = mk(0, 0, 0);
+        if (lit) {
+            f3 E;
+            mesh_light_sample(S, l, key, sp, E);
+            f3 w_i = sub(sp, p);
+            float dist = len(w_i);
+            w_i = divs(w_i, dist);
+            put(shade(S, c, w_i, w_o, E));
+        }
+        push(lit, sp, false);
+    }
     __syncthreads();
     if (threadIdx.x == 0) W.q_count[blockIdx.x] = seg_count;
     flush_counters<STATS>(cn, counters);
@@ -257,7 +269,7 @@ template <bool STATS, int FEAT>
 static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W,
                                 float* hdr, unsigned char* l, DevCounters* cnt, hipStream_t st, hipEvent_t* ev) {
     const int npix = (P.row_end - P.row_begin) * C.width;
-    const int nshadow = S.num_point + S.num_area + S.num_dir + S.num_spot;
+    const int nshadow = S.num_point + S.num_area + S.num_dir + S.num_spot + S.num_mesh;
     float4* accum = W.accum;
     for (int s = P.sample_begin; s < P.sample_begin + P.sample_count; ++s) {
         const int first = s == P.sample_begin, last = s == P.sample_begin + P.sample_count - 1;

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 1
+#define RTG_ABI_VERSION 2
 
 enum rtg_status {
     RTG_OK = 0,
@@ -100,6 +100,11 @@ typedef struct {
     double cos_half_coverage, cos_half_falloff;   /* spotLight.h:24-25 */
 } rtg_spot_light;
 typedef struct { int32_t image; int32_t pad0; } rtg_env_light;
+/* MeshLight (meshLight.h:9-47), in scene.meshLights order (parser.cpp:1474-1481).
+ * object: its index in objects[] (a LightMesh entry); radiance: its own <Radiance> --
+ * the emissive material carries the radiance of the LAST LightMesh sharing it
+ * (parser.cpp:1484-1487), the light keeps its own (raytracer.cpp:800). */
+typedef struct { int32_t object; rtg_float3 radiance; } rtg_mesh_light;
 
 /* Images: texels stored as float, w*h*channels, row-major (LDRImage.h:16-26 keeps
  * the raw 0..255 byte values; HDRImage.h keeps linear floats). */
@@ -219,7 +224,7 @@ typedef struct {
     const rtg_mesh* meshes;           int32_t num_meshes;
     const rtg_face* faces;            int64_t num_faces;
     const rtg_bvh_node* nodes;        int64_t num_nodes;
-    int32_t num_mesh_lights;          /* LightMesh sampling is not implemented: must be 0 */
+    const rtg_mesh_light* mesh_lights; int32_t num_mesh_lights;
     int32_t pad0;
 } rtg_scene_desc;
 

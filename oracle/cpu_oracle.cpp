@@ -15,7 +15,8 @@
 //   BoundingBox::doesIntersect    shape.hpp:78-100
 //   PerformShading                raytracer.cpp:65-134
 //   Shade / GetDiffuse / ...      raytracer.cpp:192-206, 474-554
-//   SampleDirectLighting          raytracer.cpp:701-805
+//   SampleDirectLighting          raytracer.cpp:701-805 (+ MeshLight::getSample, meshLight.h:27-47)
+//   ComputeGlobalIllumination     raytracer.cpp:135-191 (path tracing, Russian roulette)
 //   IsInShadow / CastShadowRay    raytracer.cpp:555-623
 //   Mirror/Dielectric/Conductor   raytracer.cpp:208-472
 //   BRDFs                         brdf{Phong,BlinnPhong,ModifiedPhong,ModifiedBlinnPhong,TorranceSparrow}.cpp
@@ -101,7 +102,17 @@ uint64_t root_key(uint64_t seed, int pixel, int sample) {
     return mix64(mix64(seed ^ 0xD1B54A32D192ED03ULL) ^ ((uint64_t)(uint32_t)pixel * 0x9E3779B97F4A7C15ULL) ^
                  ((uint64_t)(uint32_t)sample << 1));
 }
-enum { RP_MOTION = 1, RP_DOF = 2, RP_JITTER = 3, RP_AREA = 4, RP_ENV = 5, RP_ROUGH_REFL = 6, RP_ROUGH_REFR = 7 };
+double rndd(uint64_t key, uint32_t purpose, uint32_t idx) {
+    uint64_t h = mix64(key ^ mix64(((uint64_t)purpose << 32) | idx));
+    return (double)(h >> 11) * (1.0 / 9007199254740992.0);
+}
+enum { RP_MOTION = 1, RP_DOF = 2, RP_JITTER = 3, RP_AREA = 4, RP_ENV = 5, RP_ROUGH_REFL = 6, RP_ROUGH_REFR = 7,
+       RP_GI = 8, RP_MESHLIGHT = 9 };
+// Russian roulette never ends a path that keeps hitting diffuse surfaces (the throughput
+// it tests is renormalised to 1 at every bounce, raytracer.cpp:137-146), so the
+// reference recursion is unbounded; the GPU keeps at most kMaxLevel nested ray-tree
+// nodes (its per-thread frame stack) and so does this restatement.
+const int kMaxLevel = 32;
 
 const int kPerm256[256] = {
     151, 160, 137, 91,  90,  15,  131, 13,  201, 95,  96,  53,  194, 233, 7,   225, 140, 36,  103, 30,  69,  142,
@@ -141,7 +152,9 @@ struct Ray {
     HitInfo hitInfo;
     float refractiveIndexOfCurrentMedium = 1.0f;
     float motionBlurTime = 0.f;
+    Vec3f throughput = V(1.0f, 1.0f, 1.0f);
     uint64_t key = 0;
+    int level = 0;                    // ray-tree level (camera ray 0)
 };
 
 class Tracer {
@@ -211,7 +224,9 @@ private:
         ray.hitInfo.minT = INFINITY;
         ray.refractiveIndexOfCurrentMedium = original.refractiveIndexOfCurrentMedium;
         ray.motionBlurTime = original.motionBlurTime;
+        ray.throughput = original.throughput;
         ray.key = child_key(original.key, slot);
+        ray.level = original.level + 1;
         return ray;
     }
 
@@ -757,6 +772,63 @@ private:
         }
     }
 
+    // ---- raytracer.cpp:135-191 (GetNormalizedRandom draws -> counter RNG keyed by the node)
+    Vec3f ComputeGlobalIllumination(Ray& ray, const rtg_material& orgMat, Vec3f& w_o, int recDepth, int& hitMeshLightId) {
+        if (cam.russian_roulette) {
+            float probTest = rnd(ray.key, RP_GI, 0);
+            float maxThroughput = smax(ray.throughput.x, smax(ray.throughput.x, ray.throughput.z));
+            if (probTest > maxThroughput && recDepth <= 0) return V(0, 0, 0);
+            ray.throughput = ray.throughput / maxThroughput;
+        } else if (recDepth <= 0) {
+            return V(0, 0, 0);
+        }
+        if (ray.level >= kMaxLevel) return V(0, 0, 0);           // frame-stack bound (see kMaxLevel)
+        float rand1 = rnd(ray.key, RP_GI, 1);
+        float rand2 = rnd(ray.key, RP_GI, 2);
+        float phi = 2 * M_PI * rand1;
+        float theta = 0.0f;
+        if (cam.importance_sampling) theta = std::asin(std::sqrt(rand2));
+        else theta = std::acos(rand2);
+        Vec3f u, v;
+        GetOrthonormalBasis(ray.hitInfo.normal, u, v);
+        Vec3f newDir = u * std::sin(theta) * std::cos(phi) + ray.hitInfo.normal * std::cos(theta) +
+                       v * std::sin(theta) * std::sin(phi);
+        newDir = makeUnit(newDir);
+        Vec3f newOrigin = ray.hitInfo.hitPoint + ray.hitInfo.normal * 0.0001;
+        Ray globalRay = GenerateSecondaryRay(ray, newDir, newOrigin, 2);
+        cnt.secondary++;
+        IntersectObjects(globalRay);
+        Vec3f globalRaysColor = V(0, 0, 0);
+        if (globalRay.hitInfo.hasHit) {
+            const rtg_material& mat = S.materials[globalRay.hitInfo.matId];
+            if (mat.type == RTG_MAT_EMISSIVE) hitMeshLightId = ShapeId(globalRay.hitInfo.obj);
+            Vec3f transferredLight = PerformShading(globalRay, globalRay.origin, recDepth - 1);
+            globalRaysColor = Shade(ray, orgMat, globalRay.dir, w_o, transferredLight) * 2.0f * M_PI;
+        }
+        return globalRaysColor;
+    }
+    // Shape::id of an object (spheres never get one in the reference: no light matches it)
+    int ShapeId(int obj) const { return S.objects[obj].kind == RTG_OBJ_SPHERE ? INT32_MIN : S.objects[obj].id; }
+
+    // ---- meshLight.h:27-47 (face drawn uniformly over the faceCount faces; the reference's
+    // uniform_int_distribution(0, faceCount) also draws the out-of-range index faceCount)
+    void MeshLightSample(int l, uint64_t key, Vec3f& pos, double& weight) {
+        const rtg_mesh_light& L = S.mesh_lights[l];
+        const rtg_object& ob = S.objects[L.object];
+        const rtg_mesh& M = S.meshes[ob.mesh];
+        int k = (int)(rndd(key, RP_MESHLIGHT, 3 * l) * M.face_count);
+        if (k >= M.face_count) k = M.face_count - 1;
+        const rtg_face& face = S.faces[M.face_offset + k];
+        double selectionWeight = face.area / M.surface_area;
+        double rand1 = rndd(key, RP_MESHLIGHT, 3 * l + 1);
+        double rand2 = rndd(key, RP_MESHLIGHT, 3 * l + 2);
+        Vec3f a = V(face.v0), b = V(face.v1), c = V(face.v2);
+        Vec3f q = b * (1 - rand2) + c * rand2;
+        pos = a * (1 - std::sqrt(rand1)) + q * std::sqrt(rand1);
+        pos = applyT(ob.transform, pos, 1.0f);
+        weight = selectionWeight;
+    }
+
     Vec3f Shade(Ray& ray, const rtg_material& mat, Vec3f w_i, Vec3f w_o, Vec3f Li) {   // raytracer.cpp:192-206
         const rtg_object& ob = S.objects[ray.hitInfo.obj];
         if (mat.brdf >= 0) {
@@ -764,6 +836,7 @@ private:
             Vec3f kd = DiffuseCoeff(ray, ob, mat);
             Vec3f ks = SpecularCoeff(ray, ob, mat);
             Vec3f res = BrdfApply(S.brdfs[mat.brdf], mat, kd, ks, w_i, w_o, ray.hitInfo.normal);
+            ray.throughput = ray.throughput * res;
             return res * Li * costheta_i;
         }
         Vec3f kd = DiffuseCoeff(ray, ob, mat);
@@ -776,7 +849,7 @@ private:
         return diffuse + specular;
     }
 
-    Vec3f SampleDirectLighting(Ray& ray, const rtg_material& mat, Vec3f& w_o) {   // raytracer.cpp:701-805
+    Vec3f SampleDirectLighting(Ray& ray, const rtg_material& mat, Vec3f& w_o, int lightIDToSkip) {   // raytracer.cpp:701-805
         Vec3f color = V(0, 0, 0);
         for (int i = 0; i < S.num_point_lights; i++) {
             const rtg_point_light& light = S.point_lights[i];
@@ -835,6 +908,19 @@ private:
                 }
             }
             color = color + Shade(ray, mat, w_i, w_o, E);
+        }
+        for (int i = 0; i < S.num_mesh_lights; i++) {
+            const rtg_mesh_light& L = S.mesh_lights[i];
+            if (S.objects[L.object].id == lightIDToSkip) continue;
+            Vec3f lightSamplePos;
+            double weight;
+            MeshLightSample(i, ray.key, lightSamplePos, weight);
+            if (IsInShadow(ray, lightSamplePos)) continue;
+            Vec3f w_i = lightSamplePos - ray.hitInfo.hitPoint;
+            float distToLight = len(w_i);
+            w_i = w_i / distToLight;
+            Vec3f rad = V(L.radiance) * weight * 2 * M_PI;
+            color = color + Shade(ray, mat, w_i, w_o, rad);
         }
         return color;
     }
@@ -997,9 +1083,12 @@ private:
         bool travellingInsideAnObject = ray.refractiveIndexOfCurrentMedium > refractiveIndexOfVacuum;
         if (mat.type == RTG_MAT_EMISSIVE) return V(mat.radiance) * 2.0f * M_PI;
         if (ob.tex_replace_all >= 0) return TexRGB(S.textures[ob.tex_replace_all], ray.hitInfo.u, ray.hitInfo.v);
-        if (!travellingInsideAnObject) {
+        int hitLightMeshId = -1;
+        if (cam.path_tracing) color = color + ComputeGlobalIllumination(ray, mat, w_o, recursionDepth, hitLightMeshId);
+        bool sampleDirectLight = !cam.path_tracing || cam.next_event;
+        if (!travellingInsideAnObject && sampleDirectLight) {
             color = color + V(S.ambient_light) * V(mat.ambient);
-            color = color + SampleDirectLighting(ray, mat, w_o);
+            color = color + SampleDirectLighting(ray, mat, w_o, hitLightMeshId);
         }
         if (mat.type == RTG_MAT_MIRROR) {
             color = color + ComputeMirrorReflection(ray, mat, w_o, recursionDepth);

@@ -8,6 +8,10 @@
 //       (main.cpp:102-105).  Writes "RTGF" int32 w, int32 h, then w*h*3 float32 RGB,
 //       row-major 3*(x+y*w) (main.cpp:109).  Deterministic scenes only (the reference's
 //       random streams are seeded from rand() and raced by its threads).
+//   refdriver dumpavg <scene.xml> <out.bin> <n> [camera]
+//       Stochastic scenes (path tracing, area / environment lights): n RenderPixel calls per
+//       pixel, single-threaded.  Writes "RTGV" int32 w, h, n, then the per-pixel mean and
+//       the variance of that mean (w*h*3 float32 each) -- the statistical golden.
 //   refdriver bench <scene.xml> <threads> <reps> [camera]
 //       Times the reference's row-band render exactly as main.cpp:164-185 partitions it
 //       (rows [t*(H/T), (t+1)*(H/T)) per thread; spawn -> join), spp==1 per pixel via
@@ -26,6 +30,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <thread>
+#include <algorithm>
 #include <vector>
 
 #include "raytracer.hpp"
@@ -54,6 +59,42 @@ static int dump(const char* xml, const char* out, int ci) {
     std::fwrite("RTGF", 1, 4, f);
     std::fwrite(hdr, sizeof(int32_t), 2, f);
     std::fwrite(img.data(), sizeof(float), img.size(), f);
+    std::fclose(f);
+    return 0;
+}
+
+static int dumpavg(const char* xml, const char* out, int n, int ci) {
+    Scene scene;
+    scene.loadFromXml(xml);
+    Raytracer renderer(scene);
+    if (ci < 0 || ci >= (int)scene.cameras.size() || n < 2) { std::fprintf(stderr, "bad camera / n\n"); return 2; }
+    Camera& cam = scene.cameras[ci];
+    if (cam.IsPathTracingEnabled()) renderer.EnablePathTracing(cam.GetRendererParams());
+    renderer.activeCamera = &cam;
+    const int w = cam.imageWidth, h = cam.imageHeight;
+    std::vector<float> mean((size_t)w * h * 3), var((size_t)w * h * 3);
+    for (int y = 0; y < h; ++y)
+        for (int x = 0; x < w; ++x) {
+            double s[3] = {0, 0, 0}, q[3] = {0, 0, 0};
+            for (int k = 0; k < n; ++k) {
+                Vec3f c = renderer.RenderPixel(x, y, cam);
+                const double v[3] = {c.x, c.y, c.z};
+                for (int j = 0; j < 3; ++j) { s[j] += v[j]; q[j] += v[j] * v[j]; }
+            }
+            size_t i = 3 * ((size_t)x + (size_t)y * w);
+            for (int j = 0; j < 3; ++j) {
+                const double m = s[j] / n;
+                mean[i + j] = (float)m;
+                var[i + j] = (float)(std::max(0.0, q[j] / n - m * m) / (n - 1));
+            }
+        }
+    FILE* f = std::fopen(out, "wb");
+    if (!f) { std::perror(out); return 1; }
+    int32_t hdr[3] = {w, h, n};
+    std::fwrite("RTGV", 1, 4, f);
+    std::fwrite(hdr, sizeof(int32_t), 3, f);
+    std::fwrite(mean.data(), sizeof(float), mean.size(), f);
+    std::fwrite(var.data(), sizeof(float), var.size(), f);
     std::fclose(f);
     return 0;
 }
@@ -116,6 +157,8 @@ int main(int argc, char** argv) {
     if (argc >= 8 && !std::strcmp(argv[1], "tonemap"))
         return tonemap(argv[2], std::atof(argv[3]), std::atof(argv[4]), std::atof(argv[5]), std::atof(argv[6]), argv[7]);
     if (argc >= 4 && !std::strcmp(argv[1], "dump")) return dump(argv[2], argv[3], argc > 4 ? std::atoi(argv[4]) : 0);
+    if (argc >= 5 && !std::strcmp(argv[1], "dumpavg"))
+        return dumpavg(argv[2], argv[3], std::atoi(argv[4]), argc > 5 ? std::atoi(argv[5]) : 0);
     if (argc >= 5 && !std::strcmp(argv[1], "bench"))
         return bench(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), argc > 5 ? std::atoi(argv[5]) : 0);
     std::fprintf(stderr, "usage: refdriver dump <scene.xml> <out.bin> [camera] | bench <scene.xml> <threads> <reps> [camera]\n");

@@ -47,6 +47,10 @@ FIXTURES = {
     "synth_10k": ("generated", 256, 144, "exact", None),
     "ply_quads": ("generated", 160, 120, "exact", None),
     "bump_normal": ("generated", 200, 150, "exact", None),
+    # path tracing (raytracer.cpp:135-191): per-pixel mean of AVG_SAMPLES reference samples
+    "pt_cornell": ("generated", 64, 64, "stochastic_avg", None),
+    "pt_nee": ("generated", 64, 64, "stochastic_avg", None),
+    "pt_rr": ("generated", 64, 64, "stochastic_avg", None),
     "area_light": ("authored", 160, 160, "stochastic", None),
     "env_light": ("authored", 160, 120, "stochastic", None),
     "dof_motion": ("authored", 160, 120, "stochastic", None),
@@ -353,6 +357,206 @@ def make_bump_normal():
         f.write(xml)
 
 
+PT_BOX = """<Scene>
+    <MaxRecursionDepth>DEPTH</MaxRecursionDepth>
+    <BackgroundColor>0 0 0</BackgroundColor>
+    <ShadowRayEpsilon>1e-3</ShadowRayEpsilon>
+    <Cameras>
+        <Camera id="1">
+            <Position>0 0 7.5</Position>
+            <Gaze>0 0 -1</Gaze>
+            <Up>0 1 0</Up>
+            <NearPlane>-1 1 -1 1</NearPlane>
+            <NearDistance>2.5</NearDistance>
+            <ImageResolution>64 64</ImageResolution>
+            <ImageName>NAME.png</ImageName>
+            <Renderer>PathTracing</Renderer>
+            <RendererParams>PARAMS</RendererParams>
+        </Camera>
+    </Cameras>
+    <Lights>
+        <AmbientLight>5 5 5</AmbientLight>
+        LIGHTS
+    </Lights>
+    <BRDFs>
+        <OriginalBlinnPhong id="1">
+            <Exponent>30</Exponent>
+        </OriginalBlinnPhong>
+        <TorranceSparrow id="2" kdfresnel="true">
+            <Exponent>40</Exponent>
+        </TorranceSparrow>
+    </BRDFs>
+    <Materials>
+        <Material id="1">
+            <AmbientReflectance>0.2 0.2 0.2</AmbientReflectance>
+            <DiffuseReflectance>KD1</DiffuseReflectance>
+            <SpecularReflectance>0 0 0</SpecularReflectance>
+            <PhongExponent>1</PhongExponent>
+        </Material>
+        <Material id="2">
+            <AmbientReflectance>0.2 0.05 0.05</AmbientReflectance>
+            <DiffuseReflectance>0.7 0.15 0.15</DiffuseReflectance>
+            <SpecularReflectance>0 0 0</SpecularReflectance>
+        </Material>
+        <Material id="3">
+            <AmbientReflectance>0.05 0.2 0.05</AmbientReflectance>
+            <DiffuseReflectance>0.15 0.7 0.15</DiffuseReflectance>
+            <SpecularReflectance>0 0 0</SpecularReflectance>
+        </Material>
+        <Material id="4" BRDF="1">
+            <AmbientReflectance>0.1 0.1 0.2</AmbientReflectance>
+            <DiffuseReflectance>0.3 0.4 0.8</DiffuseReflectance>
+            <SpecularReflectance>0.4 0.4 0.4</SpecularReflectance>
+        </Material>
+        <Material id="5" type="mirror">
+            <AmbientReflectance>0 0 0</AmbientReflectance>
+            <DiffuseReflectance>0.1 0.1 0.1</DiffuseReflectance>
+            <SpecularReflectance>0 0 0</SpecularReflectance>
+            <MirrorReflectance>0.8 0.8 0.8</MirrorReflectance>
+        </Material>
+        <Material id="6" BRDF="2">
+            <AmbientReflectance>0.2 0.2 0.1</AmbientReflectance>
+            <DiffuseReflectance>0.8 0.6 0.3</DiffuseReflectance>
+            <SpecularReflectance>0.5 0.5 0.5</SpecularReflectance>
+            <RefractionIndex>1.5</RefractionIndex>
+        </Material>
+        <Material id="7">
+            <AmbientReflectance>0 0 0</AmbientReflectance>
+            <DiffuseReflectance>0 0 0</DiffuseReflectance>
+            <SpecularReflectance>0 0 0</SpecularReflectance>
+        </Material>
+    </Materials>
+    <VertexData>
+        -2 -2 2
+        2 -2 2
+        2 -2 -2
+        -2 -2 -2
+        -2 2 2
+        2 2 2
+        2 2 -2
+        -2 2 -2
+        -0.7 1.99 0.7
+        0.7 1.99 0.7
+        0.7 1.99 -0.7
+        -0.7 1.99 -0.7
+        SPH1
+        SPH2
+    </VertexData>
+    <Objects>
+        <Mesh id="1">
+            <Material>1</Material>
+            <Faces>
+                1 2 3
+                1 3 4
+                BACK
+                CEILING
+            </Faces>
+        </Mesh>
+        WALLS
+        LIGHTMESH
+        <Sphere id="1">
+            <Material>SPHMAT</Material>
+            <Center>13</Center>
+            <Radius>0.8</Radius>
+        </Sphere>
+        <Sphere id="2">
+            <Material>6</Material>
+            <Center>14</Center>
+            <Radius>0.7</Radius>
+        </Sphere>
+    </Objects>
+</Scene>
+"""
+PT_WALLS = """<Mesh id="2">
+            <Material>2</Material>
+            <Faces>
+                1 4 8
+                1 8 5
+            </Faces>
+        </Mesh>
+        <Mesh id="3">
+            <Material>3</Material>
+            <Faces>
+                2 6 7
+                2 7 3
+            </Faces>
+        </Mesh>"""
+PT_SCENES = {
+    # path tracing without next-event estimation: the LightMesh is only reached by GI rays
+    # (SampleDirectLighting -- and so the reference's out-of-range face draw -- never runs)
+    "pt_cornell": dict(DEPTH="3", PARAMS="ImportanceSampling", LIGHTS="", SPHMAT="4", CEILING="5 7 6\n5 8 7",
+                       BACK="4 3 7\n4 7 8", WALLS=PT_WALLS,
+                       LIGHTMESH="""<LightMesh id="4">
+            <Material>7</Material>
+            <Radiance>12 12 12</Radiance>
+            <Faces>
+                9 11 10
+                9 12 11
+            </Faces>
+        </LightMesh>"""),
+    # next-event estimation + uniform hemisphere sampling, point and area lights, a mirror
+    # sphere (its GI and mirror children), an open box
+    "pt_nee": dict(DEPTH="2", PARAMS="NextEventEstimation", SPHMAT="5", CEILING="", LIGHTMESH="",
+                   BACK="4 3 7\n4 7 8", WALLS=PT_WALLS,
+                   LIGHTS="""<PointLight id="1">
+            <Position>0 1.5 1</Position>
+            <Intensity>60 60 60</Intensity>
+        </PointLight>
+        <AreaLight id="1">
+            <Position>0 1.9 -0.5</Position>
+            <Normal>0 -1 0</Normal>
+            <Radiance>30 30 30</Radiance>
+            <Size>1</Size>
+        </AreaLight>"""),
+    # Russian roulette (+ NEE, importance sampling) over a floor only: every bounce multiplies
+    # by ~pi*kd > 1 in the reference's estimator and RR never ends a diffuse chain (the
+    # throughput it tests is renormalised each bounce), so only a scene GI rays mostly
+    # escape has a finite mean to compare
+    "pt_rr": dict(DEPTH="1", PARAMS="NextEventEstimation RussianRoulette ImportanceSampling", SPHMAT="5",
+                  CEILING="", LIGHTMESH="", BACK="", WALLS="", KD1="0.2 0.2 0.2", SPH1="-0.8 -0.6 -0.6",
+                  SPH2="0.9 -0.5 0.4",
+                  LIGHTS="""<PointLight id="1">
+            <Position>1 2.5 2</Position>
+            <Intensity>1500 1500 1500</Intensity>
+        </PointLight>"""),
+}
+
+
+# Scenes with no reference golden: next-event estimation over a LightMesh runs
+# MeshLight::getSample, whose uniform_int_distribution(0, faceCount) reads one face past
+# the end of the face vector in 1 draw of faceCount+1 (undefined behaviour, meshLight.h:22)
+# -- these are checked GPU == oracle only ("parity unpinned" against the reference).
+PT_SCENES["mesh_light"] = dict(DEPTH="1", PARAMS="", SPHMAT="4", CEILING="5 7 6\n5 8 7", BACK="4 3 7\n4 7 8",
+                               WALLS=PT_WALLS, LIGHTS="", LIGHTMESH=PT_SCENES["pt_cornell"]["LIGHTMESH"])
+PT_SCENES["pt_meshlight"] = dict(PT_SCENES["mesh_light"], DEPTH="2",
+                                 PARAMS="NextEventEstimation ImportanceSampling")
+ORACLE_ONLY = ("mesh_light", "pt_meshlight")
+
+
+def make_pt(name):
+    xml = PT_BOX.replace("NAME", name)
+    if not PT_SCENES[name]["PARAMS"]:      # a classic (Whitted) camera
+        xml = xml.replace("            <Renderer>PathTracing</Renderer>\n            <RendererParams>PARAMS</RendererParams>\n", "")
+    opts = dict(KD1="0.7 0.7 0.7", SPH1="-0.8 -1.2 -0.6", SPH2="0.9 -1.3 0.4")
+    opts.update(PT_SCENES[name])
+    for k, v in opts.items():
+        xml = xml.replace(k, v)
+    with open(os.path.join(SCENES, name + ".xml"), "w") as f:
+        f.write(xml)
+
+
+def dump_avg(name, n):
+    """Per-pixel mean of n RenderPixel calls and the variance of that mean (refdriver dumpavg)."""
+    out = os.path.join(HERE, name + ".bin")
+    subprocess.run([DRIVER, "dumpavg", name + ".xml", out, str(n)], cwd=SCENES, check=True, stdout=subprocess.DEVNULL)
+    raw = open(out, "rb").read()
+    os.remove(out)
+    assert raw[:4] == b"RTGV"
+    w, h, nn = np.frombuffer(raw[4:16], np.int32)
+    body = np.frombuffer(raw[16:], np.float32).reshape(2, h, w, 3)
+    return body[0].copy(), body[1].copy(), int(nn)
+
+
 def prepare(name, src, w, h, edits):
     dst = os.path.join(SCENES, name + ".xml")
     if src == "generated":
@@ -362,6 +566,8 @@ def prepare(name, src, w, h, edits):
             make_ply_quads()
         elif name == "bump_normal":
             make_bump_normal()
+        elif name in PT_SCENES:
+            make_pt(name)
         elif name == "c2_cornell":
             gen.config_c2(SCENES, os.path.join(SCENES, "cornell_conductors.xml"), w, h)
         elif name == "c3_blob":
@@ -398,6 +604,9 @@ TONEMAP_SOURCES = ("env_light", "brdf_lights", "c3_blob", "cornell_conductors")
 TONEMAP_PARAMS = ((0.18, 1.0, 1.0, 2.2), (0.36, 0.0, 0.8, 2.0), (0.09, 5.0, 1.2, 1.8))
 
 
+AVG_SAMPLES = 1024
+
+
 def make_tonemap_goldens():
     out = {}
     for name in TONEMAP_SOURCES:
@@ -429,15 +638,24 @@ def main():
     if only == {"tonemap"}:
         make_tonemap_goldens()
         return
+    for name in ORACLE_ONLY:
+        if not only or name in only:
+            make_pt(name)
     for name, (src, w, h, kind, edits) in FIXTURES.items():
         if only and name not in only:
             continue
         prepare(name, src, w, h, edits)
-        img = dump(name)
-        np.savez_compressed(os.path.join(HERE, name + ".npz"), hdr=img)
+        extra = {}
+        if kind == "stochastic_avg":
+            img, var, n = dump_avg(name, AVG_SAMPLES)
+            np.savez_compressed(os.path.join(HERE, name + ".npz"), hdr=img, var=var)
+            extra = {"samples": n}
+        else:
+            img = dump(name)
+            np.savez_compressed(os.path.join(HERE, name + ".npz"), hdr=img)
         man[name] = {"xml": f"scenes/{name}.xml", "width": int(img.shape[1]), "height": int(img.shape[0]),
                      "kind": kind, "source": src if src.startswith("/") else src,
-                     "sha256": hashlib.sha256(img.tobytes()).hexdigest()}
+                     "sha256": hashlib.sha256(img.tobytes()).hexdigest(), **extra}
         print(name, img.shape, kind)
     path = os.path.join(HERE, "manifest.json")
     if only and os.path.exists(path):

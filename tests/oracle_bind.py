@@ -111,3 +111,57 @@ def compare(got, ref, rel=1e-4):
         "max_abs": float(np.nanmax(np.where(both_nan, 0, d))) if d.size else 0.0,
         "n_fail": int(np.sum(~ok)),
     }
+
+
+# ---------------------------------------------------------------------------
+# Statistical goldens (kind "stochastic_avg": path tracing).  The reference golden is the
+# per-pixel mean of n RenderPixel samples plus the variance of that mean (refdriver
+# dumpavg).  Renders here use a camera with NumSamples = spp, whose Gaussian-weighted mean
+# (main.cpp:60-101) has the variance of ~0.35*spp plain samples (the sigma = 1/6 px
+# Gaussian over stratified positions), computed by gauss_eff_fraction().
+# ---------------------------------------------------------------------------
+def load_golden_avg(name):
+    d = np.load(os.path.join(GOLDEN, name + ".npz"), allow_pickle=False)
+    return d["hdr"], d["var"]
+
+
+def gauss_eff_fraction(spp):
+    """Effective-sample fraction (sum w)^2 / (n sum w^2) of renderThreadMain's weights."""
+    rng = np.random.default_rng(0)
+    n = int(np.sqrt(spp))
+    row, col = np.divmod(np.arange(n * n), n)
+    fr = []
+    for _ in range(64):
+        sx = (col + rng.random(n * n)) / n - 0.5
+        sy = (row + rng.random(n * n)) / n - 0.5
+        w = np.exp(-0.5 * (sx * sx + sy * sy) * 36.0)
+        fr.append(w.sum() ** 2 / (len(w) * (w * w).sum()))
+    return float(np.mean(fr))
+
+
+def with_samples(xml_text, spp):
+    """The scene text with the camera's <NumSamples> set to spp."""
+    import re
+    xml_text = re.sub(r"\s*<NumSamples>[^<]*</NumSamples>", "", xml_text)
+    return xml_text.replace("<ImageName>", f"<NumSamples>{spp}</NumSamples>\n            <ImageName>", 1)
+
+
+def block_zscores(got, name, spp, block=8):
+    """z-scores of 8x8-pixel block means of `got` (rendered at spp samples per pixel)
+    against the reference's statistical golden `name`."""
+    ref, var = load_golden_avg(name)
+    n_ref = manifest()[name]["samples"]
+    h, w, _ = ref.shape
+    def blk(a):
+        return np.asarray(a, np.float64).reshape(h // block, block, w // block, block, 3).mean((1, 3))
+    vref = np.asarray(var, np.float64).reshape(h // block, block, w // block, block, 3).sum((1, 3)) / block ** 4
+    vgot = vref * n_ref / (spp * gauss_eff_fraction(spp))
+    return (blk(got) - blk(ref)) / np.sqrt(vref + vgot + 1e-12)
+
+
+def zscore_ok(z):
+    """Heavy-tailed estimators (GI rays that find the emitter): rms of |z| clipped at 10
+    below 1.5 and at most 2% of blocks beyond 4 sigma."""
+    a = np.minimum(np.abs(z), 10.0)
+    return float(np.sqrt(np.mean(a * a))) < 1.5 and float(np.mean(a > 4.0)) <= 0.02, \
+        {"rms": float(np.sqrt(np.mean(a * a))), "frac_gt4": float(np.mean(a > 4.0)), "max": float(np.abs(z).max())}

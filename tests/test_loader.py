@@ -181,3 +181,16 @@ def test_instances_take_base_mesh_bump_map(tmp_path, monkeypatch):
     nob = s.replace("<Textures>2</Textures>", "")
     _, b, _ = render(_scene(tmp_path, nob, "b.xml"))
     assert (np.abs(b - ref).max(-1) > 1e-3).mean() > 0.01
+
+
+def test_recursion_deeper_than_the_frame_stack_is_rejected(tmp_path, monkeypatch):
+    """MaxRecursionDepth beyond the kernels' 32-frame ray-tree stack is refused with
+    RTG_ERR_UNSUPPORTED (before any device work), never silently truncated."""
+    monkeypatch.chdir(SCENES)
+    s = open(os.path.join(SCENES, "spheres_mirror.xml")).read()
+    import re
+    s = re.sub(r"<MaxRecursionDepth>[^<]*</MaxRecursionDepth>", "<MaxRecursionDepth>40</MaxRecursionDepth>", s)
+    hs = rtgpu.HostScene(_scene(tmp_path, s))
+    with pytest.raises(rtgpu.RTGError) as e:
+        rtgpu.DeviceScene(hs, 0)
+    assert e.value.code == -6

@@ -106,3 +106,21 @@ def test_oracle_tonemap_matches_reference(case):
     name, (key, burn, sat, gamma), ref = ob.tonemap_goldens()[case]
     got = ob.tonemap(ob.load_golden(name), key, burn, sat, gamma)
     assert np.array_equal(got, ref), (name, key, burn, np.mean(got != ref))
+
+
+AVG = sorted(k for k, v in GOLD.items() if v["kind"] == "stochastic_avg")
+
+
+@pytest.mark.parametrize("name", AVG)
+def test_oracle_path_tracing_statistical_vs_reference(name, tmp_path):
+    """Path tracing (raytracer.cpp:135-191): the oracle's per-pixel estimate at 256 spp
+    against the reference's mean of 1024 samples, 8x8-block z-scores using the reference's
+    own per-pixel variance."""
+    xml = tmp_path / (name + ".xml")
+    xml.write_text(ob.with_samples(open(os.path.join(SCENES, name + ".xml")).read(), 256))
+    hs = rtgpu.HostScene(str(xml))
+    hdr, _, st = ob.render(hs, seed=11)
+    ok, info = ob.zscore_ok(ob.block_zscores(hdr, name, 256))
+    print(name, info, st)
+    assert ok, info
+    assert st["secondary_rays"] > st["camera_rays"] * 0.3      # GI rays were traced
