@@ -21,7 +21,8 @@ import os
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "librtgpu.so")
+# RTGPU_LIB: an alternative in-tree build of the same library (A/B kernel experiments)
+LIB_PATH = os.environ.get("RTGPU_LIB") or os.path.join(HERE, "librtgpu.so")
 
 RTG_RENDER_COUNT_STATS = 1
 RTG_RENDER_ACCUM_ONLY = 2
