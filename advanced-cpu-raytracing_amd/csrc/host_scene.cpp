@@ -14,6 +14,9 @@
 //     reproduced exactly so face order / node topology match the reference;
 //   * single-character transform ids (parser.cpp:663,689,699).
 #include <cfloat>
+#include <chrono>
+#include <cstdio>
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <limits>
@@ -125,6 +128,8 @@ private:
     void constructBVH(Geometry& g, std::vector<rtg_bvh_node>& nodes);
     BBox transformBoundingBox(const BBox& b, const M4& t);
     void flatten();
+    std::chrono::steady_clock::time_point tStart;
+    double bvhSeconds = 0.0;
 };
 
 std::string need_text(XmlNode* e, const char* what) {
@@ -136,6 +141,7 @@ std::string need_text(XmlNode* e, const char* what) {
 
 // ---------------------------------------------------------------------------
 void Loader::load(const std::string& path) {
+    tStart = std::chrono::steady_clock::now();
     XmlDocument file;
     if (!file.Load(path))
         fail(file.error.rfind("cannot open", 0) == 0 ? RTG_ERR_IO : RTG_ERR_PARSE,
@@ -356,7 +362,14 @@ void Loader::load(const std::string& path) {
         spheres.push_back(sp);
     }
 
+    const auto t0 = std::chrono::steady_clock::now();
     flatten();
+    if (std::getenv("RTG_HOST_TIMING")) {   // ingest phase timings (DESIGN.md measurements)
+        const auto t1 = std::chrono::steady_clock::now();
+        std::fprintf(stderr, "[rtg host] parse+faces %.3f s, bvh build %.3f s, flatten %.3f s\n",
+                     std::chrono::duration<double>(t0 - tStart).count(), bvhSeconds,
+                     std::chrono::duration<double>(t1 - t0).count());
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -983,7 +996,9 @@ void Loader::flatten() {
     for (size_t gi = 0; gi < geos.size(); ++gi) {
         Geometry& g = geos[gi];
         std::vector<rtg_bvh_node> nodes;
-        constructBVH(g, nodes);
+        const auto tb = std::chrono::steady_clock::now();
+        if (!S.deferBvh) constructBVH(g, nodes);
+        bvhSeconds += std::chrono::duration<double>(std::chrono::steady_clock::now() - tb).count();
         rtg_mesh m;
         std::memset(&m, 0, sizeof(m));
         m.face_offset = (int32_t)S.faces.size();

@@ -20,6 +20,7 @@ struct HostScene {
     int bgTexture = -1;
     bool motionBlurEnabled = false;
     std::vector<rtg_mesh_light> mesh_lights;
+    bool deferBvh = false;      // RTG_LOAD_DEVICE_BVH: faces in parse order, no BVH (built on the device)
     V3 ambient;
     std::vector<rtg_camera> cameras;
     std::vector<rtg_material> materials;

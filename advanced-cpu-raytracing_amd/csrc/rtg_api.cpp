@@ -60,6 +60,11 @@ struct DevBuf {
     T* p = nullptr;
     size_t n = 0;
     ~DevBuf() { if (p) (void)hipFree(p); }
+    hipError_t alloc(size_t count) {
+        if (p) { (void)hipFree(p); p = nullptr; }
+        n = count;
+        return count ? hipMalloc(&p, count * sizeof(T)) : hipSuccess;
+    }
     hipError_t upload(const std::vector<T>& v) {
         if (p) { (void)hipFree(p); p = nullptr; }   // hipFree waits for the device
         n = v.size();
@@ -80,6 +85,7 @@ struct rtg_scene {
     std::vector<rtg_camera> cameras;
     int max_depth = 0;
     DevBuf<float4> nodes, tris, face_n;
+    int node_count = 0;               // nodes in use (device-built BVH: <= nodes.n / 2)
     DevBuf<int2> node_ext;
     DevBuf<int> env_images;
     DevBuf<float2> face_uv;
@@ -135,11 +141,17 @@ const char* rtg_last_error(void) { return g_err.c_str(); }
 int rtg_abi_version(void) { return RTG_ABI_VERSION; }
 
 int rtg_host_scene_load_xml(const char* xml_path, rtg_host_scene** out) {
+    return rtg_host_scene_load_xml_ex(xml_path, 0, out);
+}
+
+int rtg_host_scene_load_xml_ex(const char* xml_path, uint32_t flags, rtg_host_scene** out) {
     if (!xml_path || !out) return set_err(RTG_ERR_INVALID, "null argument");
     *out = nullptr;
+    if (flags & ~(uint32_t)RTG_LOAD_DEVICE_BVH) return set_err(RTG_ERR_INVALID, "unknown load flags 0x%x", flags);
     std::unique_ptr<rtg_host_scene> hs(new (std::nothrow) rtg_host_scene);
     if (!hs) return set_err(RTG_ERR_NOMEM, "out of memory");
     std::string err;
+    hs->s.deferBvh = (flags & RTG_LOAD_DEVICE_BVH) != 0;
     int rc = hs->s.load(xml_path, err);
     if (rc != RTG_OK) return set_err(rc, "%s: %s", xml_path, err.c_str());
     *out = hs.release();
@@ -172,11 +184,74 @@ int rtg_desc_counts(const rtg_scene_desc* d, int64_t* num_objects, int64_t* num_
     return RTG_OK;
 }
 
+int rtg_scene_export_bvh(const rtg_scene* s, float* nodes, int64_t max_nodes, float* tris, int64_t max_faces,
+                         int64_t* num_nodes, int64_t* num_faces) {
+    if (!s) return set_err(RTG_ERR_INVALID, "null scene");
+    const int64_t nn = s->node_count, nf = (int64_t)(s->tris.n / 3);
+    if (num_nodes) *num_nodes = nn;
+    if (num_faces) *num_faces = nf;
+    HIP_TRY(hipSetDevice(s->device));
+    if (nodes && max_nodes >= nn) HIP_TRY(hipMemcpy(nodes, s->nodes.p, nn * 2 * sizeof(float4), hipMemcpyDeviceToHost));
+    if (tris && max_faces >= nf) HIP_TRY(hipMemcpy(tris, s->tris.p, nf * 3 * sizeof(float4), hipMemcpyDeviceToHost));
+    return RTG_OK;
+}
+
 int rtg_device_count(int32_t* count) {
     if (!count) return set_err(RTG_ERR_INVALID, "null argument");
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     *count = e == hipSuccess ? n : 0;
+    return RTG_OK;
+}
+
+// Device ingest: every mesh's BVH and face order built on the GPU (rtg_bvh.hip) straight
+// into the scene's walk buffers; facePerm receives the final order (mesh lights sample it).
+static int build_bvh_on_device(rtg_scene* sc, const rtg_scene_desc* d, bool anyUV, bool anyMapped,
+                               std::vector<int>& meshBegin, std::vector<int>& meshEnd, bool& bigleaf,
+                               std::vector<int>& facePerm) {
+    const int64_t F = d->num_faces;
+    const size_t maxNodes = (size_t)2 * F + 1;          // <= 2n - 1 per mesh, + the pad node
+    HIP_TRY(sc->nodes.alloc(2 * maxNodes));
+    HIP_TRY(sc->node_ext.alloc(maxNodes));
+    HIP_TRY(sc->tris.alloc(3 * F));
+    HIP_TRY(sc->face_n.alloc(F));
+    if (anyUV) HIP_TRY(sc->face_uv.alloc(3 * F));
+    if (anyMapped) HIP_TRY(sc->face_v12.alloc(2 * F));
+    HIP_TRY(hipMemset(sc->nodes.p, 0, sc->nodes.n * sizeof(float4)));
+    rtg_face* dfaces = nullptr;
+    int* dperm = nullptr;
+    HIP_TRY(hipMalloc(&dfaces, F * sizeof(rtg_face)));
+    struct Free { void* p; ~Free() { if (p) (void)hipFree(p); } } freeFaces{dfaces};
+    HIP_TRY(hipMemcpy(dfaces, d->faces, F * sizeof(rtg_face), hipMemcpyHostToDevice));
+    HIP_TRY(hipMalloc(&dperm, F * sizeof(int)));
+    Free freePerm{dperm};
+    hipStream_t st = nullptr;
+    int nodeBase = 0;
+    for (int m = 0; m < d->num_meshes; ++m) {
+        const rtg_mesh& M = d->meshes[m];
+        if (M.face_count <= 0 || M.face_offset < 0 || M.face_offset + (int64_t)M.face_count > F)
+            return set_err(RTG_ERR_INVALID, "mesh %d: bad face range", m);
+        // root box: the mesh's bbox (parser.cpp:1393-1468), carried by its Mesh object
+        const rtg_object* owner = nullptr;
+        for (int i = 0; i < d->num_objects && !owner; ++i)
+            if (d->objects[i].kind == RTG_OBJ_MESH && d->objects[i].mesh == m) owner = &d->objects[i];
+        if (!owner) return set_err(RTG_ERR_INVALID, "mesh %d: no Mesh object carries its bbox", m);
+        int count = 0;
+        bool bl = false;
+        HIP_TRY(rtg::build_mesh_bvh(dfaces + M.face_offset, M.face_count, owner->bbox_min, owner->bbox_max,
+                                    M.face_offset, nodeBase, sc->nodes.p, sc->node_ext.p, sc->tris.p, sc->face_n.p,
+                                    anyUV ? sc->face_uv.p : nullptr, anyMapped ? sc->face_v12.p : nullptr,
+                                    dperm + M.face_offset, &count, &bl, st));
+        meshBegin[m] = nodeBase;
+        meshEnd[m] = nodeBase + count;
+        nodeBase += count;
+        bigleaf |= bl;
+    }
+    sc->node_count = nodeBase + 1;                      // + the zeroed pad node
+    facePerm.resize(F);
+    HIP_TRY(hipMemcpy(facePerm.data(), dperm, F * sizeof(int), hipMemcpyDeviceToHost));
+    for (int m = 0; m < d->num_meshes; ++m)
+        for (int k = 0; k < d->meshes[m].face_count; ++k) facePerm[d->meshes[m].face_offset + k] += d->meshes[m].face_offset;
     return RTG_OK;
 }
 
@@ -222,13 +297,24 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     sc->max_depth = d->max_recursion_depth;
     sc->cameras.assign(d->cameras, d->cameras + d->num_cameras);
 
+    // Device ingest (desc without a BVH, RTG_LOAD_DEVICE_BVH): face preparation and the
+    // midpoint BVH are built on the GPU (rtg_bvh.hip); otherwise the host-built reference
+    // topology is re-laid here.
+    const bool gpuBuild = d->num_faces > 0 && d->num_nodes == 0;
+    bool anyMapped = false;
+    for (int i = 0; i < d->num_objects; ++i) {
+        const rtg_object& o = d->objects[i];
+        const bool uvmesh = o.kind != RTG_OBJ_SPHERE && d->meshes[o.mesh].has_uv;
+        if ((uvmesh && o.tex_normal >= 0) || ((uvmesh || o.kind == RTG_OBJ_SPHERE) && o.tex_bump >= 0)) anyMapped = true;
+    }
+
     // ---- BVH: reference topology -> pre-order with skip links (rtg_device.hpp)
     std::vector<float4> nodes;
     std::vector<int2> next;
     bool bigleaf = false;
     nodes.reserve(2 * d->num_nodes); next.reserve(d->num_nodes);
     std::vector<int> meshBegin(d->num_meshes), meshEnd(d->num_meshes);
-    for (int m = 0; m < d->num_meshes; ++m) {
+    for (int m = 0; m < d->num_meshes && !gpuBuild; ++m) {
         const rtg_mesh& M = d->meshes[m];
         const rtg_bvh_node* N = d->nodes + M.node_offset;
         const int base = (int)(nodes.size() / 2);
@@ -273,11 +359,17 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     nodes.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
 
     // ---- faces (already BVH-permuted)
-    std::vector<float4> tris(3 * d->num_faces), fn(d->num_faces);
     bool anyUV = false;
     for (int m = 0; m < d->num_meshes; ++m) anyUV |= d->meshes[m].has_uv != 0;
-    std::vector<float2> fuv(anyUV ? 3 * d->num_faces : 0);
-    for (int64_t f = 0; f < d->num_faces; ++f) {
+    const size_t hostFaces = gpuBuild ? 0 : (size_t)d->num_faces;
+    std::vector<float4> tris(3 * hostFaces), fn(hostFaces);
+    std::vector<float2> fuv(anyUV ? 3 * hostFaces : 0);
+    std::vector<int> facePerm;      // device build: final position -> desc face (per mesh offset)
+    if (gpuBuild) {
+        int rc = build_bvh_on_device(sc.get(), d, anyUV, anyMapped, meshBegin, meshEnd, bigleaf, facePerm);
+        if (rc) return rc;
+    }
+    for (int64_t f = 0; f < (int64_t)hostFaces; ++f) {
         const rtg_face& F = d->faces[f];
         tris[3 * f] = make_float4(F.v0.x, F.v0.y, F.v0.z, 0.f);
         tris[3 * f + 1] = make_float4(F.v0.x - F.v1.x, F.v0.y - F.v1.y, F.v0.z - F.v1.z, 0.f);
@@ -293,7 +385,6 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     // ---- objects
     std::vector<rtg::DevObject> objs(d->num_objects);
     int feat = 0;
-    bool anyMapped = false;
     for (int i = 0; i < d->num_objects; ++i) {
         const rtg_object& o = d->objects[i];
         rtg::DevObject& D = objs[i];
@@ -314,7 +405,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
         const bool uvmesh = o.kind != RTG_OBJ_SPHERE && d->meshes[o.mesh].has_uv;
         D.tex_normal = uvmesh ? o.tex_normal : -1;
         D.tex_bump = (uvmesh && o.tex_normal < 0) || o.kind == RTG_OBJ_SPHERE ? o.tex_bump : -1;
-        if (D.tex_normal >= 0 || D.tex_bump >= 0) { D.flags |= rtg::OBJF_MAPPED; anyMapped = true; }
+        if (D.tex_normal >= 0 || D.tex_bump >= 0) D.flags |= rtg::OBJF_MAPPED;
         for (int k = 0; k < 3; ++k) { D.bmin[k] = o.bbox_min[k]; D.bmax[k] = o.bbox_max[k]; }
         f4(D.mbv, o.motion_blur);
         f4(D.center, o.center, o.radius);
@@ -358,7 +449,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
         L.surface_area = M.surface_area;
         for (int k = 0; k < 12; ++k) L.xf[k] = o.transform[k];
         for (int f = 0; f < M.face_count; ++f) {
-            const rtg_face& F = d->faces[M.face_offset + f];
+            const rtg_face& F = d->faces[gpuBuild ? facePerm[M.face_offset + f] : M.face_offset + f];
             rtg::DevLightFace lf;
             std::memset(&lf, 0, sizeof(lf));
             f4(lf.v0, F.v0); f4(lf.v1, F.v1); f4(lf.v2, F.v2);
@@ -445,9 +536,12 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
         if (envs[i] < 0 || envs[i] >= d->num_images) return set_err(RTG_ERR_INVALID, "env light %d: bad image", i);
     }
 
-    HIP_TRY(sc->nodes.upload(nodes)); HIP_TRY(sc->node_ext.upload(next)); HIP_TRY(sc->tris.upload(tris));
-    HIP_TRY(sc->face_n.upload(fn)); HIP_TRY(sc->face_uv.upload(fuv));
-    if (anyMapped) {
+    if (!gpuBuild) {
+        sc->node_count = (int)(nodes.size() / 2);
+        HIP_TRY(sc->nodes.upload(nodes)); HIP_TRY(sc->node_ext.upload(next)); HIP_TRY(sc->tris.upload(tris));
+        HIP_TRY(sc->face_n.upload(fn)); HIP_TRY(sc->face_uv.upload(fuv));
+    }
+    if (anyMapped && !gpuBuild) {
         std::vector<float4> v12(2 * d->num_faces);
         for (int64_t f = 0; f < d->num_faces; ++f) {
             const rtg_face& F = d->faces[f];

@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 
 #include "rtg_device.hpp"
+#include "rtgpu.h"
 
 namespace rtg {
 
@@ -26,6 +27,14 @@ hipError_t launch_tree(TreeState*& tree, const DevScene& S, const DevCamera& C, 
 size_t tonemap_scratch_bytes(long long pixels);
 hipError_t launch_tonemap(const float* hdr, int width, int height, float key, float burn, float saturation,
                           float gamma, unsigned char* ldr, void* scratch, hipStream_t stream);
+// device scene ingest (rtg_bvh.hip): the reference's midpoint BVH of one mesh built on the
+// GPU from its faces in parse order (d_faces, device copy of the desc's), written as walk
+// records at node index nodeBase and as face arrays at faceOff (BVH order); d_perm
+// (nullable) receives the final order (mesh-local indices).  Synchronises `st`.
+hipError_t build_mesh_bvh(const rtg_face* d_faces, int n, const float root_mn[3], const float root_mx[3],
+                          int faceOff, int nodeBase, float4* d_nodes, int2* d_ext, float4* d_tris, float4* d_fn,
+                          float2* d_fuv, float4* d_v12, int* d_perm, int* nodeCount, bool* bigleaf,
+                          hipStream_t st);
 enum { WAVE_STAGES = 4, MEGA_STAGES = 1, TREE_STAGES = 2, MAX_STAGES = 4 };
 
 }  // namespace rtg

@@ -29,6 +29,7 @@ RTG_RENDER_ACCUM_ONLY = 2
 RTG_RENDER_FUSED = 4
 RTG_RENDER_TIMING = 8
 RTG_RENDER_TREE = 16
+RTG_LOAD_DEVICE_BVH = 1
 
 
 class RTGError(RuntimeError):
@@ -65,7 +66,8 @@ class Stats(ctypes.Structure):
 
 # every symbol include/rtgpu.h declares
 EXPORTED = [
-    "rtg_host_scene_load_xml", "rtg_host_scene_desc", "rtg_host_scene_free",
+    "rtg_host_scene_load_xml", "rtg_host_scene_load_xml_ex", "rtg_host_scene_desc", "rtg_host_scene_free",
+    "rtg_scene_export_bvh",
     "rtg_desc_camera_info", "rtg_desc_counts", "rtg_scene_create", "rtg_scene_destroy",
     "rtg_device_count", "rtg_render", "rtg_render_device", "rtg_resolve_accum",
     "rtg_scene_stats", "rtg_scene_reset_stats", "rtg_scene_timings", "rtg_tonemap_device", "rtg_tonemap",
@@ -95,6 +97,9 @@ def lib() -> ctypes.CDLL:
     L.rtg_last_error.restype = ctypes.c_char_p
     L.rtg_abi_version.restype = ctypes.c_int
     L.rtg_host_scene_load_xml.argtypes = [ctypes.c_char_p, P(vp)]
+    L.rtg_host_scene_load_xml_ex.argtypes = [ctypes.c_char_p, ctypes.c_uint32, P(vp)]
+    L.rtg_scene_export_bvh.argtypes = [vp, vp, ctypes.c_int64, vp, ctypes.c_int64, P(ctypes.c_int64),
+                                       P(ctypes.c_int64)]
     L.rtg_host_scene_desc.argtypes = [vp]
     L.rtg_host_scene_desc.restype = vp
     L.rtg_host_scene_free.argtypes = [vp]
@@ -134,9 +139,11 @@ class HostScene:
     """Parsed + flattened scene (rtg_host_scene).  Paths inside the XML resolve like the
     reference's: PLY relative to the current directory, images as ``inputs/<name>``."""
 
-    def __init__(self, xml_path: str):
+    def __init__(self, xml_path: str, device_bvh: bool = False):
+        """device_bvh: RTG_LOAD_DEVICE_BVH -- no host BVH build; DeviceScene builds it on the GPU."""
         h = ctypes.c_void_p()
-        _check(lib().rtg_host_scene_load_xml(os.fsencode(xml_path), ctypes.byref(h)))
+        _check(lib().rtg_host_scene_load_xml_ex(os.fsencode(xml_path), RTG_LOAD_DEVICE_BVH if device_bvh else 0,
+                                                ctypes.byref(h)))
         self._h = h
         self.desc = lib().rtg_host_scene_desc(h)
 
@@ -203,6 +210,16 @@ class DeviceScene:
         o = self.opts(camera, sample_begin, sample_count, rows, flags, seed)
         _check(lib().rtg_render_device(self._s, ctypes.byref(o), hdr_ptr or None, ldr_ptr or None,
                                        accum_ptr or None, stream or None))
+
+    def export_bvh(self):
+        """(nodes (N, 8) float32, tris (F, 12) float32): the device's walk records."""
+        nn, nf = ctypes.c_int64(), ctypes.c_int64()
+        _check(lib().rtg_scene_export_bvh(self._s, None, 0, None, 0, ctypes.byref(nn), ctypes.byref(nf)))
+        nodes = np.zeros((nn.value, 8), np.float32)
+        tris = np.zeros((nf.value, 12), np.float32)
+        _check(lib().rtg_scene_export_bvh(self._s, nodes.ctypes.data, nn.value, tris.ctypes.data, nf.value,
+                                          ctypes.byref(nn), ctypes.byref(nf)))
+        return nodes, tris
 
     def stats(self) -> dict:
         st = Stats()

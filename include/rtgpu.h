@@ -238,6 +238,12 @@ typedef struct rtg_host_scene rtg_host_scene;
  * opened relative to the current directory (parser.cpp:1404), images as
  * "inputs/<name>" (parser.cpp:107,110). */
 int rtg_host_scene_load_xml(const char* xml_path, rtg_host_scene** out);
+/* Load flags.  RTG_LOAD_DEVICE_BVH: skip the host BVH build (mesh.cpp:23-156); the
+ * description then holds faces in parse order, num_nodes == 0 and every mesh's node range
+ * empty, and rtg_scene_create builds the same BVH and face order on the GPU (SURVEY §8f,
+ * device scene ingest).  Such a description is for rtg_scene_create only. */
+enum rtg_load_flags { RTG_LOAD_DEVICE_BVH = 1 };
+int rtg_host_scene_load_xml_ex(const char* xml_path, uint32_t flags, rtg_host_scene** out);
 /* The flattened description; valid until rtg_host_scene_free. */
 const rtg_scene_desc* rtg_host_scene_desc(const rtg_host_scene* hs);
 void rtg_host_scene_free(rtg_host_scene* hs);
@@ -256,6 +262,12 @@ typedef struct rtg_scene rtg_scene;
  * scene): uploads a device-resident replica of `desc` to HIP device `device`.
  * The caller may free `desc` after return. */
 int rtg_scene_create(const rtg_scene_desc* desc, int device, rtg_scene** out);
+/* The device's traversal data, for inspection and tests: the walk's node records (8 floats
+ * per node, pre-order layout of the BVH nodes, the trailing pad node included) and the
+ * per-face triangle records (12 floats per face, BVH face order).  Either buffer may be
+ * NULL; counts are reported even when the buffers are too small (then nothing is copied). */
+int rtg_scene_export_bvh(const rtg_scene* s, float* nodes, int64_t max_nodes, float* tris, int64_t max_faces,
+                         int64_t* num_nodes, int64_t* num_faces);
 void rtg_scene_destroy(rtg_scene* scene);
 int rtg_device_count(int32_t* count);
 

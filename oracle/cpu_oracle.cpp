@@ -1131,6 +1131,7 @@ int oracle_render(const rtg_scene_desc* desc, int camera, int row_begin, int row
                   int sample_count, uint64_t seed, int threads, float* hdr, uint8_t* ldr, float* accum,
                   uint64_t* stats) {
     if (!desc || camera < 0 || camera >= desc->num_cameras) return -1;
+    if (desc->num_faces > 0 && desc->num_nodes == 0) return -2;   // RTG_LOAD_DEVICE_BVH description: no BVH
     const rtg_camera& cam = desc->cameras[camera];
     const int W = cam.width, H = cam.height;
     const int spp = cam.spp < 1 ? 1 : cam.spp;

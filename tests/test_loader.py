@@ -194,3 +194,19 @@ def test_recursion_deeper_than_the_frame_stack_is_rejected(tmp_path, monkeypatch
     with pytest.raises(rtgpu.RTGError) as e:
         rtgpu.DeviceScene(hs, 0)
     assert e.value.code == -6
+
+
+def test_device_bvh_load_flag(tmp_path, monkeypatch):
+    """RTG_LOAD_DEVICE_BVH: same faces, parse order, no nodes; the oracle refuses such a
+    description (it has no BVH to walk) and so does a GPU-less rtg_scene_create."""
+    monkeypatch.chdir(SCENES)
+    a = rtgpu.HostScene("c5_dragon.xml")
+    b = rtgpu.HostScene("c5_dragon.xml", device_bvh=True)
+    ca, cb = a.counts(), b.counts()
+    assert cb["nodes"] == 0 and ca["nodes"] > 0 and ca["faces"] == cb["faces"]
+    with pytest.raises(RuntimeError):
+        ob.render(b)
+    if rtgpu.device_count() == 0:
+        with pytest.raises(rtgpu.RTGError) as e:
+            rtgpu.DeviceScene(b, 0)
+        assert e.value.code == -4
