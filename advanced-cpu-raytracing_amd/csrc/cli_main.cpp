@@ -1,7 +1,9 @@
 // rtgpu -- drop-in for the reference CLI `raytracer <scene.xml>` (src/main.cpp:132-202).
 // Same argv and outputs: for every camera, <ImageName stem>.png (LDR clamp) and, for a
 // tonemapped camera, the raw float image via rtg_write_hdr.  The 8-thread row-band
-// block (main.cpp:164-185) is replaced by one rtg_render call per camera.
+// block (main.cpp:164-185) is replaced by one rtg_render call per camera.  The BVH is built
+// on the GPU (RTG_LOAD_DEVICE_BVH; bit-identical to the reference's build); --host-bvh builds
+// it on the CPU instead.
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -18,15 +20,18 @@ static int die(const char* what) {
 
 int main(int argc, char** argv) {
     if (argc < 2) {
-        std::fprintf(stderr, "usage: %s <scene.xml> [--device N]\n", argv[0]);
+        std::fprintf(stderr, "usage: %s <scene.xml> [--device N] [--host-bvh]\n", argv[0]);
         return 2;
     }
     int device = 0;
-    for (int i = 2; i + 1 < argc; ++i)
-        if (!std::strcmp(argv[i], "--device")) device = std::atoi(argv[i + 1]);
+    uint32_t flags = RTG_LOAD_DEVICE_BVH;
+    for (int i = 2; i < argc; ++i) {
+        if (!std::strcmp(argv[i], "--device") && i + 1 < argc) device = std::atoi(argv[i + 1]);
+        if (!std::strcmp(argv[i], "--host-bvh")) flags = 0;
+    }
 
     rtg_host_scene* hs = nullptr;
-    if (rtg_host_scene_load_xml(argv[1], &hs)) return die("loading scene");
+    if (rtg_host_scene_load_xml_ex(argv[1], flags, &hs)) return die("loading scene");
     const rtg_scene_desc* desc = rtg_host_scene_desc(hs);
     auto start = std::chrono::steady_clock::now();
     rtg_scene* scene = nullptr;

@@ -78,3 +78,26 @@ def test_device_bvh_full_size(tmp_path, K):
           f"{t4 - t3:.3f}s")
     nn, nf = _same_bvh(ds_h, ds_d)
     assert nf >= K * 0.99
+
+
+@pytest.mark.parametrize("extra", [[], ["--host-bvh"]])
+def test_cli_drop_in(tmp_path, extra):
+    """The drop-in CLI (`rtgpu scene.xml`, main.cpp:132-202): same PNG as the library render,
+    with the BVH built on the GPU (default) or on the host."""
+    import re
+    import shutil
+    import subprocess
+    from PIL import Image
+    exe = os.path.join(os.path.dirname(rtgpu.LIB_PATH), "rtgpu")
+    src = open(os.path.join(SCENES, "cornell_dielectric.xml")).read()
+    m = re.search(r"<ImageName>([^<]*)</ImageName>", src)
+    (tmp_path / "s.xml").write_text(src)
+    r = subprocess.run([exe, "s.xml"] + extra, cwd=tmp_path, capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    assert "Rendering took" in r.stdout
+    png = tmp_path / (os.path.splitext(m.group(1))[0] + ".png")
+    got = np.asarray(Image.open(png).convert("RGB"))
+    hs = rtgpu.HostScene(str(tmp_path / "s.xml"))
+    _, ldr = rtgpu.DeviceScene(hs, 0).render(0)
+    assert np.array_equal(got, ldr)
+    shutil.rmtree(tmp_path, ignore_errors=True)
