@@ -460,6 +460,9 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
     h.t = minT;
     h.obj = -1;
     h.face = -1;
+    // instance world-bbox tests: the division-free slab test (same decisions, box_hit_fast);
+    // the motion-blur quirk moves r.o between objects, never r.d
+    const RayRcp rq = (FEAT & FEAT_INSTANCE) ? ray_rcp(r) : RayRcp{};
     for (int k = 0; k < S.num_objects; ++k) {
         const DevObject& ob = S.objects[k];
         c.obj();
@@ -478,7 +481,7 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
             // InstancedMesh::Intersect (instancedMesh.cpp:16-66): world bbox first
             Ray wr = r;
             if (ob.flags & OBJF_MOTION_BLUR) wr.o = add(wr.o, muls(ld3(ob.mbv), mbTime));
-            if (!box_hit(ob.bmin[0], ob.bmin[1], ob.bmin[2], ob.bmax[0], ob.bmax[1], ob.bmax[2], wr, h.t)) {
+            if (!box_hit_fast(ob.bmin[0], ob.bmin[1], ob.bmin[2], ob.bmax[0], ob.bmax[1], ob.bmax[2], wr, rq, h.t)) {
                 r.o = wr.o;
                 continue;
             }
