@@ -4,6 +4,8 @@
 // (raytracer.cpp:135-191) unrolled onto an explicit per-thread stack.  Used for path
 // tracing, motion blur and small ray-tree frames; other scenes take the wavefront
 // pipelines (rtg_wave.hip, rtg_tree.hip).
+#include <type_traits>
+
 #include "rtg_common.hpp"
 #include "rtg_kernels.hpp"
 
@@ -30,13 +32,18 @@ struct Frame {
     float selfT, selfMedium;
     int matIdx, depth;
     uint64_t key;
-    f3 tp;             // path tracing: the node's ray.throughput (children inherit it)
-    // FK_GI (path tracing): the shading point, waiting for its global-illumination child
+};
+// Path-tracing frames carry more state; the Whitted kernels keep the small frame (their
+// per-thread stacks live in scratch: 8 frames of ~120 B vs ~200 B).
+struct FramePT : Frame {
+    f3 tp;             // the node's ray.throughput (children inherit it)
+    // FK_GI: the shading point, waiting for its global-illumination child
     Surf s;
     f3 w_o, giDir;
     float mbTime;
     int obj, skip;     // skip: id of the light mesh the GI ray hit (raytracer.cpp:173-175)
 };
+template <bool PT> using FrameT = typename std::conditional<PT, FramePT, Frame>::type;
 
 struct Node {          // a ray that hit something, about to be shaded
     Ray r;
@@ -61,7 +68,7 @@ struct Child {
 // spawns a child; otherwise `out` is the node's final colour.
 template <bool STATS, bool PT>
 DEV bool shade_rest(const DevScene& S, const DevCamera& C, const ShadeCtx& c, f3 w_o, float medium, int depth,
-                    uint64_t key, float t, float mbTime, f3 tp, f3 color, int skip, f3& out, Frame& f, Child& ch,
+                    uint64_t key, float t, float mbTime, f3 tp, f3 color, int skip, f3& out, FrameT<PT>& f, Child& ch,
                     Cnt<STATS>& cn) {
     const DevMaterial& mat = *c.mat;
     const float refractiveIndexOfVacuum = 1.00001;
@@ -148,7 +155,7 @@ DEV bool shade_rest(const DevScene& S, const DevCamera& C, const ShadeCtx& c, f3
     f.key = key;
     f.selfT = t;
     f.selfMedium = medium;
-    f.tp = tp;
+    if constexpr (PT) f.tp = tp;
     ch.tp = tp;
     ch.slot = 0;
     return true;
@@ -165,7 +172,7 @@ DEV int emissive_hit_id(const DevScene& S, const Hit& h, bool hit) {
 // the node spawns a child ray (path tracing: its GI ray first); otherwise `out` is the
 // node's final colour.  `level`: frames on the stack (the node's depth in the ray tree).
 template <int MAXD, bool STATS, bool PT>
-DEV bool shade_node(const DevScene& S, const DevCamera& C, const Node& cur, int level, f3& out, Frame& f, Child& ch,
+DEV bool shade_node(const DevScene& S, const DevCamera& C, const Node& cur, int level, f3& out, FrameT<PT>& f, Child& ch,
                     Cnt<STATS>& cn) {
     const DevObject& ob = S.objects[cur.h.obj];
     ShadeCtx c;
@@ -183,7 +190,7 @@ DEV bool shade_node(const DevScene& S, const DevCamera& C, const Node& cur, int 
         return false;
     }
     f3 tp = cur.tp;
-    if (PT) {
+    if constexpr (PT) {
         // ComputeGlobalIllumination (raytracer.cpp:135-191) up to its IntersectObjects
         bool gi = true;
         if (C.russian_roulette) {
@@ -255,7 +262,7 @@ DEV f3 render_sample(const DevScene& S, const DevCamera& C, int px, int py, uint
     f3 rTp = mk(1.0f, 1.0f, 1.0f);
     int pend = 0;
 
-    Frame stack[MAXD > 0 ? MAXD : 1];
+    FrameT<PT> stack[MAXD > 0 ? MAXD : 1];
     int sp = 0;
     f3 value;
     bool vHit;
@@ -264,7 +271,9 @@ DEV f3 render_sample(const DevScene& S, const DevCamera& C, int px, int py, uint
         Node cur;
         const bool hit = trace<false, STATS>(S, R, mbTime, INFINITY, INFINITY, cur.h, cn);
         if (pend == 0 && !hit) return miss_color(S, C, px, py, R.d);
-        if (PT && pend == 3) stack[sp - 1].skip = emissive_hit_id(S, cur.h, hit);
+        if constexpr (PT) {
+            if (pend == 3) stack[sp - 1].skip = emissive_hit_id(S, cur.h, hit);
+        }
         if (hit) {
             cur.r = R;
             cur.eye = pend == 0 ? cpos : R.o;
@@ -277,7 +286,7 @@ DEV f3 render_sample(const DevScene& S, const DevCamera& C, int px, int py, uint
             Child ch;
             const bool spawn = shade_node<MAXD, STATS, PT>(S, C, cur, sp, value, stack[MAXD > 0 ? sp : 0], ch, cn);
             if (MAXD > 0 && spawn) {
-                const Frame& f = stack[sp];
+                const FrameT<PT>& f = stack[sp];
                 ++sp;
                 cn.sec();
                 R = ch.r;
@@ -295,7 +304,7 @@ DEV f3 render_sample(const DevScene& S, const DevCamera& C, int px, int py, uint
             // a child missed (ComputeMirrorReflection :461-470, dielectric :351-356, :408 --
             // the refracted miss looks the environment up in the reflected direction; a GI
             // ray that misses contributes nothing, :169-189)
-            const Frame& f = stack[MAXD > 0 ? sp - 1 : 0];
+            const FrameT<PT>& f = stack[MAXD > 0 ? sp - 1 : 0];
             if (f.kind == FK_MIRROR || f.kind == FK_DIEL) value = env_or_zero(S, f.kind == FK_MIRROR ? R.d : f.reflDir);
             else value = mk(0, 0, 0);
             vHit = false;
@@ -303,8 +312,9 @@ DEV f3 render_sample(const DevScene& S, const DevCamera& C, int px, int py, uint
         // ---- propagate finished values up the stack
         bool descended = false;
         while (MAXD > 0 && sp > 0) {
-            Frame& f = stack[sp - 1];
-            if (PT && f.kind == FK_GI) {
+            FrameT<PT>& f = stack[sp - 1];
+            if constexpr (PT) {
+              if (f.kind == FK_GI) {
                 // the GI ray's radiance: Shade(...) * 2 * pi (raytracer.cpp:177-188), then the
                 // rest of PerformShading with colour = 0 + GI
                 ShadeCtx c;
@@ -337,6 +347,7 @@ DEV f3 render_sample(const DevScene& S, const DevCamera& C, int px, int py, uint
                 vMedium = selfMedium;
                 --sp;
                 continue;
+              }
             }
             const DevMaterial& pm = S.materials[f.matIdx];
             if (f.kind == FK_DIEL && f.stage == 0) {
@@ -358,7 +369,7 @@ DEV f3 render_sample(const DevScene& S, const DevCamera& C, int px, int py, uint
                 rMedium = f.rMedium;
                 rDepth = f.depth - 1;
                 rKey = child_key(f.key, 1);
-                rTp = f.tp;
+                if constexpr (PT) rTp = f.tp;
                 pend = 2;
                 cn.sec();
                 descended = true;
