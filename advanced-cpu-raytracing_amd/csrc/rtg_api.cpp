@@ -93,6 +93,7 @@ struct rtg_scene {
     DevBuf<rtg::DevMeshLight> mesh_lights;
     DevBuf<rtg::DevLightFace> light_faces;
     DevBuf<rtg::DevObject> objects;
+    DevBuf<float4> group_box;
     DevBuf<rtg::DevMaterial> materials;
     DevBuf<rtg::DevBrdf> brdfs;
     DevBuf<rtg::DevTexture> textures;
@@ -422,6 +423,33 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
         else if (o.kind == RTG_OBJ_INSTANCE) feat |= rtg::FEAT_INSTANCE;
         else if (!ident || (o.flags & RTG_OBJF_MOTION_BLUR)) feat |= rtg::FEAT_XFORM;
     }
+    // instance groups: runs of consecutive instances without motion blur, chunked by ~sqrt of
+    // the run length, with the exact (min/max) union of the members' world boxes
+    std::vector<float4> gbox(2 * (size_t)d->num_objects, make_float4(0.f, 0.f, 0.f, 0.f));
+    for (int k = 0; k < d->num_objects;) {
+        auto eligible = [&](int i) {
+            return objs[i].kind == rtg::OBJ_INSTANCE && !(objs[i].flags & rtg::OBJF_MOTION_BLUR);
+        };
+        if (!eligible(k)) { ++k; continue; }
+        int e = k;
+        while (e < d->num_objects && eligible(e)) ++e;
+        const int run = e - k;
+        const int gsz = std::max(4, (int)std::lround(std::sqrt((double)run)));
+        for (int g = k; g < e; g += gsz) {
+            const int ge = std::min(e, g + gsz);
+            if (ge - g < 2) continue;
+            float mn[3] = {INFINITY, INFINITY, INFINITY}, mx[3] = {-INFINITY, -INFINITY, -INFINITY};
+            for (int i = g; i < ge; ++i)
+                for (int c = 0; c < 3; ++c) {
+                    mn[c] = std::min(mn[c], objs[i].bmin[c]);
+                    mx[c] = std::max(mx[c], objs[i].bmax[c]);
+                }
+            objs[g].group_end = ge;
+            gbox[2 * g] = make_float4(mn[0], mn[1], mn[2], 0.f);
+            gbox[2 * g + 1] = make_float4(mx[0], mx[1], mx[2], 0.f);
+        }
+        k = e;
+    }
     // wavefront eligibility: no ray-tree children and no motion blur
     bool branching = false, blur = false;
     for (int i = 0; i < d->num_materials; ++i) {
@@ -550,7 +578,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
         }
         HIP_TRY(sc->face_v12.upload(v12));
     }
-    HIP_TRY(sc->objects.upload(objs)); HIP_TRY(sc->materials.upload(mats)); HIP_TRY(sc->brdfs.upload(brdfs));
+    HIP_TRY(sc->objects.upload(objs)); HIP_TRY(sc->group_box.upload(gbox)); HIP_TRY(sc->materials.upload(mats)); HIP_TRY(sc->brdfs.upload(brdfs));
     HIP_TRY(sc->textures.upload(texs)); HIP_TRY(sc->images.upload(imgs)); HIP_TRY(sc->texels.upload(pool));
     HIP_TRY(sc->point_lights.upload(pls)); HIP_TRY(sc->area_lights.upload(als)); HIP_TRY(sc->dir_lights.upload(dls));
     HIP_TRY(sc->spot_lights.upload(sls)); HIP_TRY(sc->env_images.upload(envs));
@@ -573,7 +601,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     S.mesh_lights = sc->mesh_lights.p;
     S.light_faces = sc->light_faces.p;
     S.num_mesh = d->num_mesh_lights;
-    S.objects = sc->objects.p; S.materials = sc->materials.p; S.brdfs = sc->brdfs.p;
+    S.objects = sc->objects.p; S.group_box = sc->group_box.p; S.materials = sc->materials.p; S.brdfs = sc->brdfs.p;
     S.textures = sc->textures.p; S.images = sc->images.p; S.texels = sc->texels.p;
     S.point_lights = sc->point_lights.p; S.area_lights = sc->area_lights.p; S.dir_lights = sc->dir_lights.p;
     S.spot_lights = sc->spot_lights.p; S.env_images = sc->env_images.p;

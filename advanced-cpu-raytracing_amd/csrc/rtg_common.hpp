@@ -465,6 +465,17 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
     const RayRcp rq = (FEAT & FEAT_INSTANCE) ? ray_rcp(r) : RayRcp{};
     for (int k = 0; k < S.num_objects; ++k) {
         const DevObject& ob = S.objects[k];
+        // Instance groups (runs of consecutive instances without motion blur): every member's
+        // world box lies inside the group's, and the slab test is monotone in the box and in
+        // minT, so a group box that fails at the current minT fails for every member tested
+        // after it -- the members can be skipped with the same result.
+        if ((FEAT & FEAT_INSTANCE) && ob.group_end > k) {
+            const float4 ga = S.group_box[2 * k], gb = S.group_box[2 * k + 1];
+            if (!box_hit_fast(ga.x, ga.y, ga.z, gb.x, gb.y, gb.z, r, rq, h.t)) {
+                k = ob.group_end - 1;
+                continue;
+            }
+        }
         c.obj();
         if ((FEAT & FEAT_SPHERE) && ob.kind == OBJ_SPHERE) {
             c.sph();

@@ -38,7 +38,9 @@ struct DevObject {
     double inv[12];                 // rows 0..2 of inverseTransform
     double invT[12];                // rows 0..2 of inverseTransposeTransform
     double baseInvT[12];            // base mesh's inverseTransposeTransform
-    int id, pad2, pad3, pad4;       // Shape::id (XML id; spheres: never a light's id)
+    int id;                         // Shape::id (XML id; spheres: never a light's id)
+    int group_end;                  // first object of an instance group: one past its last member
+    int pad3, pad4;
 };
 
 struct DevMaterial {
@@ -101,6 +103,7 @@ struct DevScene {
     const float2* __restrict__ face_uv;
     const float4* __restrict__ face_v12;   // raw v1, v2 per face (scenes with normal / bump maps only)
     const DevObject* __restrict__ objects;
+    const float4* __restrict__ group_box;  // per object (group starts only): union of the members' world boxes
     const DevMaterial* __restrict__ materials;
     const DevBrdf* __restrict__ brdfs;
     const DevTexture* __restrict__ textures;
