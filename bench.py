@@ -174,10 +174,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # RTG_BENCH_BACKEND=gloo: rehearse the multi-rank flow on a box with fewer GPUs than ranks
+    # (ranks share devices round-robin); the driver's runs use RCCL, one GPU per rank
+    backend = os.environ.get("RTG_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     if world > 1:
         import torch.distributed as dist
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     else:
         torch.cuda.set_device(local)
     barrier = (lambda: dist.barrier()) if dist else (lambda: None)
@@ -208,10 +216,11 @@ def main():
         elapsed, kern_ms = measure(ds, torch, hdr, ldr, args.steps, args.warmup, seed, barrier)
         log(f"timed: {elapsed / args.steps * 1e3:.3f} ms/step")
         if dist:
-            t = torch.tensor([elapsed], dtype=torch.float64, device=f"cuda:{local}")
+            rdev = f"cuda:{local}" if backend == "nccl" else "cpu"
+            t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             elapsed = float(t.item())
-            k = torch.tensor([kern_ms], dtype=torch.float64, device=f"cuda:{local}")
+            k = torch.tensor([kern_ms], dtype=torch.float64, device=rdev)
             dist.all_reduce(k, op=dist.ReduceOp.MAX)
             kern_ms = float(k.item())
 
