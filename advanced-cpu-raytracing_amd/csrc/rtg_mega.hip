@@ -397,7 +397,7 @@ DEV f3 render_sample(const DevScene& S, const DevCamera& C, int px, int py, uint
 }
 
 template <int MAXD, bool STATS, bool PT>
-__global__ __launch_bounds__(256) void k_render(DevScene S, DevCamera C, RenderParams P, float* __restrict__ hdr,
+__global__ __launch_bounds__(256, RTG_MEGA_WAVES) void k_render(DevScene S, DevCamera C, RenderParams P, float* __restrict__ hdr,
                                                 unsigned char* __restrict__ ldrOut, float* __restrict__ accum,
                                                 DevCounters* __restrict__ counters) {
     int px, py;

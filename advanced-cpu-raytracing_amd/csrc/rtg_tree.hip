@@ -46,8 +46,10 @@ __global__ __launch_bounds__(256) void k_tree_gen(const DevCamera C, const Rende
     L0.key[i] = key;
 }
 
+// eight waves (64 VGPRs) for scenes without instances / transforms: +8% on C5; the instance
+// variants need twice the registers and keep their natural allocation
 template <bool STATS, int FEAT>
-__global__ __launch_bounds__(256) void k_tree_trace(const DevScene S, const TreeLevel L, const int level,
+__global__ __launch_bounds__(256, (FEAT & (FEAT_INSTANCE | FEAT_XFORM)) ? 1 : RTG_TREE_TRACE_WAVES) void k_tree_trace(const DevScene S, const TreeLevel L, const int level,
                                                     DevCounters* counters) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     Cnt<STATS> cn;
@@ -80,7 +82,7 @@ DEV int seg_append(bool want, int* lds_count) {
 }
 
 template <bool STATS>
-__global__ __launch_bounds__(256) void k_tree_shade(const DevScene S, const DevCamera C, const TreeLevel L,
+__global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_tree_shade(const DevScene S, const DevCamera C, const TreeLevel L,
                                                     const int level, const int pixel_base, const TreeSegs G,
                                                     DevCounters* counters) {
     __shared__ int nShadow, nChild;

@@ -23,7 +23,7 @@ namespace rtg {
 enum { BASE_FINAL = 1, BASE_ADD_ZERO = 2 };
 
 template <bool STATS, int FEAT>
-__global__ __launch_bounds__(256) void k_primary(const DevScene S, const DevCamera C, const RenderParams P,
+__global__ __launch_bounds__(256, RTG_PRIMARY_WAVES) void k_primary(const DevScene S, const DevCamera C, const RenderParams P,
                                                  const int sample, const WaveBufs W, DevCounters* counters) {
     int px, py;
     tile_pixel(P, px, py);
@@ -59,7 +59,7 @@ DEV int queue_append(bool want, int* lds_count) {
 }
 
 template <bool STATS>
-__global__ __launch_bounds__(256) void k_shade(const DevScene S, const DevCamera C, const RenderParams P,
+__global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_shade(const DevScene S, const DevCamera C, const RenderParams P,
                                                const int sample, const WaveBufs W, DevCounters* counters) {
     __shared__ int seg_count;
     if (threadIdx.x == 0) seg_count = 0;
