@@ -15,23 +15,20 @@
 // Minimum waves per SIMD the kernels are compiled for (__launch_bounds__'s second argument:
 // the register budget is 512 / waves).  The fused kernel at its natural 256 VGPR + AGPRs runs
 // one wave per SIMD; two (a few hundred spilled registers) measured 5% faster on C2 and
-// 40-60% faster on path tracing, four slower.  k_tree_trace at eight: +8% on C5; k_primary
-// and k_shadow at eight: 20-30% slower on C3.
+// 40-60% faster on path tracing, four slower.  The traversal kernels of plain scenes (meshes
+// with small leaves, spheres: 57-84 VGPRs) run at eight (+8% on C5); the large-leaf, instance
+// and transform variants (88-129 VGPRs) keep their natural allocation -- eight costs C3 20-30%
+// (DESIGN.md §5).
 #ifndef RTG_MEGA_WAVES
 #define RTG_MEGA_WAVES 2
 #endif
-#ifndef RTG_PRIMARY_WAVES
-#define RTG_PRIMARY_WAVES 1
-#endif
-#ifndef RTG_SHADOW_WAVES
-#define RTG_SHADOW_WAVES 1
-#endif
-#ifndef RTG_TREE_TRACE_WAVES
-#define RTG_TREE_TRACE_WAVES 8
+#ifndef RTG_LEAN_WAVES
+#define RTG_LEAN_WAVES 8
 #endif
 #ifndef RTG_SHADE_WAVES
 #define RTG_SHADE_WAVES 1
 #endif
+#define RTG_TRACE_WAVES(FEAT) (((FEAT) & ~FEAT_SPHERE) ? 1 : RTG_LEAN_WAVES)
 
 namespace rtg {
 
@@ -1183,7 +1180,7 @@ DEV void flush_counters(Cnt<STATS>& cn, DevCounters* counters) {
 // one thread per queued shadow ray, CastShadowRay as early-exit any-hit (raytracer.cpp:585-623).
 template <bool STATS, int FEAT>
 // grid (shade blocks, slots): block (b, c) takes entries [256c, 256c+256) of segment b
-__global__ __launch_bounds__(256, RTG_SHADOW_WAVES) void k_shadow(const DevScene S, const WaveBufs W, DevCounters* counters) {
+__global__ __launch_bounds__(256, RTG_TRACE_WAVES(FEAT)) void k_shadow(const DevScene S, const WaveBufs W, DevCounters* counters) {
     const int k = blockIdx.y * 256 + threadIdx.x;
     const size_t q = ((size_t)blockIdx.x * W.num_slots) * 256 + k;
     Cnt<STATS> cn;

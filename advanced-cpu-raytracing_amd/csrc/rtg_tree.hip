@@ -46,10 +46,8 @@ __global__ __launch_bounds__(256) void k_tree_gen(const DevCamera C, const Rende
     L0.key[i] = key;
 }
 
-// eight waves (64 VGPRs) for scenes without instances / transforms: +8% on C5; the instance
-// variants need twice the registers and keep their natural allocation
 template <bool STATS, int FEAT>
-__global__ __launch_bounds__(256, (FEAT & (FEAT_INSTANCE | FEAT_XFORM)) ? 1 : RTG_TREE_TRACE_WAVES) void k_tree_trace(const DevScene S, const TreeLevel L, const int level,
+__global__ __launch_bounds__(256, RTG_TRACE_WAVES(FEAT)) void k_tree_trace(const DevScene S, const TreeLevel L, const int level,
                                                     DevCounters* counters) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     Cnt<STATS> cn;

@@ -23,7 +23,7 @@ namespace rtg {
 enum { BASE_FINAL = 1, BASE_ADD_ZERO = 2 };
 
 template <bool STATS, int FEAT>
-__global__ __launch_bounds__(256, RTG_PRIMARY_WAVES) void k_primary(const DevScene S, const DevCamera C, const RenderParams P,
+__global__ __launch_bounds__(256, RTG_TRACE_WAVES(FEAT)) void k_primary(const DevScene S, const DevCamera C, const RenderParams P,
                                                  const int sample, const WaveBufs W, DevCounters* counters) {
     int px, py;
     tile_pixel(P, px, py);
