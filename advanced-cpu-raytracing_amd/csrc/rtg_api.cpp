@@ -458,6 +458,12 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     }
     for (int i = 0; i < d->num_objects; ++i) blur |= (d->objects[i].flags & RTG_OBJF_MOTION_BLUR) != 0;
     sc->feat = feat | (bigleaf ? rtg::FEAT_BIGLEAF : 0);
+    // RTG_FEAT_FORCE=<bits> ORs traversal feature bits in (experiments: a superset of the
+    // scene's features selects a more general kernel with the same results)
+    if (const char* e = std::getenv("RTG_FEAT_FORCE")) sc->feat |= std::atoi(e) & rtg::FEAT_ALL;
+    // RTG_NO_COOP=1: large leaves tested by their own lane (the sequential walk handles any
+    // leaf size; the cooperative one is only faster)
+    if (std::getenv("RTG_NO_COOP")) sc->feat &= ~rtg::FEAT_BIGLEAF;
     sc->tree_ok = !blur && d->max_recursion_depth > 0 && branching;
     sc->wave_ok = !blur && (d->max_recursion_depth <= 0 || !branching);
     sc->num_slots = d->num_point_lights + d->num_area_lights + d->num_env_lights + d->num_dir_lights +
