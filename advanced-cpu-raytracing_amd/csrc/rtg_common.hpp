@@ -28,7 +28,11 @@
 #ifndef RTG_SHADE_WAVES
 #define RTG_SHADE_WAVES 1
 #endif
-#define RTG_TRACE_WAVES(FEAT) (((FEAT) & ~FEAT_SPHERE) ? 1 : RTG_LEAN_WAVES)
+#ifndef RTG_BIGLEAF_LEAN
+#define RTG_BIGLEAF_LEAN 0
+#endif
+#define RTG_TRACE_WAVES(FEAT) \
+    (((FEAT) & ~(FEAT_SPHERE | (RTG_BIGLEAF_LEAN ? FEAT_BIGLEAF : 0))) ? 1 : RTG_LEAN_WAVES)
 
 namespace rtg {
 
@@ -322,6 +326,71 @@ DEV bool walk_bvh_seq(const DevScene& S, int i, const int end, const Ray& r, flo
     return hit;
 }
 
+// One step's large leaves, tested by the whole wave at once.  Every lane that reached a
+// large leaf in this step (`coop`) posts an event -- its ray, minT and leaf -- to the wave's
+// table in LDS; the (event, face) pairs of all events are dealt over the wave's lanes, and
+// each candidate hit lowers its event's (t, face) key with an LDS 64-bit atomic min.  The
+// result per event is the minimum over the leaf's faces with t < minT -- what the lane's
+// own sequential loop would keep -- with no per-event reduction chain, and the faces'
+// loads independent of each other.  Returns the calling lane's key (~0: none).
+// Block size 256 (four waves, one table each), the size of every traversal kernel.
+struct CoopEvent {
+    float ox, oy, oz, dx, dy, dz, minT;
+    int first, cnt, start;
+    unsigned long long best;
+};
+DEV void wave_lds_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+DEV uint64_t coop_leaf_tests(const DevScene& S, uint64_t coop, const Ray& r, float minT, int first, int cnt) {
+    __shared__ CoopEvent table[4][64];
+    CoopEvent* E = table[threadIdx.x >> 6];
+    const uint64_t em = __ballot(1);
+    const int lane = threadIdx.x & 63;
+    const int nact = __popcll(em);
+    const int rank = __popcll(em & ((1ull << lane) - 1ull));
+    const int ne = __popcll(coop);
+    const int slot = cnt > 0 ? __popcll(coop & ((1ull << lane) - 1ull)) : -1;
+    if (slot >= 0) {
+        CoopEvent& e = E[slot];
+        e.ox = r.o.x; e.oy = r.o.y; e.oz = r.o.z;
+        e.dx = r.d.x; e.dy = r.d.y; e.dz = r.d.z;
+        e.minT = minT;
+        e.first = first;
+        e.cnt = cnt;
+        e.best = ~0ull;
+    }
+    wave_lds_sync();
+    int total = 0, start = 0;
+    for (int k = 0; k < ne; ++k) {
+        if (k == slot) start = total;
+        total += E[k].cnt;
+    }
+    if (slot >= 0) E[slot].start = start;
+    wave_lds_sync();
+    for (int w = rank; w < total; w += nact) {
+        int lo = 0, hi = ne - 1;                        // last event with start <= w
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) >> 1;
+            if (E[mid].start <= w) lo = mid;
+            else hi = mid - 1;
+        }
+        const CoopEvent& e = E[lo];
+        Ray lr;
+        lr.o = mk(e.ox, e.oy, e.oz);
+        lr.d = mk(e.dx, e.dy, e.dz);
+        const int f = e.first + (w - e.start);
+        float t;
+        if (tri_test_fast(S, f, lr, e.minT, t)) atomicMin(&E[lo].best, (unsigned long long)hit_key(t, f));
+    }
+    wave_lds_sync();
+    const uint64_t mine = slot >= 0 ? (uint64_t)E[slot].best : ~0ull;
+    wave_lds_sync();                                    // the table is rewritten next step
+    return mine;
+}
+
 // BVH::IntersectBVH (bvh.cpp:5-30) as a stackless pre-order walk (rtg_device.hpp).
 // ANY: stop at the first accepted face with t < limit (CastShadowRay semantics).
 //
@@ -384,37 +453,16 @@ DEV bool walk_bvh(const DevScene& S, int i, const int end, const Ray& r, float& 
             }
             if (i >= end) active = false;
         }
-        uint64_t coop = __ballot(coopCnt > 0);
+        const uint64_t coop = __ballot(coopCnt > 0);
         if (coop) {
-            const uint64_t em = __ballot(1);
-            const int lane = threadIdx.x & 63;
-            const int nact = __popcll(em);
-            const int rank = __popcll(em & ((1ull << lane) - 1ull));
-            while (coop) {
-                const int L = __ffsll((long long)coop) - 1;
-                coop &= coop - 1;
-                Ray lr;
-                lr.o = mk(__shfl(r.o.x, L), __shfl(r.o.y, L), __shfl(r.o.z, L));
-                lr.d = mk(__shfl(r.d.x, L), __shfl(r.d.y, L), __shfl(r.d.z, L));
-                const float mt = __shfl(minT, L);
-                const int lf = __shfl(coopFirst, L), lc = __shfl(coopCnt, L);
-                uint64_t best = ~0ull;
-                for (int k = rank; k < lc; k += nact) {
-                    float t;
-                    if (tri_test_fast(S, lf + k, lr, mt, t)) {
-                        const uint64_t key = hit_key(t, lf + k);
-                        if (key < best) best = key;
-                    }
-                }
-                best = wave_min_key(best, em);
-                if (lane == L) {
-                    c.template tri_n<ANY>((uint32_t)lc);
-                    if (best != ~0ull) {
-                        minT = __uint_as_float((uint32_t)(best >> 32));
-                        hitFace = (int)(uint32_t)best;
-                        hit = true;
-                        if (ANY && minT < limit) active = false;
-                    }
+            const uint64_t best = coop_leaf_tests(S, coop, r, minT, coopFirst, coopCnt);
+            if (coopCnt > 0) {
+                c.template tri_n<ANY>((uint32_t)coopCnt);
+                if (best != ~0ull) {
+                    minT = __uint_as_float((uint32_t)(best >> 32));
+                    hitFace = (int)(uint32_t)best;
+                    hit = true;
+                    if (ANY && minT < limit) active = false;
                 }
             }
         }

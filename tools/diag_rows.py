@@ -1,4 +1,5 @@
-"""k_primary time for row bands of C3 (is the per-wave cost or the tail the problem?)."""
+"""Where a configuration's traversal time goes: k_primary / k_shadow time and traversal
+counts per 32-row band of one sample pass.  python tools/diag_rows.py [config]"""
 import os
 import sys
 import tempfile
@@ -10,16 +11,26 @@ import torch  # noqa: E402,F401
 import rtgpu  # noqa: E402
 import scenes  # noqa: E402
 
+cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
 d = tempfile.mkdtemp()
 os.chdir(d)
-xml = scenes.config_c3(d, spp=1)
+xml = getattr(scenes, "config_" + cfg)(d, spp=1)
 hs = rtgpu.HostScene(xml)
 ds = rtgpu.DeviceScene(hs, 0)
-for rows in ((0, 1080), (112, 176), (112, 128), (128, 144), (400, 464), (0, 112), (176, 1080)):
+H = hs.camera(0)["height"]
+rows = []
+for r0 in range(0, H, 32):
+    band = (r0, min(H, r0 + 32))
     for _ in range(2):
-        ds.render(0, rows=rows, flags=rtgpu.RTG_RENDER_TIMING)
+        ds.render(0, rows=band, flags=rtgpu.RTG_RENDER_TIMING)
         t = ds.timings()
     ds.reset_stats()
-    ds.render(0, rows=rows, flags=rtgpu.RTG_RENDER_COUNT_STATS)
+    ds.render(0, rows=band, flags=rtgpu.RTG_RENDER_COUNT_STATS)
     st = ds.stats()
-    print(rows, {k: round(v, 3) for k, v in t.items()}, st["node_visits"], st["tri_tests"], flush=True)
+    rows.append((band, t.get("k_primary", 0), t.get("k_shadow", 0), st["node_visits"], st["tri_tests"],
+                 st["shadow_node_visits"], st["shadow_tri_tests"]))
+tot = sum(r[1] + r[2] for r in rows)
+print(f"{cfg}: sum of band times {tot:.3f} ms")
+for r in rows:
+    print(f"rows {r[0][0]:4d}-{r[0][1]:4d}  prim {r[1]:.3f} shadow {r[2]:.3f} ms  visits {r[3]:9d} tris {r[4]:8d}  "
+          f"svisits {r[5]:9d} stris {r[6]:8d}", flush=True)

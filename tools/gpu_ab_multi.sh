@@ -19,7 +19,7 @@ done
 for l in "$@"; do
   [ $l = base ] && continue
   export RTGPU_LIB=$PWD/advanced-cpu-raytracing_amd/$l
-  timeout -k 10 600 python -m pytest tests/test_gpu_parity.py tests/test_gpu_pathtrace.py -q -x > $out/pytest_$l.log 2>&1
+  timeout -k 10 600 python -m pytest tests/test_gpu_parity.py tests/test_gpu_pathtrace.py tests/test_gpu_configs.py -q -x > $out/pytest_$l.log 2>&1
   rc=$?; echo "pytest $l rc=$rc" >> $out/status.txt
   [ $rc -ne 0 ] && exit $rc
 done
