@@ -619,6 +619,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     S.eps = d->shadow_epsilon;
     S.ambient[0] = d->ambient_light.x; S.ambient[1] = d->ambient_light.y; S.ambient[2] = d->ambient_light.z;
     for (int k = 0; k < 3; ++k) S.background[k] = d->background[k];
+    S.coop = (sc->feat & rtg::FEAT_BIGLEAF) ? 1 : 0;
     HIP_TRY(hipDeviceSynchronize());
     *out = sc.release();
     return RTG_OK;

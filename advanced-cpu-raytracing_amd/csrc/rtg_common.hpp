@@ -407,6 +407,9 @@ template <bool ANY, bool STATS, bool COOP>
 DEV bool walk_bvh(const DevScene& S, int i, const int end, const Ray& r, float& minT, int& hitFace, float limit,
                   Cnt<STATS>& c) {
     if constexpr (!COOP) return walk_bvh_seq<ANY, STATS>(S, i, end, r, minT, hitFace, limit, c);
+    // general kernels (the fused one) on scenes without large leaves: the plain walk, without
+    // the wave-uniform loop and its per-step ballots (a uniform branch)
+    if (!S.coop) return walk_bvh_seq<ANY, STATS>(S, i, end, r, minT, hitFace, limit, c);
     bool hit = false;
     const RayRcp q = ray_rcp(r);
     bool active = i < end;

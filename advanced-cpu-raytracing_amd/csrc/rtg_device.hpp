@@ -123,6 +123,7 @@ struct DevScene {
     float eps;
     float ambient[3];
     int background[3];
+    int coop;                        // the scene has large leaves (FEAT_BIGLEAF)
 };
 
 struct DevCamera {
