@@ -80,7 +80,7 @@ DEV int seg_append(bool want, int* lds_count) {
 }
 
 template <bool STATS>
-__global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_tree_shade(const DevScene S, const DevCamera C, const TreeLevel L,
+__global__ __launch_bounds__(256, RTG_TREE_SHADE_WAVES) void k_tree_shade(const DevScene S, const DevCamera C, const TreeLevel L,
                                                     const int level, const int pixel_base, const TreeSegs G,
                                                     DevCounters* counters) {
     __shared__ int nShadow, nChild;
