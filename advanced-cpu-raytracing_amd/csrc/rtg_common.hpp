@@ -18,7 +18,7 @@
 // 40-60% faster on path tracing, four slower.  The traversal kernels of plain scenes (meshes
 // with small leaves, spheres: 57-84 VGPRs) run at eight (+8% on C5); the large-leaf, instance
 // and transform variants (88-129 VGPRs) keep their natural allocation -- eight costs C3 20-30%
-// (DESIGN.md §5).
+// -- except the instance ones, at five (+8% on C4).
 #ifndef RTG_MEGA_WAVES
 #define RTG_MEGA_WAVES 2
 #endif
@@ -36,8 +36,12 @@
 #ifndef RTG_BIGLEAF_LEAN
 #define RTG_BIGLEAF_LEAN 0
 #endif
+#ifndef RTG_INST_WAVES
+#define RTG_INST_WAVES 5
+#endif
 #define RTG_TRACE_WAVES(FEAT) \
-    (((FEAT) & ~(FEAT_SPHERE | (RTG_BIGLEAF_LEAN ? FEAT_BIGLEAF : 0))) ? 1 : RTG_LEAN_WAVES)
+    (((FEAT) & ~(FEAT_SPHERE | (RTG_BIGLEAF_LEAN ? FEAT_BIGLEAF : 0))) \
+         ? (((FEAT) & FEAT_INSTANCE) ? RTG_INST_WAVES : 1) : RTG_LEAN_WAVES)
 
 namespace rtg {
 
