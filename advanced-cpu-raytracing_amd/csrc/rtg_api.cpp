@@ -344,7 +344,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
             const int first = M.face_offset + n.first;
             int leaf = -1;
             if (n.left < 0) leaf = (first < (1 << 23) && n.count < 255) ? (first << 8) | n.count : rtg::LEAF_EXT;
-            if (n.left < 0 && n.count > rtg::kCoopLeaf) bigleaf = true;
+            if (n.left < 0 && n.count > rtg::kBigLeaf) bigleaf = true;
             float4 a, b;
             a.x = n.bmin[0]; a.y = n.bmin[1]; a.z = n.bmin[2]; a.w = n.bmax[0];
             b.x = n.bmax[1]; b.y = n.bmax[2];

@@ -51,7 +51,7 @@ struct BvhTmp {
     int* axis; float* split; int* S; int* a; int* dosplit; int* childoff;
     unsigned long long* keys;       // 6 per node: child-box reduction keys
     int* size; int* pos;
-    int* bigleaf;                   // any leaf wider than kCoopLeaf
+    int* bigleaf;                   // any leaf wider than kBigLeaf
     void* scan_tmp; size_t scan_bytes;
 };
 
@@ -275,7 +275,7 @@ __global__ void k_write_nodes(BvhTmp T, int nn, int base, int faceOff, float4* _
         const int first = faceOff + T.first[v], cnt = T.count[v];
         leaf = (first < (1 << 23) && cnt < 255) ? (first << 8) | cnt : LEAF_EXT;
         e = make_int2(first, cnt);
-        if (cnt > kCoopLeaf) atomicOr(T.bigleaf, 1);
+        if (cnt > kBigLeaf) atomicOr(T.bigleaf, 1);
     }
     nodes[2 * at] = make_float4(b[0], b[1], b[2], b[3]);
     nodes[2 * at + 1] = make_float4(b[4], b[5], __int_as_float(skip), __int_as_float(leaf));

@@ -93,7 +93,17 @@ enum : int { LEAF_EXT = 0x7FFFFFFF };
 // Scene feature bits (kernel specialisation): spheres, mesh instances, any mesh with a
 // non-identity transform or motion blur, BVH leaves of more than kCoopLeaf faces.
 enum : int { FEAT_SPHERE = 1, FEAT_INSTANCE = 2, FEAT_XFORM = 4, FEAT_BIGLEAF = 8, FEAT_ALL = 15 };
-constexpr int kCoopLeaf = 8;
+// A scene with a leaf wider than kBigLeaf faces takes the cooperative walk (FEAT_BIGLEAF);
+// inside it, every leaf of more than kCoopLeaf faces is tested by the whole wave (threshold
+// 8 / 4 / 2 / 1 / 0: C3 1494 / 1680 / 1781 / 1886 / 1912, C4 1481 / 1537 / 1613 / 1648 / 1555
+// Mrays/s).  The selection threshold stays
+// higher: the cooperative walk costs ~40% where no leaf needs it, and the headline and C5
+// scenes have leaves of up to 4 faces.
+#ifndef RTG_COOP_LEAF
+#define RTG_COOP_LEAF 1
+#endif
+constexpr int kCoopLeaf = RTG_COOP_LEAF;
+constexpr int kBigLeaf = 8;
 
 struct DevScene {
     const float4* __restrict__ nodes;
