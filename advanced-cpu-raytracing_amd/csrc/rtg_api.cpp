@@ -126,8 +126,18 @@ struct rtg_scene {
     // RTG_RENDER_TIMING events (stage k runs between ev[k] and ev[k+1])
     hipEvent_t ev[rtg::MAX_STAGES + 1] = {};
     int timed_stages = 0;             // stages recorded by the last timed render
+    // the scene's own stream (rtg_render) and the event marking the end of its last render
+    // on whatever stream it was issued (rtg_scene_stats waits for it, not for the device)
+    hipStream_t stream = nullptr;
+    hipEvent_t done = nullptr;
+    // rtg_scene_create_multi: the other replicas (replica i renders part i of 1 + size())
+    std::vector<rtg_scene*> replicas;
     ~rtg_scene() {
+        for (rtg_scene* r : replicas) delete r;
+        (void)hipSetDevice(device);
         if (tree) rtg::tree_destroy(tree);
+        if (done) (void)hipEventDestroy(done);
+        if (stream) (void)hipStreamDestroy(stream);
         for (auto& e : ev)
             if (e) (void)hipEventDestroy(e);
         if (d_hdr) (void)hipFree(d_hdr);
@@ -620,15 +630,56 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     S.ambient[0] = d->ambient_light.x; S.ambient[1] = d->ambient_light.y; S.ambient[2] = d->ambient_light.z;
     for (int k = 0; k < 3; ++k) S.background[k] = d->background[k];
     S.coop = (sc->feat & rtg::FEAT_BIGLEAF) ? 1 : 0;
+    HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
+    HIP_TRY(hipEventCreateWithFlags(&sc->done, hipEventDisableTiming));
     HIP_TRY(hipDeviceSynchronize());
     *out = sc.release();
     return RTG_OK;
 }
 
+int rtg_scene_create_multi(const rtg_scene_desc* d, const int32_t* devices, int32_t n, rtg_scene** out) {
+    if (!d || !out || !devices || n < 1) return set_err(RTG_ERR_INVALID, "bad device list");
+    *out = nullptr;
+    rtg_scene* first = nullptr;
+    int rc = rtg_scene_create(d, devices[0], &first);
+    if (rc) return rc;
+    std::unique_ptr<rtg_scene> sc(first);
+    for (int i = 1; i < n; ++i) {
+        rtg_scene* r = nullptr;
+        rc = rtg_scene_create(d, devices[i], &r);
+        if (rc) return rc;
+        sc->replicas.push_back(r);
+    }
+    *out = sc.release();
+    return RTG_OK;
+}
+
+int rtg_scene_num_devices(const rtg_scene* s, int32_t* n) {
+    if (!s || !n) return set_err(RTG_ERR_INVALID, "null argument");
+    *n = 1 + (int32_t)s->replicas.size();
+    return RTG_OK;
+}
+
 void rtg_scene_destroy(rtg_scene* s) {
-    if (!s) return;
-    (void)hipSetDevice(s->device);
     delete s;
+}
+
+int rtg_part_runs(int32_t row_begin, int32_t row_end, int32_t part, int32_t parts, int32_t* runs, int32_t cap,
+                  int32_t* count) {
+    if (!count) return set_err(RTG_ERR_INVALID, "null argument");
+    if (parts <= 0) parts = 1;
+    if (part < 0 || part >= parts || row_begin < 0 || row_end < row_begin)
+        return set_err(RTG_ERR_INVALID, "bad partition (part %d of %d, rows [%d, %d))", part, parts, row_begin, row_end);
+    int n = 0, r0 = -1, r1 = -1;
+    for (int b = part; row_begin + b * RTG_PART_BAND_ROWS < row_end; b += parts) {
+        const int a = row_begin + b * RTG_PART_BAND_ROWS, e = std::min(a + RTG_PART_BAND_ROWS, (int)row_end);
+        if (a == r1) { r1 = e; continue; }
+        if (r0 >= 0) { if (runs && n < cap) { runs[2 * n] = r0; runs[2 * n + 1] = r1; } ++n; }
+        r0 = a; r1 = e;
+    }
+    if (r0 >= 0) { if (runs && n < cap) { runs[2 * n] = r0; runs[2 * n + 1] = r1; } ++n; }
+    *count = n;
+    return RTG_OK;
 }
 
 // Block -> tile assignment.  The hardware deals workgroups to the 8 XCDs round-robin
@@ -702,9 +753,23 @@ static int prepare(rtg_scene* s, const rtg_render_opts* o, rtg::DevCamera& C, rt
     P.accum_only = (o->flags & RTG_RENDER_ACCUM_ONLY) ? 1 : 0;
     if (!P.accum_only && (P.sample_begin != 0 || P.sample_count != C.spp))
         return set_err(RTG_ERR_INVALID, "a partial sample range requires RTG_RENDER_ACCUM_ONLY");
+    P.part_count = o->part_count <= 0 ? 1 : o->part_count;
+    P.part_index = o->part_index;
+    if (P.part_index < 0 || P.part_index >= P.part_count)
+        return set_err(RTG_ERR_INVALID, "part %d of %d", P.part_index, P.part_count);
+    // this part's bands of RTG_PART_BAND_ROWS (= the tile height) rows and its row count
+    const int bands = (P.row_end - P.row_begin + RTG_PART_BAND_ROWS - 1) / RTG_PART_BAND_ROWS;
+    const int own = bands > P.part_index ? (bands - P.part_index + P.part_count - 1) / P.part_count : 0;
+    P.part_rows = 0;
+    if (own > 0) {
+        const int lastBand = P.part_index + (own - 1) * P.part_count;
+        P.part_rows = (own - 1) * RTG_PART_BAND_ROWS +
+                      std::min(RTG_PART_BAND_ROWS, P.row_end - P.row_begin - lastBand * RTG_PART_BAND_ROWS);
+    }
     P.tiles_x = (c.width + 15) / 16;
-    P.tiles_y = (P.row_end - P.row_begin + 15) / 16;
+    P.tiles_y = own;
     P.num_tiles = P.tiles_x * P.tiles_y;
+    if (P.num_tiles == 0) return RTG_OK;   // nothing of this part in the row range
     P.seed = o->seed;
     int rc = ensure_tile_map(s, P.tiles_x, P.tiles_y);
     if (rc) return rc;
@@ -750,7 +815,7 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
     }
     // ray trees: the wavefront tree pipeline for large frames (it synchronises once per tree
     // level), the fused kernel otherwise; RTG_RENDER_TREE / RTG_RENDER_FUSED force either
-    const long long work = (long long)(P.row_end - P.row_begin) * C.width * P.sample_count;
+    const long long work = (long long)P.part_rows * C.width * P.sample_count;
     // path tracing runs in the fused kernel only (its GI chains live on the per-thread stack)
     const bool fused_only = (o->flags & RTG_RENDER_FUSED) || C.path_tracing;
     const bool use_tree = s->tree_ok && !fused_only &&
@@ -767,12 +832,11 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
         return RTG_OK;
     }
     if (s->wave_ok && !fused_only) {
-        const size_t rows = (size_t)(P.row_end - P.row_begin);
+        const size_t rows = (size_t)P.part_rows;
         int rc = ensure_wave(s, rows * C.width, s->num_slots, (size_t)P.num_tiles);
         if (rc) return rc;
         rtg::WaveBufs W = s->wave;
         W.num_slots = s->num_slots;
-        W.pixel_base = P.row_begin * C.width;
         if (P.accum_only) W.accum = (float4*)d_accum;
         else if (C.spp > 1) {   // internal accumulator indexed by absolute pixel
             size_t need = (size_t)C.width * C.height;
@@ -781,7 +845,6 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
                 if (rc2) return rc2;
                 W = s->wave;
                 W.num_slots = s->num_slots;
-                W.pixel_base = P.row_begin * C.width;
             }
         }
         HIP_TRY(rtg::launch_wave(s->ds, C, P, W, d_hdr, d_ldr, s->counters.p, stats, s->feat, stream, ev));
@@ -800,42 +863,133 @@ int rtg_render_device(rtg_scene* s, const rtg_render_opts* o, float* d_hdr, uint
     int rc = prepare(s, o, C, P);
     if (rc) return rc;
     if (P.accum_only && !d_accum) return set_err(RTG_ERR_INVALID, "RTG_RENDER_ACCUM_ONLY needs an accumulation buffer");
+    if (P.num_tiles == 0) return RTG_OK;
     HIP_TRY(hipSetDevice(s->device));
-    return launch(s, o, C, P, d_hdr, d_ldr, d_accum, (hipStream_t)stream);
+    rc = launch(s, o, C, P, d_hdr, d_ldr, d_accum, (hipStream_t)stream);
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(s->done, (hipStream_t)stream));
+    return RTG_OK;
 }
 
-int rtg_render(rtg_scene* s, const rtg_render_opts* o, float* hdr_rgb, uint8_t* ldr_rgb) {
-    rtg::DevCamera C;
-    rtg::RenderParams P;
-    int rc = prepare(s, o, C, P);
+// D2H of the rows of opts' part: one async copy per run of consecutive rows, straight into
+// the same offsets of the host frame (layout 3*(x + y*width), main.cpp:109).
+static int copy_part(const rtg_render_opts* o, int width, int height, const float* d_hdr, const uint8_t* d_ldr,
+                     float* hdr, uint8_t* ldr, hipStream_t st) {
+    const int rb = o->row_begin < 0 ? 0 : o->row_begin;
+    const int re = (o->row_end <= 0 || o->row_end > height) ? height : o->row_end;
+    int32_t n = 0;
+    int rc = rtg_part_runs(rb, re, o->part_index, o->part_count, nullptr, 0, &n);
     if (rc) return rc;
-    if (P.accum_only) return set_err(RTG_ERR_INVALID, "use rtg_render_device for RTG_RENDER_ACCUM_ONLY");
-    HIP_TRY(hipSetDevice(s->device));
-    const size_t pixels = (size_t)C.width * C.height;
-    if (s->d_pixels < pixels) {
-        if (s->d_hdr) { (void)hipFree(s->d_hdr); s->d_hdr = nullptr; }
-        if (s->d_ldr) { (void)hipFree(s->d_ldr); s->d_ldr = nullptr; }
-        s->d_pixels = 0;
-        HIP_TRY(hipMalloc(&s->d_hdr, pixels * 3 * sizeof(float)));
-        HIP_TRY(hipMalloc(&s->d_ldr, pixels * 3));
-        s->d_pixels = pixels;
+    std::vector<int32_t> runs(2 * (size_t)n);
+    rc = rtg_part_runs(rb, re, o->part_index, o->part_count, runs.data(), n, &n);
+    if (rc) return rc;
+    for (int k = 0; k < n; ++k) {
+        const size_t off = (size_t)runs[2 * k] * width * 3, cnt = (size_t)(runs[2 * k + 1] - runs[2 * k]) * width * 3;
+        if (hdr && d_hdr) HIP_TRY(hipMemcpyAsync(hdr + off, d_hdr + off, cnt * sizeof(float), hipMemcpyDeviceToHost, st));
+        if (ldr && d_ldr) HIP_TRY(hipMemcpyAsync(ldr + off, d_ldr + off, cnt, hipMemcpyDeviceToHost, st));
     }
-    HIP_TRY(hipMemset(s->d_hdr, 0, pixels * 3 * sizeof(float)));
-    HIP_TRY(hipMemset(s->d_ldr, 0, pixels * 3));
-    rc = launch(s, o, C, P, s->d_hdr, s->d_ldr, nullptr, nullptr);
-    if (rc) return rc;
-    // tonemapped camera, whole image: the LDR output is the tonemapped image (main.cpp:187-192)
+    return RTG_OK;
+}
+
+int rtg_copy_part_to_host(rtg_scene* s, const rtg_render_opts* o, const float* d_hdr, const uint8_t* d_ldr,
+                          float* hdr_rgb, uint8_t* ldr_rgb, void* stream) {
+    if (!s || !o) return set_err(RTG_ERR_INVALID, "null argument");
+    if (o->camera < 0 || o->camera >= (int)s->cameras.size()) return set_err(RTG_ERR_INVALID, "bad camera %d", o->camera);
+    const rtg_camera& c = s->cameras[o->camera];
+    HIP_TRY(hipSetDevice(s->device));
+    return copy_part(o, c.width, c.height, d_hdr, d_ldr, hdr_rgb, ldr_rgb, (hipStream_t)stream);
+}
+
+// Replaces main.cpp:164-185.  With replicas (rtg_scene_create_multi) replica i renders part
+// i of n on its own stream and copies its rows into the caller's buffers; the renders of all
+// replicas are enqueued before any copy (a copy to pageable memory may block the host), then
+// every stream is synchronised -- never the whole device.
+int rtg_render(rtg_scene* s, const rtg_render_opts* o, float* hdr_rgb, uint8_t* ldr_rgb) {
+    if (!s || !o) return set_err(RTG_ERR_INVALID, "null argument");
+    if (o->flags & RTG_RENDER_ACCUM_ONLY) return set_err(RTG_ERR_INVALID, "use rtg_render_device for RTG_RENDER_ACCUM_ONLY");
+    std::vector<rtg_scene*> reps(1, s);
+    reps.insert(reps.end(), s->replicas.begin(), s->replicas.end());
+    const int n = (int)reps.size();
+    if (n > 1 && o->part_count > 1)
+        return set_err(RTG_ERR_INVALID, "a multi-device scene deals its own partition (part_count must be <= 1)");
+    if (o->camera < 0 || o->camera >= (int)s->cameras.size()) return set_err(RTG_ERR_INVALID, "bad camera %d", o->camera);
     const rtg_camera& cam = s->cameras[o->camera];
-    if (cam.has_tonemapper && P.row_begin == 0 && P.row_end == C.height) {
-        rtg_tonemap_params tp = {cam.tm_key, cam.tm_burn, cam.tm_saturation, cam.tm_gamma};
-        rc = rtg_tonemap_device(s->d_hdr, C.width, C.height, &tp, s->d_ldr, s->device, nullptr);
+    std::vector<rtg_render_opts> ro(n, *o);
+    bool whole = false;
+    for (int i = 0; i < n; ++i) {
+        rtg_scene* r = reps[i];
+        if (n > 1) { ro[i].part_index = i; ro[i].part_count = n; }
+        rtg::DevCamera C;
+        rtg::RenderParams P;
+        int rc = prepare(r, &ro[i], C, P);
+        if (rc) return rc;
+        whole = P.row_begin == 0 && P.row_end == C.height && (n > 1 || P.part_count == 1);
+        HIP_TRY(hipSetDevice(r->device));
+        const size_t pixels = (size_t)C.width * C.height;
+        if (r->d_pixels < pixels) {
+            HIP_TRY(hipStreamSynchronize(r->stream));
+            if (r->d_hdr) { (void)hipFree(r->d_hdr); r->d_hdr = nullptr; }
+            if (r->d_ldr) { (void)hipFree(r->d_ldr); r->d_ldr = nullptr; }
+            r->d_pixels = 0;
+            HIP_TRY(hipMalloc(&r->d_hdr, pixels * 3 * sizeof(float)));
+            HIP_TRY(hipMalloc(&r->d_ldr, pixels * 3));
+            r->d_pixels = pixels;
+        }
+        if (P.num_tiles == 0) continue;
+        rc = launch(r, &ro[i], C, P, r->d_hdr, r->d_ldr, nullptr, r->stream);
+        if (rc) return rc;
+        HIP_TRY(hipEventRecord(r->done, r->stream));
+    }
+    // tonemapped camera over the whole image: the LDR output is the tonemapped image
+    // (main.cpp:187-192); it needs every pixel, so with several parts it runs on the
+    // gathered float image
+    const bool tonemap = cam.has_tonemapper && whole;
+    const rtg_tonemap_params tp = {cam.tm_key, cam.tm_burn, cam.tm_saturation, cam.tm_gamma};
+    if (tonemap && n == 1) {
+        int rc = rtg_tonemap_device(s->d_hdr, cam.width, cam.height, &tp, s->d_ldr, s->device, s->stream);
         if (rc) return rc;
     }
-    HIP_TRY(hipDeviceSynchronize());
-    // rows outside [row_begin, row_end) are left untouched in the caller's buffers
-    const size_t off = (size_t)P.row_begin * C.width * 3, n = (size_t)(P.row_end - P.row_begin) * C.width * 3;
-    if (hdr_rgb) HIP_TRY(hipMemcpy(hdr_rgb + off, s->d_hdr + off, n * sizeof(float), hipMemcpyDeviceToHost));
-    if (ldr_rgb) HIP_TRY(hipMemcpy(ldr_rgb + off, s->d_ldr + off, n, hipMemcpyDeviceToHost));
+    std::vector<float> tmp;
+    float* hdr = hdr_rgb;
+    if (tonemap && n > 1 && ldr_rgb && !hdr) {
+        tmp.resize((size_t)cam.width * cam.height * 3);
+        hdr = tmp.data();
+    }
+    for (int i = 0; i < n; ++i) {
+        HIP_TRY(hipSetDevice(reps[i]->device));
+        int rc = copy_part(&ro[i], cam.width, cam.height, reps[i]->d_hdr, reps[i]->d_ldr, hdr,
+                           (tonemap && n > 1) ? nullptr : ldr_rgb, reps[i]->stream);
+        if (rc) return rc;
+    }
+    for (int i = 0; i < n; ++i) {
+        HIP_TRY(hipSetDevice(reps[i]->device));
+        HIP_TRY(hipStreamSynchronize(reps[i]->stream));
+    }
+    if (tonemap && n > 1 && ldr_rgb) return rtg_tonemap(hdr, cam.width, cam.height, &tp, ldr_rgb, s->device);
+    return RTG_OK;
+}
+
+int rtg_host_alloc(size_t bytes, void** out) {
+    if (!out || !bytes) return set_err(RTG_ERR_INVALID, "bad arguments");
+    *out = nullptr;
+    HIP_TRY(hipHostMalloc(out, bytes, hipHostMallocPortable));
+    return RTG_OK;
+}
+
+int rtg_host_free(void* p) {
+    if (p) HIP_TRY(hipHostFree(p));
+    return RTG_OK;
+}
+
+int rtg_host_register(void* p, size_t bytes) {
+    if (!p || !bytes) return set_err(RTG_ERR_INVALID, "bad arguments");
+    HIP_TRY(hipHostRegister(p, bytes, hipHostRegisterPortable));
+    return RTG_OK;
+}
+
+int rtg_host_unregister(void* p) {
+    if (!p) return set_err(RTG_ERR_INVALID, "null argument");
+    HIP_TRY(hipHostUnregister(p));
     return RTG_OK;
 }
 
@@ -888,27 +1042,36 @@ int rtg_resolve_accum(const float* accum, int32_t w, int32_t h, float* hdr, uint
 
 int rtg_scene_stats(rtg_scene* s, rtg_stats* out) {
     if (!s || !out) return set_err(RTG_ERR_INVALID, "null argument");
-    HIP_TRY(hipSetDevice(s->device));
-    rtg::DevCounters c;
-    HIP_TRY(hipDeviceSynchronize());
-    HIP_TRY(hipMemcpy(&c, s->counters.p, sizeof(c), hipMemcpyDeviceToHost));
-    out->camera_rays = c.camera_rays;
-    out->secondary_rays = c.secondary_rays;
-    out->shadow_rays = c.shadow_rays;
-    out->node_visits = c.node_visits;
-    out->tri_tests = c.tri_tests;
-    out->sphere_tests = c.sphere_tests;
-    out->object_tests = c.object_tests;
-    out->shadow_node_visits = c.shadow_node_visits;
-    out->shadow_tri_tests = c.shadow_tri_tests;
-    out->pad0 = 0;
+    std::vector<rtg_scene*> reps(1, s);
+    reps.insert(reps.end(), s->replicas.begin(), s->replicas.end());
+    std::memset(out, 0, sizeof(*out));
+    for (rtg_scene* r : reps) {
+        HIP_TRY(hipSetDevice(r->device));
+        rtg::DevCounters c;
+        HIP_TRY(hipEventSynchronize(r->done));
+        HIP_TRY(hipMemcpy(&c, r->counters.p, sizeof(c), hipMemcpyDeviceToHost));
+        out->camera_rays += c.camera_rays;
+        out->secondary_rays += c.secondary_rays;
+        out->shadow_rays += c.shadow_rays;
+        out->node_visits += c.node_visits;
+        out->tri_tests += c.tri_tests;
+        out->sphere_tests += c.sphere_tests;
+        out->object_tests += c.object_tests;
+        out->shadow_node_visits += c.shadow_node_visits;
+        out->shadow_tri_tests += c.shadow_tri_tests;
+    }
     return RTG_OK;
 }
 
 int rtg_scene_reset_stats(rtg_scene* s) {
     if (!s) return set_err(RTG_ERR_INVALID, "null argument");
-    HIP_TRY(hipSetDevice(s->device));
-    HIP_TRY(hipMemset(s->counters.p, 0, sizeof(rtg::DevCounters)));
+    std::vector<rtg_scene*> reps(1, s);
+    reps.insert(reps.end(), s->replicas.begin(), s->replicas.end());
+    for (rtg_scene* r : reps) {
+        HIP_TRY(hipSetDevice(r->device));
+        HIP_TRY(hipEventSynchronize(r->done));
+        HIP_TRY(hipMemset(r->counters.p, 0, sizeof(rtg::DevCounters)));
+    }
     return RTG_OK;
 }
 

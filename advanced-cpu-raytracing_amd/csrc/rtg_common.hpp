@@ -1216,12 +1216,30 @@ DEV unsigned char ldr(float c) {
 
 // 16x16-pixel tile per 256-thread block, 8x8 per wave; tiles dealt so that consecutive
 // tiles share an XCD (blocks b and b+8 share one under round-robin dispatch).
-DEV void tile_pixel(const RenderParams& P, int& px, int& py) {
+// Image row of compact row `crow` of this render's part (RenderParams): band crow/16 of
+// the part is band (crow/16) * part_count + part_index of the row range.
+DEV int part_row(const RenderParams& P, int crow) {
+    return P.row_begin + (((crow >> 4) * P.part_count + P.part_index) << 4) + (crow & 15);
+}
+// Image pixel of compact pixel index i (= crow * width + x).
+DEV int part_pixel(const RenderParams& P, int width, int i) {
+    const int crow = i / width;
+    return part_row(P, crow) * width + (i - crow * width);
+}
+
+// tile_pixel also returns the compact row (index of the pixel's work-buffer entries:
+// crow * width + px).
+DEV void tile_pixel(const RenderParams& P, int& px, int& py, int& crow) {
     const int tile = P.tile_map[blockIdx.x];
     const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     px = tx * 16 + (w & 1) * 8 + (l & 7);
-    py = P.row_begin + ty * 16 + (w >> 1) * 8 + (l >> 3);
+    crow = ty * 16 + (w >> 1) * 8 + (l >> 3);
+    py = part_row(P, crow);
+}
+DEV void tile_pixel(const RenderParams& P, int& px, int& py) {
+    int crow;
+    tile_pixel(P, px, py, crow);
 }
 
 template <bool STATS>

@@ -144,13 +144,18 @@ struct DevCamera {
     int path_tracing, next_event, importance_sampling, russian_roulette;   // RendererParams (rendererParams.h)
 };
 
+// Image partition (multi-GPU): the rows [row_begin, row_end) are cut into 16-row bands
+// (the tile height), band b counted from row_begin belongs to part b % part_count.  A
+// render covers its part's rows only; they are numbered densely ("compact rows", 0 ..
+// part_rows-1) for the per-pixel work buffers, and part_row() maps them back to image rows.
 struct RenderParams {
     int row_begin, row_end;
     int sample_begin, sample_count;
     int accum_only;
-    int tiles_x, tiles_y, num_tiles;
+    int tiles_x, tiles_y, num_tiles;    // tiles_y: this part's bands
+    int part_index, part_count, part_rows;
     unsigned long long seed;
-    const int* __restrict__ tile_map;   // block -> 16x16 tile (host-built, XCD-aware)
+    const int* __restrict__ tile_map;   // block -> 16x16 tile of this part (host-built, XCD-aware)
 };
 
 // Wavefront pipeline buffers (rtg_wave.hip), one entry per pixel of the rendered rows
@@ -170,7 +175,6 @@ struct WaveBufs {
     int* __restrict__ q_count;          // per block: entries in its segment
     float4* __restrict__ accum;         // multi-sample: sum w*c, sum w
     int num_slots;                      // lights per pixel
-    int pixel_base;                     // row_begin * width
 };
 
 // One level of the wavefront ray tree (rtg_tree.hip): rays, their hits, the shading node

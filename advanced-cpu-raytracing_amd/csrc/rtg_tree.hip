@@ -33,10 +33,10 @@ enum : int { TK_LIT = 16 };
 enum : int { TM_ZERO = 0, TM_ENV = 1 };
 
 __global__ __launch_bounds__(256) void k_tree_gen(const DevCamera C, const RenderParams P, const int sample,
-                                                  const TreeLevel L0, const int pixel_base) {
+                                                  const TreeLevel L0) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= L0.n) return;
-    const int pixel = pixel_base + i;
+    const int pixel = part_pixel(P, C.width, i);
     const int px = pixel % C.width, py = pixel / C.width;
     const uint64_t key = root_key(P.seed, pixel, sample);
     float mbTime;
@@ -81,7 +81,7 @@ DEV int seg_append(bool want, int* lds_count) {
 
 template <bool STATS>
 __global__ __launch_bounds__(256, RTG_TREE_SHADE_WAVES) void k_tree_shade(const DevScene S, const DevCamera C, const TreeLevel L,
-                                                    const int level, const int pixel_base, const TreeSegs G,
+                                                    const int level, const RenderParams P, const TreeSegs G,
                                                     DevCounters* counters) {
     __shared__ int nShadow, nChild;
     if (threadIdx.x == 0) { nShadow = 0; nChild = 0; }
@@ -112,7 +112,7 @@ __global__ __launch_bounds__(256, RTG_TREE_SHADE_WAVES) void k_tree_shade(const 
         if (obj < 0) {
             f3 v;
             if (level == 0) {
-                const int pixel = pixel_base + i;
+                const int pixel = part_pixel(P, C.width, i);
                 v = miss_color(S, C, pixel % C.width, pixel / C.width, r.d);
             } else {
                 const float4 m = L.miss[i];
@@ -346,7 +346,7 @@ __global__ __launch_bounds__(256) void k_tree_compact(const TreeSegs G, const in
 __global__ __launch_bounds__(256) void k_tree_resolve(const DevScene S, const DevCamera C, const RenderParams P,
                                                       const int sample, const int first, const int last,
                                                       const TreeLevel L, const TreeLevel Lc, const int level,
-                                                      const int num_slots, const int pixel_base,
+                                                      const int num_slots,
                                                       float* __restrict__ hdr, unsigned char* __restrict__ ldrOut,
                                                       float4* __restrict__ accum) {
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -415,7 +415,7 @@ __global__ __launch_bounds__(256) void k_tree_resolve(const DevScene S, const De
         return;
     }
     // level 0: the pixel (RenderPixel's colour), spp accumulation as k_resolve
-    const int pixel = pixel_base + i;
+    const int pixel = part_pixel(P, C.width, i);
     if (C.spp <= 1 && !P.accum_only) {
         const size_t idx = 3 * (size_t)pixel;
         if (hdr) { hdr[idx] = value.x; hdr[idx + 1] = value.y; hdr[idx + 2] = value.z; }
@@ -513,8 +513,7 @@ static hipError_t tree_pass(TreeState& T, const DevScene& S, const DevCamera& C,
                             bool first, bool last, float* hdr, unsigned char* l, float4* accum, DevCounters* cnt,
                             hipStream_t st, hipEvent_t* ev) {
     const int ns = S.num_point + S.num_area + S.num_env + S.num_dir + S.num_spot + S.num_mesh;
-    const int npix = (P.row_end - P.row_begin) * C.width;
-    const int pixel_base = P.row_begin * C.width;
+    const int npix = P.part_rows * C.width;
     hipError_t e;
     size_t n = (size_t)npix;
     int level = 0;
@@ -525,9 +524,9 @@ static hipError_t tree_pass(TreeState& T, const DevScene& S, const DevCamera& C,
         TreeLevel& L = T.levels[level].L;
         const int blocks = (int)((n + 255) / 256);
         if ((e = ensure_segs(T, (size_t)blocks, ns)) != hipSuccess) return e;
-        if (level == 0) hipLaunchKernelGGL(k_tree_gen, dim3(blocks), dim3(256), 0, st, C, P, s, L, pixel_base);
+        if (level == 0) hipLaunchKernelGGL(k_tree_gen, dim3(blocks), dim3(256), 0, st, C, P, s, L);
         hipLaunchKernelGGL((k_tree_trace<STATS, FEAT>), dim3(blocks), dim3(256), 0, st, S, L, level, cnt);
-        hipLaunchKernelGGL((k_tree_shade<STATS>), dim3(blocks), dim3(256), 0, st, S, C, L, level, pixel_base, T.G, cnt);
+        hipLaunchKernelGGL((k_tree_shade<STATS>), dim3(blocks), dim3(256), 0, st, S, C, L, level, P, T.G, cnt);
         if (ns > 0) {
             WaveBufs W{};
             W.q_o = T.G.q_o; W.q_d = T.G.q_d; W.q_slot = T.G.q_slot; W.q_count = T.G.q_count;
@@ -553,7 +552,7 @@ static hipError_t tree_pass(TreeState& T, const DevScene& S, const DevCamera& C,
         const TreeLevel& Lc = lv < level ? T.levels[lv + 1].L : L;
         const int blocks = (int)((L.n + 255) / 256);
         hipLaunchKernelGGL(k_tree_resolve, dim3(blocks), dim3(256), 0, st, S, C, P, s, (int)first, (int)last, L,
-                           Lc, lv, ns, pixel_base, hdr, l, accum);
+                           Lc, lv, ns, hdr, l, accum);
     }
     if (ev) (void)hipEventRecord(ev[2], st);
     return hipGetLastError();

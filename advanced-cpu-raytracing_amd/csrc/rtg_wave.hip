@@ -25,8 +25,8 @@ enum { BASE_FINAL = 1, BASE_ADD_ZERO = 2 };
 template <bool STATS, int FEAT>
 __global__ __launch_bounds__(256, RTG_TRACE_WAVES(FEAT)) void k_primary(const DevScene S, const DevCamera C, const RenderParams P,
                                                  const int sample, const WaveBufs W, DevCounters* counters) {
-    int px, py;
-    tile_pixel(P, px, py);
+    int px, py, crow;
+    tile_pixel(P, px, py, crow);
     Cnt<STATS> cn;
     if (px < C.width && py < P.row_end) {
         const int pixel = px + py * C.width;
@@ -36,7 +36,7 @@ __global__ __launch_bounds__(256, RTG_TRACE_WAVES(FEAT)) void k_primary(const De
         cn.cam();
         Hit h;
         trace<false, STATS, FEAT>(S, ray, mbTime, INFINITY, INFINITY, h, cn);
-        const int i = pixel - W.pixel_base;
+        const int i = crow * C.width + px;
         W.hit_t[i] = h.t;
         W.hit_obj[i] = h.obj;
         W.hit_face[i] = h.face;
@@ -64,13 +64,13 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_shade(const DevScene S
     __shared__ int seg_count;
     if (threadIdx.x == 0) seg_count = 0;
     __syncthreads();
-    int px, py;
-    tile_pixel(P, px, py);
+    int px, py, crow;
+    tile_pixel(P, px, py, crow);
     const size_t seg = (size_t)blockIdx.x * 256 * W.num_slots;
     Cnt<STATS> cn;
     const bool valid = px < C.width && py < P.row_end;
     const int pixel = valid ? px + py * C.width : 0;
-    const int i = pixel - W.pixel_base;
+    const int i = valid ? crow * C.width + px : 0;
     const uint64_t key = root_key(P.seed, pixel, sample);
     const int obj = valid ? W.hit_obj[i] : -1;
     // lanes that need the light loop
@@ -226,9 +226,9 @@ __global__ __launch_bounds__(256) void k_resolve(const DevCamera C, const Render
                                                  float* __restrict__ hdr, unsigned char* __restrict__ ldrOut,
                                                  float4* __restrict__ accum) {
     const int i = blockIdx.x * 256 + threadIdx.x;
-    const int npix = (P.row_end - P.row_begin) * C.width;
+    const int npix = P.part_rows * C.width;
     if (i >= npix) return;
-    const int pixel = i + W.pixel_base;
+    const int pixel = part_pixel(P, C.width, i);
     const float4 b = W.base[i];
     const int flags = __float_as_int(b.w);
     f3 color = mk(b.x, b.y, b.z);
@@ -268,7 +268,7 @@ __global__ __launch_bounds__(256) void k_resolve(const DevCamera C, const Render
 template <bool STATS, int FEAT>
 static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W,
                                 float* hdr, unsigned char* l, DevCounters* cnt, hipStream_t st, hipEvent_t* ev) {
-    const int npix = (P.row_end - P.row_begin) * C.width;
+    const int npix = P.part_rows * C.width;
     const int nshadow = S.num_point + S.num_area + S.num_dir + S.num_spot + S.num_mesh;
     float4* accum = W.accum;
     for (int s = P.sample_begin; s < P.sample_begin + P.sample_count; ++s) {

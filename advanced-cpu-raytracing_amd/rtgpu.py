@@ -52,6 +52,8 @@ class RenderOpts(ctypes.Structure):
         ("row_end", ctypes.c_int32),
         ("flags", ctypes.c_int32),
         ("seed", ctypes.c_uint64),
+        ("part_index", ctypes.c_int32),
+        ("part_count", ctypes.c_int32),
     ]
 
 
@@ -73,6 +75,8 @@ EXPORTED = [
     "rtg_scene_stats", "rtg_scene_reset_stats", "rtg_scene_timings", "rtg_tonemap_device", "rtg_tonemap",
     "rtg_write_png", "rtg_write_hdr",
     "rtg_last_error", "rtg_abi_version",
+    "rtg_scene_create_multi", "rtg_scene_num_devices", "rtg_part_runs", "rtg_copy_part_to_host",
+    "rtg_host_alloc", "rtg_host_free", "rtg_host_register", "rtg_host_unregister",
 ]
 
 _lib = None
@@ -120,6 +124,14 @@ def lib() -> ctypes.CDLL:
     L.rtg_tonemap.argtypes = [vp, i32, i32, P(TonemapParams), vp, i32]
     L.rtg_write_png.argtypes = [ctypes.c_char_p, i32, i32, vp]
     L.rtg_write_hdr.argtypes = [ctypes.c_char_p, i32, i32, vp]
+    L.rtg_scene_create_multi.argtypes = [vp, P(i32), i32, P(vp)]
+    L.rtg_scene_num_devices.argtypes = [vp, P(i32)]
+    L.rtg_part_runs.argtypes = [i32, i32, i32, i32, vp, i32, P(i32)]
+    L.rtg_copy_part_to_host.argtypes = [vp, P(RenderOpts), vp, vp, vp, vp, vp]
+    L.rtg_host_alloc.argtypes = [ctypes.c_size_t, P(vp)]
+    L.rtg_host_free.argtypes = [vp]
+    L.rtg_host_register.argtypes = [vp, ctypes.c_size_t]
+    L.rtg_host_unregister.argtypes = [vp]
     _lib = L
     return L
 
@@ -181,35 +193,58 @@ class HostScene:
 
 
 class DeviceScene:
-    """Device-resident scene replica (rtg_scene) on HIP device ``device``."""
+    """Device-resident scene replica (rtg_scene) on HIP device ``device``, or -- with
+    ``devices=[d0, d1, ...]`` -- one replica per listed device (rtg_scene_create_multi),
+    among which ``render()`` deals the frame's parts (multigpu.py)."""
 
-    def __init__(self, host: HostScene, device: int = 0):
+    def __init__(self, host: HostScene, device: int = 0, devices=None):
         s = ctypes.c_void_p()
-        _check(lib().rtg_scene_create(host.desc, device, ctypes.byref(s)))
+        if devices:
+            arr = (ctypes.c_int32 * len(devices))(*devices)
+            _check(lib().rtg_scene_create_multi(host.desc, arr, len(devices), ctypes.byref(s)))
+            device = devices[0]
+        else:
+            _check(lib().rtg_scene_create(host.desc, device, ctypes.byref(s)))
         self._s = s
         self.host = host
         self.device = device
+        self.devices = list(devices) if devices else [device]
 
     @staticmethod
-    def opts(camera=0, sample_begin=0, sample_count=-1, rows=(0, 0), flags=0, seed=0x5EED) -> RenderOpts:
-        return RenderOpts(camera, sample_begin, sample_count, rows[0], rows[1], flags, seed)
+    def opts(camera=0, sample_begin=0, sample_count=-1, rows=(0, 0), flags=0, seed=0x5EED, part=(0, 1)) -> RenderOpts:
+        return RenderOpts(camera, sample_begin, sample_count, rows[0], rows[1], flags, seed, part[0], part[1])
 
-    def render(self, camera: int = 0, rows=(0, 0), flags: int = 0, seed: int = 0x5EED):
-        """Host-buffer render of one camera -> (hdr float32 HxWx3, ldr uint8 HxWx3)."""
+    def render(self, camera: int = 0, rows=(0, 0), flags: int = 0, seed: int = 0x5EED, part=(0, 1), out=None):
+        """Host-buffer render of one camera -> (hdr float32 HxWx3, ldr uint8 HxWx3).  With
+        ``part=(i, n)`` only part i's rows are rendered and written (zeros elsewhere, or
+        what ``out=(hdr, ldr)`` already holds)."""
         c = self.host.camera(camera)
-        hdr = np.zeros((c["height"], c["width"], 3), np.float32)
-        ldr = np.zeros((c["height"], c["width"], 3), np.uint8)
-        o = self.opts(camera, 0, -1, rows, flags, seed)
-        _check(lib().rtg_render(self._s, ctypes.byref(o), hdr.ctypes.data, ldr.ctypes.data))
+        if out is None:
+            hdr = np.zeros((c["height"], c["width"], 3), np.float32)
+            ldr = np.zeros((c["height"], c["width"], 3), np.uint8)
+        else:
+            hdr, ldr = out
+        o = self.opts(camera, 0, -1, rows, flags, seed, part)
+        _check(lib().rtg_render(self._s, ctypes.byref(o), hdr.ctypes.data if hdr is not None else None,
+                                ldr.ctypes.data if ldr is not None else None))
         return hdr, ldr
 
     def render_device(self, hdr_ptr: int, ldr_ptr: int, stream: int = 0, camera: int = 0, flags: int = 0,
                       seed: int = 0x5EED, accum_ptr: int = 0, sample_begin: int = 0, sample_count: int = -1,
-                      rows=(0, 0)):
-        """Asynchronous render into device buffers (e.g. torch tensor data_ptr()s) on ``stream``."""
-        o = self.opts(camera, sample_begin, sample_count, rows, flags, seed)
+                      rows=(0, 0), part=(0, 1)):
+        """Asynchronous render into device buffers (e.g. torch tensor data_ptr()s) on ``stream``;
+        ``part=(i, n)``: part i of n of the frame (multigpu.py)."""
+        o = self.opts(camera, sample_begin, sample_count, rows, flags, seed, part)
         _check(lib().rtg_render_device(self._s, ctypes.byref(o), hdr_ptr or None, ldr_ptr or None,
                                        accum_ptr or None, stream or None))
+
+    def copy_part_to_host(self, d_hdr: int, d_ldr: int, h_hdr: int, h_ldr: int, stream: int = 0, camera: int = 0,
+                          rows=(0, 0), part=(0, 1)):
+        """Enqueue the DMA of part ``part``'s rows from full-frame device buffers to the same
+        offsets of full-frame host buffers (the host framebuffer gather)."""
+        o = self.opts(camera, 0, -1, rows, 0, 0, part)
+        _check(lib().rtg_copy_part_to_host(self._s, ctypes.byref(o), d_hdr or None, d_ldr or None, h_hdr or None,
+                                           h_ldr or None, stream or None))
 
     def export_bvh(self):
         """(nodes (N, 8) float32, tris (F, 12) float32): the device's walk records."""
@@ -241,6 +276,30 @@ class DeviceScene:
         if getattr(self, "_s", None):
             lib().rtg_scene_destroy(self._s)
             self._s = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+class PinnedArray:
+    """Page-locked host array (rtg_host_alloc): the frame buffer of the drop-in host path
+    (the CLI allocates its frames the same way), so the device-to-host copy is one DMA."""
+
+    def __init__(self, shape, dtype):
+        nbytes = int(np.prod(shape)) * np.dtype(dtype).itemsize
+        p = ctypes.c_void_p()
+        _check(lib().rtg_host_alloc(nbytes, ctypes.byref(p)))
+        self.ptr = p.value
+        self.array = np.frombuffer((ctypes.c_char * nbytes).from_address(self.ptr), dtype).reshape(shape)
+
+    def close(self):
+        if getattr(self, "ptr", None):
+            self.array = None
+            lib().rtg_host_free(self.ptr)
+            self.ptr = None
 
     def __del__(self):
         try:

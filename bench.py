@@ -1,18 +1,23 @@
 """Headline bench: Mrays/s on the BASELINE.json synthetic K-triangle scene at 1920x1080
-(primary + shadow rays), with the HBM-roofline fraction of the render kernel and the
-reference's own multithreaded CPU path timed on this host beside it.
+(primary + shadow rays), the roofline fraction of the dominant kernel against the memory
+level that serves its bytes, and the reference's own multithreaded CPU path timed on this
+host beside it.
 
     python bench.py [--gpus N --steps K --warmup W]
     python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1 \
         --master-port P bench.py --gpus N --steps K --warmup W
 
-A step = one full 1920x1080 frame (one sample pass) traced and shaded on each rank,
-inputs (scene, BVH) resident in HBM.  Ranks are independent (sample-parallel: rank r
-traces sample pass r of the same frame) -> weak scaling, no collective on the data path;
-the only collectives are the barriers around the timed region and the max-over-ranks of
-the elapsed time.
+A step = one full 1920x1080 frame (one sample pass) traced and shaded, inputs (scene, BVH)
+resident in HBM.  With N ranks the frame is partitioned (multigpu.py): rank r renders the
+16-row bands b with b % N == r into its own HBM -- strong scaling of one frame, no collective
+on the data path (the barriers around the timed region and the max-over-ranks of the elapsed
+time are the only collectives).  `value` = rays of the frame x steps / max-over-ranks time.
+The host framebuffer gather (every rank DMA-ing its rows into one page-locked shared frame)
+is timed separately ("gather"); the one-process host-buffer path of the CLI ("host_frame")
+too -- neither is `value` (the PCIe-inclusive rates).
 """
 import argparse
+import glob
 import json
 import os
 import shutil
@@ -26,7 +31,9 @@ PKG = os.path.join(ROOT, "advanced-cpu-raytracing_amd")
 sys.path.insert(0, PKG)
 
 METRIC = "Mrays/sec + achieved HBM GB/s fraction, 1920×1080 primary+shadow rays"
-HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md)
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak (MI355X_MICROARCH.md, "HBM")
+L2_PEAK_GBS = 34500.0      # MI355X L2 aggregate over the 8 XCDs (MI355X_MICROARCH.md, "L2 (per XCD)")
+SWEEP_K = (1000, 10082, 100352, 1002528)
 
 
 def parse():
@@ -38,9 +45,9 @@ def parse():
     p.add_argument("--width", type=int, default=1920)
     p.add_argument("--height", type=int, default=1080)
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-threads", type=int, default=8, help="reference THREAD_COUNT (main.cpp:15)")
     p.add_argument("--cpu-reps", type=int, default=3)
-    p.add_argument("--sweep", action="store_true", help="also report K in {1k,10k,1M} (extra field)")
+    p.add_argument("--no-sweep", action="store_true", help="skip the K sweep (rank 0, N=1 only)")
+    p.add_argument("--no-extras", action="store_true", help="skip gather / host-frame timings")
     p.add_argument("--config", default="headline", choices=["headline", "c2", "c3", "c4", "c5"],
                    help="BASELINE.json configuration (c2-c5: one frame = all camera samples)")
     return p.parse_args()
@@ -55,11 +62,12 @@ CONFIG_DESC = {
 }
 
 
-def make_workload(args, out_dir):
+def make_workload(args, out_dir, K=None):
     import scenes
-    if args.config == "headline":
-        xml = scenes.synthetic_heightfield(out_dir, K=args.K, width=args.width, height=args.height)
-        desc = (f"synthetic height field K={args.K} tris, {args.width}x{args.height}, 1 spp, 1 point light, "
+    if args.config == "headline" or K is not None:
+        K = K or args.K
+        xml = scenes.synthetic_heightfield(out_dir, K=K, width=args.width, height=args.height)
+        desc = (f"synthetic height field K={K} tris, {args.width}x{args.height}, 1 spp, 1 point light, "
                 "default Blinn-Phong, primary+shadow rays")
         return xml, desc
     if args.config == "c2":
@@ -69,45 +77,87 @@ def make_workload(args, out_dir):
     return xml, CONFIG_DESC[args.config]
 
 
-def cpu_baseline(xml_dir, xml, rays_per_frame, threads, reps):
-    """Reference CPU path (oracle/_ref/refdriver: the reference's own sources, row-band
-    threads exactly as main.cpp:38-39,164-185) on this host; falls back to the oracle
-    restatement ("port") when the reference build is absent."""
-    drv = os.path.join(ROOT, "oracle", "_ref", "refdriver")
-    sample = f"full 1920x1080 frame x {reps} reps, {threads} threads (render only: spawn->join)"
-    if os.path.exists(drv):
-        out = subprocess.run([drv, "bench", os.path.basename(xml), str(threads), str(reps)], cwd=xml_dir,
-                             capture_output=True, text=True, timeout=600, check=True).stdout
-        line = [l for l in out.splitlines() if l.startswith("{")][-1]
-        secs = sorted(json.loads(line)["seconds"])
-        med = secs[len(secs) // 2]
-        return {"value": round(rays_per_frame / med / 1e6, 3), "unit": "Mrays/s", "cores": threads,
-                "kind": "reference", "sample": sample, "seconds_median": round(med, 4)}
-    sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import oracle_bind as ob
-    import rtgpu
-    hs = rtgpu.HostScene(xml)
-    secs = []
-    for _ in range(reps):
-        t0 = time.perf_counter()
-        ob.render(hs, threads=threads)
-        secs.append(time.perf_counter() - t0)
-    secs.sort()
-    med = secs[len(secs) // 2]
-    return {"value": round(rays_per_frame / med / 1e6, 3), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": sample, "seconds_median": round(med, 4)}
-
-
 def log(msg):
     """Progress on stderr (long configurations: keeps the run visibly alive)."""
     print(f"[bench {time.strftime('%H:%M:%S')}] {msg}", file=sys.stderr, flush=True)
 
 
-def measure(ds, torch, hdr, ldr, steps, warmup, seed, barrier):
+# ----------------------------------------------------------------------------- CPU baseline
+def box_threads():
+    """The host cores this process may use: the affinity mask, capped by OMP_NUM_THREADS
+    (the GPU box sets it to the box's CPU share)."""
+    n = len(os.sched_getaffinity(0))
+    omp = int(os.environ.get("OMP_NUM_THREADS", "0") or 0)
+    return min(n, omp) if omp > 0 else n
+
+
+def cpu_model():
+    try:
+        out = subprocess.run(["lscpu"], capture_output=True, text=True, timeout=10).stdout
+        for line in out.splitlines():
+            if line.startswith("Model name:"):
+                return line.split(":", 1)[1].strip()
+    except (OSError, subprocess.SubprocessError):
+        pass
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _median(v):
+    v = sorted(v)
+    return v[len(v) // 2]
+
+
+def cpu_baseline(xml_dir, xml, rays_per_frame, reps):
+    """The reference's CPU path (oracle/_ref/refdriver: its own sources, row-band threads
+    exactly as main.cpp:38-39,164-185) on this host, in SURVEY §8d's two modes: A = the
+    reference's THREAD_COUNT (8), B = every core of this box's share.  Per mode: the
+    render alone (thread spawn -> join) and the reference-equivalent span main.cpp:138->199
+    (Raytracer copy + render + PNG encode).  Falls back to the CPU restatement ("port") when
+    the reference build is absent."""
+    drv = os.path.join(ROOT, "oracle", "_ref", "refdriver")
+    modes = {}
+    kind = "reference" if os.path.exists(drv) else "port"
+    for label, threads in (("A", 8), ("B", box_threads())):
+        if kind == "reference":
+            out = subprocess.run([drv, "bench", os.path.basename(xml), str(threads), str(reps), "0",
+                                  os.path.join(xml_dir, "refdriver_bench.png")], cwd=xml_dir,
+                                 capture_output=True, text=True, timeout=900, check=True).stdout
+            rec = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
+            render_s, span_s = _median(rec["seconds"]), _median(rec["span_seconds"])
+        else:
+            sys.path.insert(0, os.path.join(ROOT, "tests"))
+            import oracle_bind as ob
+            import rtgpu
+            hs = rtgpu.HostScene(xml)
+            secs = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                ob.render(hs, threads=threads)
+                secs.append(time.perf_counter() - t0)
+            render_s = span_s = _median(secs)
+        modes[label] = {"threads": threads, "render_s": round(render_s, 4), "span_s": round(span_s, 4),
+                        "mrays_s": round(rays_per_frame / render_s / 1e6, 3),
+                        "span_mrays_s": round(rays_per_frame / span_s / 1e6, 3)}
+        log(f"cpu baseline mode {label}: {threads} threads, {modes[label]['mrays_s']} Mrays/s")
+    a = modes["A"]
+    return {"value": a["mrays_s"], "unit": "Mrays/s", "cores": a["threads"], "kind": kind,
+            "sample": f"full {os.path.basename(xml)} frame x {reps} reps per mode; value = mode A (the reference's "
+                      f"THREAD_COUNT=8, render only: spawn->join, main.cpp:164-185); mode B = the box's "
+                      f"{modes['B']['threads']} cores; span = main.cpp:138->199 (Raytracer copy + render + PNG)",
+            "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(), "modes": modes}
+
+
+# ----------------------------------------------------------------------------- timing
+def measure(render, torch, steps, warmup, barrier):
     stream = torch.cuda.current_stream()
-    sptr = stream.cuda_stream
     for k in range(warmup):
-        ds.render_device(hdr.data_ptr(), ldr.data_ptr(), sptr, seed=seed)
+        render()
         torch.cuda.synchronize()
         log(f"warmup {k + 1}/{warmup}")
     torch.cuda.synchronize()
@@ -118,7 +168,7 @@ def measure(ds, torch, hdr, ldr, steps, warmup, seed, barrier):
     t0 = time.perf_counter()
     for k in range(steps):
         starts[k].record(stream)
-        ds.render_device(hdr.data_ptr(), ldr.data_ptr(), sptr, seed=seed)
+        render()
         ends[k].record(stream)
     torch.cuda.synchronize()
     barrier()
@@ -127,34 +177,19 @@ def measure(ds, torch, hdr, ldr, steps, warmup, seed, barrier):
     return elapsed, kern_ms
 
 
-def kernel_times(ds, torch, hdr, ldr, steps, seed):
+def kernel_times(ds, torch, render_timed, steps):
     """Per-kernel durations: HIP events recorded by the library around each kernel on the
-    render's stream (RTG_RENDER_TIMING), averaged over `steps` frames run after the timed
-    region."""
-    import rtgpu
-    sptr = torch.cuda.current_stream().cuda_stream
+    render's stream (RTG_RENDER_TIMING), averaged over `steps` frames."""
     acc = {}
     for _ in range(steps):
-        ds.render_device(hdr.data_ptr(), ldr.data_ptr(), sptr, seed=seed, flags=rtgpu.RTG_RENDER_TIMING)
+        render_timed()
         for k, v in ds.timings().items():
             acc[k] = acc.get(k, 0.0) + v
     return {k: v / steps for k, v in acc.items()}
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
-    (profiles/*_pmc.json, made by tools/pmc_summary.py from separate rocprofv3 --pmc
-    FETCH_SIZE / WRITE_SIZE passes of this bench); None when absent."""
-    import glob
-    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc.json")))
-    if not files:
-        return None, None
-    k = json.load(open(files[-1]))["kernels"].get(kernel + "<false>")
-    return (k["traffic_bytes"] if k else None), os.path.basename(files[-1])
-
-
 def kernel_bytes(st, W, H):
-    """Algorithmic HBM bytes per launch of each kernel (32 B per node visit,
+    """Algorithmic bytes per launch of each kernel (32 B per node visit,
     36 B per triangle test, 64 B per ray = ray in + hit out, 15 B per pixel written)."""
     ext_rays = st["camera_rays"] + st["secondary_rays"]
     ext = 32 * st["node_visits"] + 36 * st["tri_tests"] + 64 * ext_rays
@@ -163,35 +198,132 @@ def kernel_bytes(st, W, H):
             "tree_levels": ext + shd, "frame": ext + shd + 15 * W * H}
 
 
+def pmc_summary(kernel, K, world):
+    """Counter-measured bytes per launch of `kernel` for the K-triangle headline scene from
+    the newest committed summary (profiles/r*_pmc*.json, tools/pmc_summary.py over separate
+    rocprofv3 --pmc passes of this bench): HBM traffic = 2 x FETCH_SIZE + WRITE_SIZE (gfx950
+    correction, MI355X_MICROARCH.md), L2 hit rate from TCC_HIT / TCC_MISS.  None if absent."""
+    best = None
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc*.json"))):
+        rec = json.load(open(f))
+        cfg = rec.get("config", {"K": 100352, "n_gpus": 1})
+        if cfg.get("K") != K or cfg.get("n_gpus", 1) != world:
+            continue
+        # the timed kernels (the counting pass runs the <true> = STATS instantiations)
+        v = rec["kernels"].get(kernel + "<false>") or rec["kernels"].get(kernel)
+        if v and "traffic_bytes" in v:
+            best = dict(v, source=os.path.basename(f))
+    return best
+
+
+def roofline(kernel, algo_bytes, kernel_ms, pmc):
+    """Dominant kernel's roofline.  `achieved` = algorithmic bytes / its average launch time.
+    The peak is that of the level serving those bytes: HBM when the counter-measured HBM
+    traffic is at least half the algorithmic bytes, else L2 (the scene's nodes and
+    triangles are re-read from the caches: the 10 MB headline scene sits in L2 / Infinity
+    Cache and the measured HBM bytes are a few % of the algorithmic ones)."""
+    secs = kernel_ms * 1e-3
+    achieved = algo_bytes / secs / 1e9
+    traffic = pmc["traffic_bytes"] if pmc else None
+    hbm_gbs = traffic / secs / 1e9 if traffic is not None else None
+    serves_hbm = traffic is not None and traffic >= 0.5 * algo_bytes
+    peak = HBM_PEAK_GBS if serves_hbm else L2_PEAK_GBS
+    r = {"bound": "hbm" if serves_hbm else "l2", "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
+         "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": kernel, "kernel_ms": round(kernel_ms, 4),
+         "algo_bytes_per_launch": int(algo_bytes),
+         "hbm_gbs_measured": round(hbm_gbs, 1) if hbm_gbs is not None else None,
+         "hbm_frac_measured": round(hbm_gbs / HBM_PEAK_GBS, 4) if hbm_gbs is not None else None,
+         "l2_frac": round(achieved / L2_PEAK_GBS, 4)}
+    if pmc:
+        r["traffic_source"] = pmc["source"]
+        if "l2_hit_rate" in pmc:
+            r["l2_hit_rate"] = pmc["l2_hit_rate"]
+    return r
+
+
+def frame_stats(ds, torch, render_counting, reduce_sum):
+    ds.reset_stats()
+    render_counting()
+    torch.cuda.synchronize()
+    st = reduce_sum(ds.stats())
+    return st, st["camera_rays"] + st["secondary_rays"] + st["shadow_rays"]
+
+
+def sweep_point(args, torch, rtgpu, local, K, hdr, ldr):
+    """One K of the sweep on this GPU: rays, Mrays/s, dominant kernel and its roofline."""
+    sub = tempfile.mkdtemp(prefix="rtg_sweep_")
+    old = os.getcwd()
+    try:
+        xml, _ = make_workload(args, sub, K=K)
+        os.chdir(sub)
+        hs = rtgpu.HostScene(xml)
+        ds = rtgpu.DeviceScene(hs, local)
+        sptr = torch.cuda.current_stream().cuda_stream
+        st, rays = frame_stats(ds, torch, lambda: ds.render_device(hdr.data_ptr(), ldr.data_ptr(), sptr,
+                                                                   flags=rtgpu.RTG_RENDER_COUNT_STATS), lambda s: s)
+        steps = max(5, args.steps // 2)
+        e, _ = measure(lambda: ds.render_device(hdr.data_ptr(), ldr.data_ptr(), sptr), torch, steps, 1, lambda: None)
+        kt = kernel_times(ds, torch, lambda: ds.render_device(hdr.data_ptr(), ldr.data_ptr(), sptr,
+                                                              flags=rtgpu.RTG_RENDER_TIMING), 5)
+        kb = kernel_bytes(st, args.width, args.height)
+        dom = max((k for k in kt if k in kb), key=lambda k: kt[k])
+        rl = roofline(dom, kb[dom], kt[dom], pmc_summary(dom, K, 1))
+        ds.close()
+        hs.close()
+        return {"mrays_s": round(rays * steps / e / 1e6, 1), "ms_per_frame": round(e / steps * 1e3, 4),
+                "rays": int(rays), "kernels_ms": {k: round(v, 4) for k, v in kt.items()}, "roofline": rl}
+    finally:
+        os.chdir(old)
+        shutil.rmtree(sub, ignore_errors=True)
+
+
 def main():
     args = parse()
     import torch
 
+    import multigpu
     import rtgpu
-    import scenes
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}; launch N>1 with "
+                         "torch.distributed.run --nproc-per-node N (one rank per GPU)")
     dist = None
     # RTG_BENCH_BACKEND=gloo: rehearse the multi-rank flow on a box with fewer GPUs than ranks
     # (ranks share devices round-robin); the driver's runs use RCCL, one GPU per rank
     backend = os.environ.get("RTG_BENCH_BACKEND", "nccl")
     if backend != "nccl":
         local = local % max(1, torch.cuda.device_count())
+    torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
-    else:
-        torch.cuda.set_device(local)
     barrier = (lambda: dist.barrier()) if dist else (lambda: None)
+    rdev = f"cuda:{local}" if backend == "nccl" else "cpu"
+
+    def reduce_max(x):
+        if not dist:
+            return x
+        t = torch.tensor([x], dtype=torch.float64, device=rdev)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        return float(t.item())
+
+    def reduce_sum(stats):
+        if not dist:
+            return stats
+        keys = sorted(stats)
+        t = torch.tensor([stats[k] for k in keys], dtype=torch.float64, device=rdev)
+        dist.all_reduce(t)
+        return {k: int(v) for k, v in zip(keys, t.tolist())}
 
     tmp = tempfile.mkdtemp(prefix=f"rtg_bench_r{rank}_")
     old = os.getcwd()
+    frame = None
     try:
         xml, desc = make_workload(args, tmp)
         os.chdir(tmp)
@@ -201,39 +333,36 @@ def main():
         H, W = cam["height"], cam["width"]
         hdr = torch.empty((H, W, 3), dtype=torch.float32, device=f"cuda:{local}")
         ldr = torch.empty((H, W, 3), dtype=torch.uint8, device=f"cuda:{local}")
-        seed = 0x5EED + rank
+        seed = 0x5EED
+        part = (rank, world)
+        sptr = torch.cuda.current_stream().cuda_stream
 
-        # untimed counting pass: rays / BVH nodes / triangle tests per frame
-        log(f"scene ready: {hs.counts()}, counting pass")
-        ds.reset_stats()
-        ds.render_device(hdr.data_ptr(), ldr.data_ptr(), torch.cuda.current_stream().cuda_stream, seed=seed,
-                         flags=rtgpu.RTG_RENDER_COUNT_STATS)
-        torch.cuda.synchronize()
-        st = ds.stats()
+        def render(flags=0):
+            ds.render_device(hdr.data_ptr(), ldr.data_ptr(), sptr, seed=seed, flags=flags, part=part)
+
+        # untimed counting pass: rays / BVH nodes / triangle tests of the whole frame
+        log(f"scene ready: {hs.counts()}, part {rank}/{world}, counting pass")
+        part_st, part_rays = frame_stats(ds, torch, lambda: render(rtgpu.RTG_RENDER_COUNT_STATS), lambda s: s)
+        st = reduce_sum(part_st)
         rays = st["camera_rays"] + st["secondary_rays"] + st["shadow_rays"]
 
-        log(f"rays/frame {rays}; timing {args.steps} steps")
-        elapsed, kern_ms = measure(ds, torch, hdr, ldr, args.steps, args.warmup, seed, barrier)
+        log(f"rays/frame {rays} (this part {part_rays}); timing {args.steps} steps")
+        elapsed, kern_ms = measure(render, torch, args.steps, args.warmup, barrier)
         log(f"timed: {elapsed / args.steps * 1e3:.3f} ms/step")
-        if dist:
-            rdev = f"cuda:{local}" if backend == "nccl" else "cpu"
-            t = torch.tensor([elapsed], dtype=torch.float64, device=rdev)
-            dist.all_reduce(t, op=dist.ReduceOp.MAX)
-            elapsed = float(t.item())
-            k = torch.tensor([kern_ms], dtype=torch.float64, device=rdev)
-            dist.all_reduce(k, op=dist.ReduceOp.MAX)
-            kern_ms = float(k.item())
+        elapsed = reduce_max(elapsed)
+        kern_ms = reduce_max(kern_ms)
+        value = rays * args.steps / elapsed / 1e6
 
-        value = world * rays * args.steps / elapsed / 1e6
-        ktimes = kernel_times(ds, torch, hdr, ldr, args.steps, seed)
-        # the library times the kernels of the last sample pass: bytes of one pass
-        kbytes = {k: v / max(1, cam["spp"]) for k, v in kernel_bytes(st, W, H).items()}
-        # the dominant traversal kernel: k_primary (wavefront) or k_render (fused)
+        ktimes = kernel_times(ds, torch, lambda: render(rtgpu.RTG_RENDER_TIMING), args.steps)
+        # the library times the kernels of the last sample pass: bytes of this rank's pass
+        kbytes = {k: v / max(1, cam["spp"]) for k, v in kernel_bytes(part_st, W, H).items()}
         dom = max((k for k in ktimes if k in kbytes), key=lambda k: ktimes[k])
-        algo_bytes = kbytes[dom]
-        achieved = algo_bytes / (ktimes[dom] * 1e-3) / 1e9
-        frame_gbs = kbytes["frame"] * max(1, cam["spp"]) / (kern_ms * 1e-3) / 1e9
-        traffic, traffic_src = pmc_traffic(dom) if args.config == "headline" else (None, None)
+        K = int(args.K) if args.config == "headline" else None
+        rl = roofline(dom, kbytes[dom], ktimes[dom], pmc_summary(dom, K, world) if K else None)
+        rl.update({"kernels_ms": {k: round(v, 4) for k, v in ktimes.items()}, "frame_ms": round(kern_ms, 4),
+                   "frame_algo_bytes": int(kernel_bytes(st, W, H)["frame"]),
+                   "frame_l2_frac": round(kernel_bytes(st, W, H)["frame"] / (kern_ms * 1e-3) / 1e9 / L2_PEAK_GBS, 4)})
+        ext = max(rays - st["shadow_rays"], 1)
         result = {
             "metric": METRIC,
             "value": round(value, 2),
@@ -243,66 +372,85 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 4),
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (seeded procedural height field, written as the reference's XML+PLY)",
             "config": {
                 "workload": desc,
-                "scene_K": int(args.K) if args.config == "headline" else int(hs.counts()["faces"]),
+                "scene_K": K if K else int(hs.counts()["faces"]),
                 "width": W, "height": H, "spp": int(cam["spp"]),
                 "rays_per_frame": int(rays),
                 "camera_rays": int(st["camera_rays"]), "shadow_rays": int(st["shadow_rays"]),
-                "node_visits_per_extend_ray": round(st["node_visits"] / max(rays - st["shadow_rays"], 1), 2),
-                "tri_tests_per_extend_ray": round(st["tri_tests"] / max(rays - st["shadow_rays"], 1), 2),
+                "node_visits_per_extend_ray": round(st["node_visits"] / ext, 2),
+                "tri_tests_per_extend_ray": round(st["tri_tests"] / ext, 2),
                 "shadow_node_visits_per_ray": round(st["shadow_node_visits"] / max(st["shadow_rays"], 1), 2),
                 "shadow_tri_tests_per_ray": round(st["shadow_tri_tests"] / max(st["shadow_rays"], 1), 2),
-                "parallelism": f"sample-parallel x{world} (rank r traces sample pass r)",
+                "parallelism": f"image partition x{world}: 16-row bands dealt round-robin, rank r renders bands "
+                               f"b % {world} == r (one frame per step)",
             },
-            "roofline": {
-                "bound": "hbm",
-                "achieved": round(achieved, 1),
-                "peak": HBM_PEAK_GBS,
-                "unit": "GB/s",
-                "frac": round(achieved / HBM_PEAK_GBS, 4),
-                "traffic": traffic,
-                "traffic_source": traffic_src,
-                "kernel": dom,
-                "kernel_ms": round(ktimes[dom], 4),
-                "algo_bytes_per_launch": int(algo_bytes),
-                "kernels_ms": {k: round(v, 4) for k, v in ktimes.items()},
-                "frame_ms": round(kern_ms, 4),
-                "frame_algo_bytes": int(kbytes["frame"] * max(1, cam["spp"])),
-                "frame_frac": round(frame_gbs / HBM_PEAK_GBS, 4),
-            },
+            "roofline": rl,
             "cpu_baseline": None,
         }
-        if args.sweep and rank == 0 and args.config == "headline":
+
+        if not args.no_extras:
+            # host framebuffer gather: every rank DMAs its rows into one page-locked shared
+            # frame (LDR = what main.cpp saves; + the float frame for a tonemapped camera)
+            name = f"rtg_bench_{os.environ.get('MASTER_PORT', str(os.getpid()))}"
+            if rank == 0:
+                frame = multigpu.SharedFrame(name, H, W, hdr=cam["tonemapped"], ldr=True, create=True)
+            barrier()
+            if rank != 0:
+                frame = multigpu.SharedFrame(name, H, W, hdr=cam["tonemapped"], ldr=True)
+            frame.pin()
+            fr = frame
+            g_el, _ = measure(lambda: multigpu.render_part(ds, rank, world, hdr.data_ptr(), ldr.data_ptr(), sptr, fr,
+                                                           seed=seed), torch, args.steps, 1, barrier)
+            g_el = reduce_max(g_el)
+            result["gather"] = {"ms_per_frame": round(g_el / args.steps * 1e3, 4),
+                                "mrays_s": round(rays * args.steps / g_el / 1e6, 2),
+                                "bytes_per_frame": int(H * W * 3 * (5 if cam["tonemapped"] else 1)),
+                                "what": "render + DMA of each rank's rows into one page-locked /dev/shm frame"}
+            if world == 1:
+                # the drop-in host path (rtg_render: per-scene stream, page-locked frame, as the CLI)
+                ph = rtgpu.PinnedArray((H, W, 3), "float32") if cam["tonemapped"] else None
+                pl = rtgpu.PinnedArray((H, W, 3), "uint8")
+                outs = (ph.array if ph else None, pl.array)
+                for _ in range(2):
+                    ds.render(0, seed=seed, out=outs)
+                t0 = time.perf_counter()
+                for _ in range(args.steps):
+                    ds.render(0, seed=seed, out=outs)
+                hf = (time.perf_counter() - t0) / args.steps
+                t0 = time.perf_counter()
+                rtgpu.write_png(os.path.join(tmp, "frame.png"), pl.array)
+                png = time.perf_counter() - t0
+                result["host_frame"] = {"render_ms": round(hf * 1e3, 4), "png_ms": round(png * 1e3, 2),
+                                        "mrays_s": round(rays / hf / 1e6, 2),
+                                        "what": "rtg_render into page-locked host frames (CLI path; the PNG "
+                                                "encode of main.cpp:197 timed apart)"}
+                pl.close()
+                if ph:
+                    ph.close()
+
+        if rank == 0 and world == 1 and not args.no_sweep and args.config == "headline":
             sweep = {}
-            for K in (1000, 10082, 1002528):
-                sub = tempfile.mkdtemp(prefix="rtg_sweep_")
-                x2 = scenes.synthetic_heightfield(sub, K=K, width=W, height=H)
-                os.chdir(sub)
-                h2 = rtgpu.HostScene(x2)
-                d2 = rtgpu.DeviceScene(h2, local)
-                d2.reset_stats()
-                d2.render_device(hdr.data_ptr(), ldr.data_ptr(), torch.cuda.current_stream().cuda_stream,
-                                 flags=rtgpu.RTG_RENDER_COUNT_STATS)
-                torch.cuda.synchronize()
-                s2 = d2.stats()
-                r2 = s2["camera_rays"] + s2["shadow_rays"] + s2["secondary_rays"]
-                e2, k2 = measure(d2, torch, hdr, ldr, max(3, args.steps // 2), 1, 0x5EED, lambda: None)
-                sweep[str(K)] = {"mrays_s": round(r2 * max(3, args.steps // 2) / e2 / 1e6, 1),
-                                 "kernel_ms": round(k2, 3), "rays": int(r2)}
-                d2.close()
-                h2.close()
-                shutil.rmtree(sub, ignore_errors=True)
+            for Ks in SWEEP_K:
+                if Ks == args.K:
+                    sweep[str(Ks)] = {"mrays_s": round(value, 1), "ms_per_frame": result["ms_per_step"],
+                                      "rays": int(rays), "kernels_ms": rl["kernels_ms"],
+                                      "roofline": {k: rl[k] for k in rl if k not in ("kernels_ms",)}}
+                    continue
+                log(f"sweep K={Ks}")
+                sweep[str(Ks)] = sweep_point(args, torch, rtgpu, local, Ks, hdr, ldr)
             result["sweep_K"] = sweep
         if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "headline":
-            result["cpu_baseline"] = cpu_baseline(tmp, xml, rays, args.cpu_threads, args.cpu_reps)
+            result["cpu_baseline"] = cpu_baseline(tmp, xml, rays, args.cpu_reps)
         if rank == 0:
             print(json.dumps(result), flush=True)
     finally:
+        if frame is not None:
+            frame.close()
         os.chdir(old)
         shutil.rmtree(tmp, ignore_errors=True)
         if dist:

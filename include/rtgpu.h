@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 2
+#define RTG_ABI_VERSION 3
 
 enum rtg_status {
     RTG_OK = 0,
@@ -271,6 +271,18 @@ int rtg_scene_export_bvh(const rtg_scene* s, float* nodes, int64_t max_nodes, fl
 void rtg_scene_destroy(rtg_scene* scene);
 int rtg_device_count(int32_t* count);
 
+/* Multi-GPU scene (replaces the reference's 8 row-band threads,
+ * main.cpp:38-39,164-185, with the GPUs of one node): one device-resident replica per
+ * entry of `devices`, each with its own stream (an entry may repeat: several replicas on
+ * one device).  rtg_render on such a scene deals the frame to the replicas -- replica i
+ * renders part i of num_devices (rtg_render_opts.part_index) -- and each copies its rows
+ * straight into the caller's host buffers: the host framebuffer gather, no collective.
+ * rtg_render_device, rtg_scene_timings and rtg_scene_export_bvh use the first replica;
+ * rtg_scene_stats sums all replicas. */
+int rtg_scene_create_multi(const rtg_scene_desc* desc, const int32_t* devices, int32_t num_devices,
+                           rtg_scene** out);
+int rtg_scene_num_devices(const rtg_scene* scene, int32_t* num_devices);
+
 enum rtg_render_flags {
     RTG_RENDER_COUNT_STATS = 1,   /* accumulate rtg_stats (slower kernel variant)      */
     RTG_RENDER_ACCUM_ONLY = 2,    /* write the weighted sample sum (r,g,b,w) only; used
@@ -293,7 +305,23 @@ typedef struct {
                                      row bands (main.cpp:38-39) are one choice */
     int32_t flags;                /* rtg_render_flags */
     uint64_t seed;                /* counter-based RNG key (stochastic features) */
+    /* Image partition (ABI 3).  The rows [row_begin, row_end) are cut into bands of
+     * RTG_PART_BAND_ROWS rows; band b (counted from row_begin) belongs to part
+     * b % part_count.  A render with part_count > 1 computes and writes only the pixels
+     * of part part_index; the union of parts 0..part_count-1 is bit-identical to the
+     * whole render (pixels are independent, the RNG is keyed by pixel).  This is how
+     * the frame is dealt to the GPUs of a node (main.cpp:38-39 deals row bands to
+     * threads).  part_count <= 0 means 1. */
+    int32_t part_index, part_count;
 } rtg_render_opts;
+
+#define RTG_PART_BAND_ROWS 16
+
+/* The rows of part `part_index` of `part_count` within [row_begin, row_end), as maximal
+ * runs of consecutive rows: runs[2k] = first row, runs[2k+1] = one past the last.  Writes
+ * up to `cap` runs; *count = number of runs.  Pure host arithmetic (no device needed). */
+int rtg_part_runs(int32_t row_begin, int32_t row_end, int32_t part_index, int32_t part_count, int32_t* runs,
+                  int32_t cap, int32_t* count);
 
 typedef struct {
     uint64_t camera_rays;         /* primary rays (one per pixel-sample)            */
@@ -324,11 +352,26 @@ int rtg_render(rtg_scene* scene, const rtg_render_opts* opts, float* hdr_rgb, ui
 int rtg_render_device(rtg_scene* scene, const rtg_render_opts* opts, float* d_hdr_rgb,
                       uint8_t* d_ldr_rgb, float* d_accum, void* stream);
 
+/* Host framebuffer gather for one process per GPU: enqueue on `stream` the copies of the
+ * rows of part opts->part_index (opts as given to rtg_render_device) from full-frame device
+ * buffers into the same offsets of full-frame host buffers (either pair may be NULL).  With
+ * page-locked host memory (rtg_host_alloc / rtg_host_register, e.g. a shared-memory frame
+ * mapped by every rank) the copies are asynchronous DMA. */
+int rtg_copy_part_to_host(rtg_scene* scene, const rtg_render_opts* opts, const float* d_hdr_rgb,
+                          const uint8_t* d_ldr_rgb, float* hdr_rgb, uint8_t* ldr_rgb, void* stream);
+
+/* Page-locked host memory for frame buffers (hipHostMalloc / hipHostRegister). */
+int rtg_host_alloc(size_t bytes, void** out);
+int rtg_host_free(void* ptr);
+int rtg_host_register(void* ptr, size_t bytes);
+int rtg_host_unregister(void* ptr);
+
 /* Normalise an accumulation buffer (sum over devices) into hdr/ldr, host side. */
 int rtg_resolve_accum(const float* accum, int32_t width, int32_t height, float* hdr_rgb,
                       uint8_t* ldr_rgb);
 
-/* Stats of the last RTG_RENDER_COUNT_STATS render (synchronises). */
+/* Stats of the last RTG_RENDER_COUNT_STATS render (waits for the scene's last render,
+ * not for the device). */
 int rtg_scene_stats(rtg_scene* scene, rtg_stats* out);
 int rtg_scene_reset_stats(rtg_scene* scene);
 

@@ -12,10 +12,11 @@
 //       Stochastic scenes (path tracing, area / environment lights): n RenderPixel calls per
 //       pixel, single-threaded.  Writes "RTGV" int32 w, h, n, then the per-pixel mean and
 //       the variance of that mean (w*h*3 float32 each) -- the statistical golden.
-//   refdriver bench <scene.xml> <threads> <reps> [camera]
+//   refdriver bench <scene.xml> <threads> <reps> [camera] [png]
 //       Times the reference's row-band render exactly as main.cpp:164-185 partitions it
 //       (rows [t*(H/T), (t+1)*(H/T)) per thread; spawn -> join), spp==1 per pixel via
-//       RenderPixel, and prints one JSON line with the per-rep seconds.
+//       RenderPixel, and the reference-equivalent span main.cpp:138-199 (Raytracer copy +
+//       render + PNG encode); prints one JSON line with the per-rep seconds of both.
 //   refdriver tonemap <in.bin> <key> <burn%> <saturation> <gamma> <out.bin>
 //       The reference's own Tonemapper::Tonemap (tonemapper.h:28-60) on an "RTGF" float
 //       image (as dump writes); writes "RTGL" int32 w, int32 h, w*h*3 uint8 (the LDR
@@ -99,16 +100,23 @@ static int dumpavg(const char* xml, const char* out, int n, int ci) {
     return 0;
 }
 
-static int bench(const char* xml, int threads, int reps, int ci) {
+// Per rep two clocks: "seconds" = spawn -> join of the row-band threads (render only,
+// main.cpp:164-185); "span_seconds" = the reference's own "Rendering took" span
+// main.cpp:138 -> 199 for one camera: Raytracer copy-construction (main.cpp:140), the
+// LDR frame buffer, the threaded render with the clamp of main.cpp:118-124, and the PNG
+// encode of main.cpp:197 (written to png_out, "" = /dev/null-like temp name).
+static int bench(const char* xml, int threads, int reps, int ci, const char* png_out) {
     Scene scene;
     scene.loadFromXml(xml);
-    Raytracer renderer(scene);
     Camera& cam = scene.cameras[ci];
-    renderer.activeCamera = &cam;
     const int w = cam.imageWidth, h = cam.imageHeight;
     std::vector<float> img((size_t)w * h * 3);
-    std::printf("{\"threads\": %d, \"width\": %d, \"height\": %d, \"seconds\": [", threads, w, h);
+    std::vector<double> render_s, span_s;
     for (int r = 0; r < reps; ++r) {
+        auto s0 = std::chrono::steady_clock::now();
+        Raytracer renderer(scene);
+        renderer.activeCamera = &cam;
+        std::vector<unsigned char> ldr((size_t)w * h * 3);
         auto t0 = std::chrono::steady_clock::now();
         std::vector<std::thread> th;
         for (int t = 0; t < threads; ++t) {
@@ -119,15 +127,24 @@ static int bench(const char* xml, int threads, int reps, int ci) {
                         Vec3f c = renderer.RenderPixel(x, y, cam);
                         size_t i = 3 * ((size_t)x + (size_t)y * w);
                         img[i] = c.x; img[i + 1] = c.y; img[i + 2] = c.z;
+                        Vec3i q = clamp(c);
+                        ldr[i] = q.x; ldr[i + 1] = q.y; ldr[i + 2] = q.z;
                     }
             });
         }
         for (auto& t : th) t.join();
-        double s = std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
-        std::printf("%s%.6f", r ? ", " : "", s);
+        auto t1 = std::chrono::steady_clock::now();
+        stbi_write_png(png_out, w, h, 3, ldr.data(), w * 3);
+        auto s1 = std::chrono::steady_clock::now();
+        render_s.push_back(std::chrono::duration<double>(t1 - t0).count());
+        span_s.push_back(std::chrono::duration<double>(s1 - s0).count());
     }
     double checksum = 0;
     for (float v : img) checksum += v;
+    std::printf("{\"threads\": %d, \"width\": %d, \"height\": %d, \"seconds\": [", threads, w, h);
+    for (size_t r = 0; r < render_s.size(); ++r) std::printf("%s%.6f", r ? ", " : "", render_s[r]);
+    std::printf("], \"span_seconds\": [");
+    for (size_t r = 0; r < span_s.size(); ++r) std::printf("%s%.6f", r ? ", " : "", span_s[r]);
     std::printf("], \"checksum\": %.6f}\n", checksum);
     return 0;
 }
@@ -160,7 +177,8 @@ int main(int argc, char** argv) {
     if (argc >= 5 && !std::strcmp(argv[1], "dumpavg"))
         return dumpavg(argv[2], argv[3], std::atoi(argv[4]), argc > 5 ? std::atoi(argv[5]) : 0);
     if (argc >= 5 && !std::strcmp(argv[1], "bench"))
-        return bench(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), argc > 5 ? std::atoi(argv[5]) : 0);
+        return bench(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), argc > 5 ? std::atoi(argv[5]) : 0,
+                     argc > 6 ? argv[6] : "refdriver_bench.png");
     std::fprintf(stderr, "usage: refdriver dump <scene.xml> <out.bin> [camera] | bench <scene.xml> <threads> <reps> [camera]\n");
     return 2;
 }

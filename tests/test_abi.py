@@ -37,12 +37,12 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert rtgpu.lib().rtg_abi_version() == 2
+    assert rtgpu.lib().rtg_abi_version() == 3
 
 
 def test_struct_layouts_are_plain_c():
     # the opts/stats structs Python mirrors must match the header's sizes
-    assert ctypes.sizeof(rtgpu.RenderOpts) == 32
+    assert ctypes.sizeof(rtgpu.RenderOpts) == 40
     assert ctypes.sizeof(rtgpu.Stats) == 80
 
 
