@@ -104,6 +104,9 @@ struct rtg_scene {
     DevBuf<rtg::DevDirLight> dir_lights;
     DevBuf<rtg::DevSpotLight> spot_lights;
     DevBuf<rtg::DevCounters> counters;
+    DevBuf<rtg::WNode> wnodes;
+    DevBuf<int2> node_up;
+    DevBuf<int> face_leaf;
     DevBuf<int> perm;
     DevBuf<float> grad;
     bool wave_ok = false;             // scene renders on the wavefront pipeline
@@ -264,6 +267,68 @@ static int build_bvh_on_device(rtg_scene* sc, const rtg_scene_desc* d, bool anyU
     for (int m = 0; m < d->num_meshes; ++m)
         for (int k = 0; k < d->meshes[m].face_count; ++k) facePerm[d->meshes[m].face_offset + k] += d->meshes[m].face_offset;
     return RTG_OK;
+}
+
+// Any-hit wide BVH (rtg_device.hpp WNode, rtg_common.hpp trace_any_wide): each mesh's
+// reference BVH (pre-order records with skip links, as uploaded) collapsed to 4-wide nodes.
+// A wide node's children are found by opening, from {left, right}, the inner child of largest
+// surface area until four remain (the collapse of Ylitie et al., HPG 2017, without a re-build):
+// every slot is a reference node with its box copied bit for bit, and the leaves are the
+// reference's leaves -- what the exactness argument of trace_any_wide needs.  Returns the root.
+static int build_wide(const std::vector<float4>& nodes, int root, std::vector<rtg::WNode>& out) {
+    auto leafv = [&](int i) { int l; std::memcpy(&l, &nodes[2 * i + 1].w, 4); return l; };
+    auto skipv = [&](int i) { int k; std::memcpy(&k, &nodes[2 * i + 1].z, 4); return k; };
+    auto area = [&](int i) {
+        const float4 a = nodes[2 * i], b = nodes[2 * i + 1];
+        const double dx = (double)a.w - a.x, dy = (double)b.x - a.y, dz = (double)b.y - a.z;
+        return dx * dy + dy * dz + dz * dx;
+    };
+    struct Job { int ref, slot_owner, slot; };
+    std::vector<Job> jobs{{root, -1, 0}};
+    int rootIdx = -1;
+    while (!jobs.empty()) {
+        const Job j = jobs.back();
+        jobs.pop_back();
+        std::vector<int> C;
+        if (leafv(j.ref) >= 0) C.push_back(j.ref);
+        else { C.push_back(j.ref + 1); C.push_back(skipv(j.ref + 1)); }
+        while (C.size() < 4) {
+            int best = -1;
+            double ba = -1.0;
+            for (size_t k = 0; k < C.size(); ++k)
+                if (leafv(C[k]) < 0 && area(C[k]) > ba) { ba = area(C[k]); best = (int)k; }
+            if (best < 0) break;
+            const int x = C[best];
+            C[best] = x + 1;
+            C.insert(C.begin() + best + 1, skipv(x + 1));
+        }
+        const int w = (int)out.size();
+        out.emplace_back();
+        rtg::WNode& W = out.back();
+        float* lo[3] = {&W.lox.x, &W.loy.x, &W.loz.x};
+        float* hi[3] = {&W.hix.x, &W.hiy.x, &W.hiz.x};
+        int* ch = &W.child.x;
+        int* lf = &W.leaf.x;
+        for (int k = 0; k < 4; ++k) {
+            if (k >= (int)C.size()) {
+                for (int a = 0; a < 3; ++a) { lo[a][k] = INFINITY; hi[a][k] = -INFINITY; }
+                ch[k] = rtg::WCHILD_EMPTY;
+                lf[k] = 0;
+                continue;
+            }
+            const float4 a = nodes[2 * C[k]], b = nodes[2 * C[k] + 1];
+            lo[0][k] = a.x; lo[1][k] = a.y; lo[2][k] = a.z;
+            hi[0][k] = a.w; hi[1][k] = b.x; hi[2][k] = b.y;
+            const int l = leafv(C[k]);
+            ch[k] = l >= 0 ? -2 - C[k] : rtg::WCHILD_EMPTY;
+            lf[k] = l >= 0 ? l : 0;
+        }
+        if (j.slot_owner >= 0) (&out[j.slot_owner].child.x)[j.slot] = w;
+        else rootIdx = w;
+        for (int k = (int)C.size() - 1; k >= 0; --k)
+            if (leafv(C[k]) < 0) jobs.push_back({C[k], w, k});
+    }
+    return rootIdx;
 }
 
 int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
@@ -433,6 +498,50 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
         else if (o.kind == RTG_OBJ_INSTANCE) feat |= rtg::FEAT_INSTANCE;
         else if (!ident || (o.flags & RTG_OBJF_MOTION_BLUR)) feat |= rtg::FEAT_XFORM;
     }
+    // shadow-ray acceleration (rtg_common.hpp): parent links + face -> leaf for the walk from
+    // the origin's leaf (trace_any_up), and the any-hit wide BVH (trace_any_wide, A/B builds).
+    // RTG_NO_FAST_SHADOW=1: shadow rays walk the reference BVH top-down.
+    std::vector<rtg::WNode> wide;
+    std::vector<int2> nodeUp;
+    std::vector<int> faceLeaf;
+    for (int i = 0; i < d->num_objects; ++i) objs[i].wroot = -1;
+    if (!std::getenv("RTG_NO_FAST_SHADOW") && d->num_meshes > 0 && (RTG_SHADOW_MODE == 2 || RTG_SHADOW_MODE == 3)) {
+        std::vector<float4> dn;
+        std::vector<int2> dx;
+        if (gpuBuild) {
+            dn.resize(2 * (size_t)sc->node_count);
+            HIP_TRY(hipMemcpy(dn.data(), sc->nodes.p, dn.size() * sizeof(float4), hipMemcpyDeviceToHost));
+            dx.resize((size_t)sc->node_count);
+            HIP_TRY(hipMemcpy(dx.data(), sc->node_ext.p, dx.size() * sizeof(int2), hipMemcpyDeviceToHost));
+        }
+        const std::vector<float4>& nd = gpuBuild ? dn : nodes;
+        const std::vector<int2>& nx = gpuBuild ? dx : next;
+        auto leafv = [&](int i) { int l; std::memcpy(&l, &nd[2 * i + 1].w, 4); return l; };
+        auto skipv = [&](int i) { int k; std::memcpy(&k, &nd[2 * i + 1].z, 4); return k; };
+        const size_t nn = nd.size() / 2;
+        nodeUp.assign(nn, make_int2(-1, -1));
+        faceLeaf.assign((size_t)d->num_faces, -1);
+        std::vector<int> wroot(d->num_meshes, -1);
+        for (int m = 0; m < d->num_meshes; ++m) {
+            for (int p = meshBegin[m]; p < meshEnd[m]; ++p) {
+                const int l = leafv(p);
+                if (l < 0) {
+                    const int2 up = make_int2(p, skipv(p));
+                    nodeUp[p + 1] = up;
+                    nodeUp[skipv(p + 1)] = up;
+                } else {
+                    int first = l >> 8, cnt = l & 255;
+                    if (l == rtg::LEAF_EXT) { first = nx[p].x; cnt = nx[p].y; }
+                    for (int f = first; f < first + cnt; ++f) faceLeaf[f] = p;
+                }
+            }
+#if RTG_SHADOW_MODE == 3
+            if (meshEnd[m] > meshBegin[m]) wroot[m] = build_wide(nd, meshBegin[m], wide);
+#endif
+        }
+        for (int i = 0; i < d->num_objects; ++i)
+            objs[i].wroot = d->objects[i].kind != RTG_OBJ_SPHERE ? wroot[d->objects[i].mesh] : -1;
+    }
     // instance groups: runs of consecutive instances without motion blur, chunked by ~sqrt of
     // the run length, with the exact (min/max) union of the members' world boxes
     std::vector<float4> gbox(2 * (size_t)d->num_objects, make_float4(0.f, 0.f, 0.f, 0.f));
@@ -599,6 +708,9 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     HIP_TRY(sc->point_lights.upload(pls)); HIP_TRY(sc->area_lights.upload(als)); HIP_TRY(sc->dir_lights.upload(dls));
     HIP_TRY(sc->spot_lights.upload(sls)); HIP_TRY(sc->env_images.upload(envs));
     HIP_TRY(sc->mesh_lights.upload(mls)); HIP_TRY(sc->light_faces.upload(lfs));
+    HIP_TRY(sc->wnodes.upload(wide));
+    HIP_TRY(sc->node_up.upload(nodeUp));
+    HIP_TRY(sc->face_leaf.upload(faceLeaf));
     std::vector<rtg::DevCounters> zero(1);
     std::memset(zero.data(), 0, sizeof(rtg::DevCounters));
     HIP_TRY(sc->counters.upload(zero));
@@ -630,6 +742,9 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     S.ambient[0] = d->ambient_light.x; S.ambient[1] = d->ambient_light.y; S.ambient[2] = d->ambient_light.z;
     for (int k = 0; k < 3; ++k) S.background[k] = d->background[k];
     S.coop = (sc->feat & rtg::FEAT_BIGLEAF) ? 1 : 0;
+    S.wnodes = wide.empty() ? nullptr : sc->wnodes.p;
+    S.node_up = nodeUp.empty() ? nullptr : sc->node_up.p;
+    S.face_leaf = faceLeaf.empty() ? nullptr : sc->face_leaf.p;
     HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&sc->done, hipEventDisableTiming));
     HIP_TRY(hipDeviceSynchronize());
@@ -807,6 +922,9 @@ static int ensure_wave(rtg_scene* s, size_t pixels, int slots, size_t tiles) {
 static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& C, const rtg::RenderParams& P,
                   float* d_hdr, uint8_t* d_ldr, float* d_accum, hipStream_t stream) {
     const bool stats = (o->flags & RTG_RENDER_COUNT_STATS) != 0;
+    // RTG_RENDER_EXACT_SHADOW: shadow rays walk the reference BVH (cross-checks of the wide one)
+    rtg::DevScene ds = s->ds;
+    if (o->flags & RTG_RENDER_EXACT_SHADOW) ds.exact_shadow = 1;
     hipEvent_t* ev = nullptr;
     if (o->flags & RTG_RENDER_TIMING) {
         for (auto& e : s->ev)
@@ -827,7 +945,7 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
             if (rc) return rc;
             acc = s->wave.accum;
         }
-        HIP_TRY(rtg::launch_tree(s->tree, s->ds, C, P, d_hdr, d_ldr, acc, s->counters.p, stats, s->feat, stream, ev));
+        HIP_TRY(rtg::launch_tree(s->tree, ds, C, P, d_hdr, d_ldr, acc, s->counters.p, stats, s->feat, stream, ev));
         if (ev) s->timed_stages = rtg::TREE_STAGES;
         return RTG_OK;
     }
@@ -847,11 +965,11 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
                 W.num_slots = s->num_slots;
             }
         }
-        HIP_TRY(rtg::launch_wave(s->ds, C, P, W, d_hdr, d_ldr, s->counters.p, stats, s->feat, stream, ev));
+        HIP_TRY(rtg::launch_wave(ds, C, P, W, d_hdr, d_ldr, s->counters.p, stats, s->feat, stream, ev));
         if (ev) s->timed_stages = rtg::WAVE_STAGES;
         return RTG_OK;
     }
-    HIP_TRY(rtg::launch_mega(s->ds, C, P, d_hdr, d_ldr, d_accum, s->counters.p, stats, stream, ev));
+    HIP_TRY(rtg::launch_mega(ds, C, P, d_hdr, d_ldr, d_accum, s->counters.p, stats, stream, ev));
     if (ev) s->timed_stages = rtg::MEGA_STAGES;
     return RTG_OK;
 }
@@ -1059,6 +1177,8 @@ int rtg_scene_stats(rtg_scene* s, rtg_stats* out) {
         out->object_tests += c.object_tests;
         out->shadow_node_visits += c.shadow_node_visits;
         out->shadow_tri_tests += c.shadow_tri_tests;
+        out->shadow_wide_visits += c.shadow_wide_visits;
+        out->shadow_fallbacks += c.shadow_fallbacks;
     }
     return RTG_OK;
 }

@@ -123,9 +123,14 @@ template <bool STATS> struct Cnt {
     template <bool ANY> DEV void tri_n(uint32_t) {}
     DEV void sph() {} DEV void obj() {}
     DEV void cam() {} DEV void sec() {} DEV void shd() {}
+    DEV void wnode() {}
+    DEV void fallback() {}
 };
 template <> struct Cnt<true> {
-    uint32_t nodes = 0, tris = 0, sphs = 0, objs = 0, cams = 0, secs = 0, shds = 0, snodes = 0, stris = 0;
+    uint32_t nodes = 0, tris = 0, sphs = 0, objs = 0, cams = 0, secs = 0, shds = 0, snodes = 0, stris = 0, wnodes = 0,
+             fallbacks = 0;
+    DEV void wnode() { ++wnodes; }
+    DEV void fallback() { ++fallbacks; }
     template <bool ANY> DEV void node() { if (ANY) ++snodes; else ++nodes; }
     template <bool ANY> DEV void tri() { if (ANY) ++stris; else ++tris; }
     template <bool ANY> DEV void tri_n(uint32_t n) { if (ANY) stris += n; else tris += n; }
@@ -482,6 +487,94 @@ DEV bool walk_bvh(const DevScene& S, int i, const int end, const Ray& r, float& 
     return hit;
 }
 
+// Packet form of walk_bvh_seq for coherent rays (a wave's 8x8 pixel tile of camera rays,
+// or the tile's shadow rays towards one light): the wave walks ONE pre-order node sequence,
+// the union of its lanes' walks, with a wave-uniform node index -- node and triangle records
+// are scalar loads (one per wave, through the scalar cache, no per-lane addresses for the
+// texture path) -- and every lane keeps its own walk exactly: a lane whose box test fails at
+// node n sets resume = skip(n) and sits out until the wave reaches resume, i.e. it ignores
+// n's subtree [n, skip(n)) precisely as its own stackless walk would.  Each lane therefore
+// tests the same boxes and faces, in the same order, with the same minT, as walk_bvh_seq --
+// same hits, same ties, same counters -- and the wave only adds masked-off idle lanes.
+// The wave advances to i + 1 when some active lane enters node i's subtree, else to skip(i);
+// if no lane is active at i (ANY lanes that finished), it jumps to the lanes' minimum resume.
+DEV int wave_min_int(int v) {
+    for (int m = 1; m < 64; m <<= 1) {
+        const int o = __shfl_xor(v, m);
+        v = o < v ? o : v;
+    }
+    return v;
+}
+
+template <bool ANY, bool STATS>
+DEV bool walk_bvh_packet(const DevScene& S, const int begin, const int end, const Ray& r, float& minT, int& hitFace,
+                         float limit, Cnt<STATS>& c) {
+    bool hit = false;
+    const RayRcp q = ray_rcp(r);
+    const int kDone = 0x7FFFFFFF;
+    int resume = begin;                              // per lane: first node it takes part in again
+    int i = begin;                                   // wave-uniform
+    while (i < end) {
+        bool act = resume <= i;
+        if (!__ballot(act)) {                        // only after ANY lanes finished
+            const int all = __ballot(1) == ~0ull ? wave_min_int(resume) : [&] {
+                int m = kDone;
+                uint64_t em = __ballot(1);
+                while (em) {
+                    const int l = __ffsll((long long)em) - 1;
+                    em &= em - 1;
+                    const int v = __shfl(resume, l);
+                    m = v < m ? v : m;
+                }
+                return m;
+            }();
+            i = __builtin_amdgcn_readfirstlane(all);
+            continue;
+        }
+        i = __builtin_amdgcn_readfirstlane(i);
+        const float4 a = S.nodes[2 * i];
+        const float4 b = S.nodes[2 * i + 1];
+        const int skip = __float_as_int(b.z);
+        const int leaf = __float_as_int(b.w);
+        bool pass = false;
+        if (act) {
+            c.template node<ANY>();
+            pass = box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, r, q, minT);
+            if (!pass) resume = skip;
+        }
+        const bool any = __ballot(pass) != 0;
+        if (leaf >= 0) {
+            if (any) {
+                int first = leaf >> 8, cnt = leaf & 255;
+                if (leaf == LEAF_EXT) {
+                    const int2 e = S.node_ext[i];
+                    first = e.x;
+                    cnt = e.y;
+                }
+                for (int f = first; f < first + cnt; ++f) {
+                    if (pass) {
+                        c.template tri<ANY>();
+                        float t;
+                        if (tri_test_fast(S, f, r, minT, t)) {
+                            minT = t;
+                            hitFace = f;
+                            hit = true;
+                            if (ANY && t < limit) {
+                                pass = false;
+                                resume = kDone;
+                            }
+                        }
+                    }
+                }
+            }
+            i = skip;
+        } else {
+            i = any ? i + 1 : skip;
+        }
+    }
+    return hit;
+}
+
 // Sphere::Intersect (sphere.cpp:13-78): root selection and acceptance; lo/ld local ray.
 DEV bool sphere_t(const DevObject& ob, const Ray& lr, float minT, float& tout) {
     const f3 center = mk(ob.center[0], ob.center[1], ob.center[2]);
@@ -533,7 +626,7 @@ struct Hit {
 // bbox test fails leaves its offset on the ray origin (instancedMesh.cpp:18-60).
 // FEAT (scene features the caller guarantees absent when the bit is clear) lets the
 // traversal kernels drop whole code paths -- and their registers -- for plain scenes.
-template <bool ANY, bool STATS, int FEAT = FEAT_ALL>
+template <bool ANY, bool STATS, int FEAT = FEAT_ALL, bool PK = false>
 DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit, Hit& h, Cnt<STATS>& c) {
     h.t = minT;
     h.obj = -1;
@@ -541,19 +634,30 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
     // instance world-bbox tests: the division-free slab test (same decisions, box_hit_fast);
     // the motion-blur quirk moves r.o between objects, never r.d
     const RayRcp rq = (FEAT & FEAT_INSTANCE) ? ray_rcp(r) : RayRcp{};
+    int gskip = 0;                   // packet walks: this lane skips objects below gskip
     for (int k = 0; k < S.num_objects; ++k) {
         const DevObject& ob = S.objects[k];
         // Instance groups (runs of consecutive instances without motion blur): every member's
         // world box lies inside the group's, and the slab test is monotone in the box and in
         // minT, so a group box that fails at the current minT fails for every member tested
         // after it -- the members can be skipped with the same result.
+        // Packet walks keep the object index wave-uniform (walk_bvh_packet needs one node
+        // range per wave): a lane whose group box fails sits the group out, and the wave
+        // jumps over it when every lane does.
         if ((FEAT & FEAT_INSTANCE) && ob.group_end > k) {
             const float4 ga = S.group_box[2 * k], gb = S.group_box[2 * k + 1];
-            if (!box_hit_fast(ga.x, ga.y, ga.z, gb.x, gb.y, gb.z, r, rq, h.t)) {
+            if constexpr (PK) {
+                if (k >= gskip && !box_hit_fast(ga.x, ga.y, ga.z, gb.x, gb.y, gb.z, r, rq, h.t)) gskip = ob.group_end;
+                if (!__ballot(k >= gskip)) {
+                    k = ob.group_end - 1;
+                    continue;
+                }
+            } else if (!box_hit_fast(ga.x, ga.y, ga.z, gb.x, gb.y, gb.z, r, rq, h.t)) {
                 k = ob.group_end - 1;
                 continue;
             }
         }
+        if (PK && k < gskip) continue;
         c.obj();
         if ((FEAT & FEAT_SPHERE) && ob.kind == OBJ_SPHERE) {
             c.sph();
@@ -579,12 +683,297 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
         Ray lr = (FEAT & FEAT_XFORM) ? trav_ray(ob, r, mbTime) : r;
         int face = -1;
         float t = h.t;
-        if (walk_bvh<ANY, STATS, (FEAT & FEAT_BIGLEAF) != 0>(S, ob.node_begin, ob.node_end, lr, t, face, limit, c)) {
+        bool found;
+        if constexpr (PK) found = walk_bvh_packet<ANY, STATS>(S, ob.node_begin, ob.node_end, lr, t, face, limit, c);
+        else found = walk_bvh<ANY, STATS, (FEAT & FEAT_BIGLEAF) != 0>(S, ob.node_begin, ob.node_end, lr, t, face, limit, c);
+        if (found) {
             h.t = t; h.obj = k; h.face = face; h.o = r.o;
             if (ANY && t < limit) return true;
         }
     }
     return !ANY && h.obj >= 0;
+}
+
+// ---------------------------------------------------------------------------
+// Shadow rays on the any-hit wide BVH (WNode, rtg_device.hpp)
+// ---------------------------------------------------------------------------
+// CastShadowRay (raytracer.cpp:585-623) answers one boolean: with minT0 = the initial minT
+// (lightT + 0.01, or inf) and limit = lightT, the reference walks the objects in order,
+// each with its BVH in its own order, minT shrinking to every accepted hit, and answers
+// true once a hit with t < limit is found.  Until then minT_cur lies in [limit, minT0].
+// For a face f of reference leaf L (box B_L), with tri_ok(f) = "IntersectFace accepts f
+// with 0 < t < limit" (its early outs do not depend on minT):
+//   * sufficient: tri_ok(f) and slab(B_L, limit) [and, for an instance, its world box at
+//     limit].  Every ancestor box of L contains B_L (unions of face boxes, exact min/max),
+//     and the slab test is monotone in the box and in minT, so every box on L's path
+//     passes at any minT_cur >= limit, and f is accepted with t < limit <= minT_cur;
+//   * necessary: some f with tri_ok(f) and slab(B_L, minT0) (same monotonicity).
+// The wide walk visits every leaf whose box passes at minT0 (each wide child box contains
+// the leaf boxes below it; the child test is conservative), in any order, and answers 1 at
+// the first face meeting the sufficient condition.  A face meeting only the necessary one
+// (its leaf box entry within rounding of lightT -- a light lying on a surface) or a full
+// traversal stack make the answer "undecided" (-1): the caller then runs the reference
+// walk for that ray.  0: no face meets the necessary condition -- not in shadow.
+#ifndef RTG_WIDE_STACK
+#define RTG_WIDE_STACK 24
+#endif
+// k_shadow<FAST> (the wide walk + the in-place reference fallback) compiled for this many
+// waves per SIMD (the 24-KB LDS stack allows six); instance scenes keep RTG_INST_WAVES
+#ifndef RTG_WIDE_WAVES_PLAIN
+#define RTG_WIDE_WAVES_PLAIN 6
+#endif
+#define RTG_WIDE_WAVES(FEAT) (((FEAT) & FEAT_INSTANCE) ? RTG_INST_WAVES : RTG_WIDE_WAVES_PLAIN)
+
+
+// Conservative slab test: accepts every box the exact test (box_hit) accepts at minT.  The
+// fast slab distances (m - o) * rcp(d) are within 2^-22 |t| of the exact quotients (RayRcp,
+// q.fast), so exact tmax > 0, tmax >= tmin, tmin < minT imply the tests below on the fast
+// values (minTc = minT (1 + 2^-21); the 1e-30 terms cover subnormal products).  (An fma form
+// m * rcp - o * rcp saves six instructions but its error scales with |o * rcp|, which loosens
+// the test badly for rays with a small direction component: measured 2x slower.)
+struct SlabRay {
+    f3 o;
+    float ix, iy, iz;
+};
+DEV SlabRay slab_ray(const Ray& r, const RayRcp& q) {
+    SlabRay s;
+    s.o = r.o;
+    s.ix = q.ix; s.iy = q.iy; s.iz = q.iz;
+    return s;
+}
+DEV bool slab_cons(float lx, float ly, float lz, float hx, float hy, float hz, const SlabRay& s, float minTc,
+                   float& tnear) {
+    const float tx1 = (lx - s.o.x) * s.ix, tx2 = (hx - s.o.x) * s.ix;
+    const float ty1 = (ly - s.o.y) * s.iy, ty2 = (hy - s.o.y) * s.iy;
+    const float tz1 = (lz - s.o.z) * s.iz, tz2 = (hz - s.o.z) * s.iz;
+    const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+    const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+    tnear = tmin;
+    return (tmax > -1e-30f) & (tmax >= tmin * (1.0f - 0x1p-21f) - 1e-30f) & (tmin < minTc);
+}
+
+// One mesh's wide BVH (local ray lr).  inst_conf: the instance's world box passes at limit
+// (true for plain meshes).  Returns 1 / 0 / -1 as above.  A node's leaf children are tested
+// in place (all lanes stay in step: a separate iteration per leaf measured 2x slower), then
+// the nearest hit inner child is the next node and the others go onto the stack.
+template <bool STATS>
+DEV int walk_wide_any(const DevScene& S, int node, const Ray& lr, float minT0, float limit, bool inst_conf,
+                      Cnt<STATS>& c) {
+    __shared__ int stack[RTG_WIDE_STACK][256];
+    const RayRcp q = ray_rcp(lr);
+    if (!q.fast) return -1;                          // zero / tiny direction component: reference walk
+    const float minTc = minT0 * (1.0f + 0x1p-21f);
+    const SlabRay sr = slab_ray(lr, q);
+    const int tid = threadIdx.x;
+    int sp = 0;
+    bool undecided = false;
+    while (true) {
+        const WNode* N = S.wnodes + node;
+        const float4 lox = N->lox, hix = N->hix, loy = N->loy, hiy = N->hiy, loz = N->loz, hiz = N->hiz;
+        const int4 ch = N->child, lf = N->leaf;
+        c.wnode();
+        float tn[4];
+        bool h[4];
+        h[0] = slab_cons(lox.x, loy.x, loz.x, hix.x, hiy.x, hiz.x, sr, minTc, tn[0]) & (ch.x != WCHILD_EMPTY);
+        h[1] = slab_cons(lox.y, loy.y, loz.y, hix.y, hiy.y, hiz.y, sr, minTc, tn[1]) & (ch.y != WCHILD_EMPTY);
+        h[2] = slab_cons(lox.z, loy.z, loz.z, hix.z, hiy.z, hiz.z, sr, minTc, tn[2]) & (ch.z != WCHILD_EMPTY);
+        h[3] = slab_cons(lox.w, loy.w, loz.w, hix.w, hiy.w, hiz.w, sr, minTc, tn[3]) & (ch.w != WCHILD_EMPTY);
+        const int cidx[4] = {ch.x, ch.y, ch.z, ch.w};
+        const int lidx[4] = {lf.x, lf.y, lf.z, lf.w};
+        int next = -1;
+        float nextT = INFINITY;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (!h[k]) continue;
+            const int cr = cidx[k];
+            if (cr >= 0) {
+                int spill = cr;
+                if (tn[k] < nextT) {
+                    spill = next;
+                    next = cr;
+                    nextT = tn[k];
+                }
+                if (spill >= 0) {
+                    if (sp < RTG_WIDE_STACK) stack[sp++][tid] = spill;
+                    else undecided = true;
+                }
+                continue;
+            }
+            const int ref = -2 - cr;
+            int first = lidx[k] >> 8, cnt = lidx[k] & 255;
+            if (lidx[k] == LEAF_EXT) {
+                const int2 e = S.node_ext[ref];
+                first = e.x;
+                cnt = e.y;
+            }
+            for (int f = first; f < first + cnt; ++f) {
+                c.template tri<true>();
+                float t;
+                if (!tri_test_fast(S, f, lr, limit, t)) continue;
+                // exact decisions on the leaf's own (reference) box
+                const float4 a = S.nodes[2 * ref], b = S.nodes[2 * ref + 1];
+                if (!box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, minT0)) break;   // leaf unreachable
+                if (inst_conf && box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, limit)) return 1;
+                undecided = true;
+            }
+        }
+        if (next >= 0) {
+            node = next;
+            continue;
+        }
+        if (sp == 0) break;
+        node = stack[--sp][tid];
+    }
+    return undecided ? -1 : 0;
+}
+
+// CastShadowRay on the wide BVH: objects in any order (the answer is a boolean), spheres
+// exactly (a sphere hit with t < limit is accepted at any minT_cur >= limit, one with
+// t >= limit never decides).  Returns 1 / 0 / -1 (undecided: run trace<true>).
+template <bool STATS, int FEAT>
+DEV int trace_any_wide(const DevScene& S, const Ray& r, float minT0, float limit, Cnt<STATS>& c) {
+    const RayRcp rq = (FEAT & FEAT_INSTANCE) ? ray_rcp(r) : RayRcp{};
+    if ((FEAT & FEAT_INSTANCE) && !rq.fast) return -1;
+    bool undecided = false;
+    for (int k = 0; k < S.num_objects; ++k) {
+        const DevObject& ob = S.objects[k];
+        if ((FEAT & FEAT_INSTANCE) && ob.group_end > k) {
+            const float4 ga = S.group_box[2 * k], gb = S.group_box[2 * k + 1];
+            if (!box_hit_fast(ga.x, ga.y, ga.z, gb.x, gb.y, gb.z, r, rq, minT0)) {
+                k = ob.group_end - 1;
+                continue;
+            }
+        }
+        c.obj();
+        if ((FEAT & FEAT_SPHERE) && ob.kind == OBJ_SPHERE) {
+            c.sph();
+            Ray lr = trav_ray(ob, r, 0.f);
+            float t;
+            if (sphere_t(ob, lr, limit, t)) return 1;
+            continue;
+        }
+        if (ob.flags & OBJF_SHADOW_SKIP) continue;
+        bool conf = true;
+        if ((FEAT & FEAT_INSTANCE) && ob.kind == OBJ_INSTANCE) {
+            if (!box_hit_fast(ob.bmin[0], ob.bmin[1], ob.bmin[2], ob.bmax[0], ob.bmax[1], ob.bmax[2], r, rq, minT0))
+                continue;
+            conf = box_hit_fast(ob.bmin[0], ob.bmin[1], ob.bmin[2], ob.bmax[0], ob.bmax[1], ob.bmax[2], r, rq, limit);
+        }
+        const Ray lr = (FEAT & FEAT_XFORM) ? trav_ray(ob, r, 0.f) : r;
+        const int res = walk_wide_any<STATS>(S, ob.wroot, lr, minT0, limit, conf, c);
+        if (res > 0) return 1;
+        undecided |= res < 0;
+    }
+    return undecided ? -1 : 0;
+}
+
+// The same decision on the reference BVH itself, walked from the shadow ray's origin
+// upwards.  A shadow ray starts on the surface it leaves (hit point + eps n), so top-down
+// every ancestor of the origin's leaf is hit and both children are tested at every level;
+// starting at the origin's leaf L0 (the leaf of the hit face) and climbing, only the
+// sibling subtree of each ancestor is walked -- the path boxes are not tested at all (taken
+// as hit: a superset, which the necessary condition allows), nearby subtrees come first
+// (early exit), and L0 plus the siblings' subtrees cover the whole tree whatever L0 is.
+// Boxes are tested conservatively at minT0 (slab_cons); the exact decisions on a leaf's box
+// (at minT0: necessary, at limit: sufficient) are taken only for a face with tri_ok.
+// One mesh (node range [begin, end), local ray lr): from leaf `start` upwards when the ray
+// leaves this object (start >= 0), else top-down.  node_up[i] = (parent, parent's skip).
+// One flat loop (a node visit or a climb per iteration) keeps the wave's lanes in step.
+template <bool STATS>
+DEV int walk_any_up(const DevScene& S, const int begin, const int end, const int start, const Ray& lr,
+                    float minT0, float limit, bool conf, bool& undecided, Cnt<STATS>& c) {
+    const RayRcp q = ray_rcp(lr);
+    if (!q.fast) {                                   // zero / tiny direction component: reference walk
+        undecided = true;
+        return 0;
+    }
+    const float minTc = minT0 * (1.0f + 0x1p-21f);
+    const SlabRay sr = slab_ray(lr, q);
+    const bool up = start >= begin && start < end;
+    int i = up ? start : begin, e = up ? start + 1 : end;   // node range being walked
+    int cur = up ? start : begin, cur_end = up ? start + 1 : end;   // top of the climbed path
+    while (true) {
+        if (i >= e) {
+            if (cur == begin) break;
+            // climb: left child (cur == parent + 1): the right sibling is [cur_end, parent's
+            // end); right child: the left sibling is [parent + 1, cur)
+            const int2 u = S.node_up[cur];
+            const bool left = cur == u.x + 1;
+            i = left ? cur_end : u.x + 1;
+            e = left ? u.y : cur;
+            cur = u.x;
+            cur_end = u.y;
+            continue;
+        }
+        const float4 a = S.nodes[2 * i];
+        const float4 b = S.nodes[2 * i + 1];
+        c.template node<true>();
+        const int skip = __float_as_int(b.z);
+        float tn;
+        const int leaf = __float_as_int(b.w);
+        if (!slab_cons(a.x, a.y, a.z, a.w, b.x, b.y, sr, minTc, tn)) {
+            i = skip;
+            continue;
+        }
+        if (leaf < 0) {
+            i = i + 1;
+            continue;
+        }
+        int first = leaf >> 8, cnt = leaf & 255;
+        if (leaf == LEAF_EXT) {
+            const int2 x = S.node_ext[i];
+            first = x.x;
+            cnt = x.y;
+        }
+        for (int f = first; f < first + cnt; ++f) {
+            c.template tri<true>();
+            float t;
+            if (!tri_test_fast(S, f, lr, limit, t)) continue;
+            if (!box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, minT0)) break;   // leaf unreachable
+            if (conf && box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, limit)) return 1;
+            undecided = true;
+        }
+        i = skip;
+    }
+    return 0;
+}
+
+// CastShadowRay from the hit (object sobj, face sface) it leaves; returns 1 / 0 / -1.
+template <bool STATS, int FEAT>
+DEV int trace_any_up(const DevScene& S, const Ray& r, float minT0, float limit, int sobj, int sface,
+                     Cnt<STATS>& c) {
+    const RayRcp rq = (FEAT & FEAT_INSTANCE) ? ray_rcp(r) : RayRcp{};
+    if ((FEAT & FEAT_INSTANCE) && !rq.fast) return -1;
+    bool undecided = false;
+    for (int k = 0; k < S.num_objects; ++k) {
+        const DevObject& ob = S.objects[k];
+        if ((FEAT & FEAT_INSTANCE) && ob.group_end > k) {
+            const float4 ga = S.group_box[2 * k], gb = S.group_box[2 * k + 1];
+            if (!box_hit_fast(ga.x, ga.y, ga.z, gb.x, gb.y, gb.z, r, rq, minT0)) {
+                k = ob.group_end - 1;
+                continue;
+            }
+        }
+        c.obj();
+        if ((FEAT & FEAT_SPHERE) && ob.kind == OBJ_SPHERE) {
+            c.sph();
+            Ray lr = trav_ray(ob, r, 0.f);
+            float t;
+            if (sphere_t(ob, lr, limit, t)) return 1;
+            continue;
+        }
+        if (ob.flags & OBJF_SHADOW_SKIP) continue;
+        bool conf = true;
+        if ((FEAT & FEAT_INSTANCE) && ob.kind == OBJ_INSTANCE) {
+            if (!box_hit_fast(ob.bmin[0], ob.bmin[1], ob.bmin[2], ob.bmax[0], ob.bmax[1], ob.bmax[2], r, rq, minT0))
+                continue;
+            conf = box_hit_fast(ob.bmin[0], ob.bmin[1], ob.bmin[2], ob.bmax[0], ob.bmax[1], ob.bmax[2], r, rq, limit);
+        }
+        const Ray lr = (FEAT & FEAT_XFORM) ? trav_ray(ob, r, 0.f) : r;
+        const int start = (k == sobj && sface >= 0) ? S.face_leaf[sface] : -1;
+        if (walk_any_up<STATS>(S, ob.node_begin, ob.node_end, start, lr, minT0, limit, conf, undecided, c)) return 1;
+    }
+    return undecided ? -1 : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -1245,8 +1634,9 @@ DEV void tile_pixel(const RenderParams& P, int& px, int& py) {
 template <bool STATS>
 DEV void flush_counters(Cnt<STATS>& cn, DevCounters* counters) {
     if constexpr (STATS) {
-        unsigned long long v[9] = {cn.cams, cn.secs, cn.shds, cn.nodes, cn.tris, cn.sphs, cn.objs, cn.snodes, cn.stris};
-        for (int k = 0; k < 9; ++k) {
+        unsigned long long v[11] = {cn.cams, cn.secs, cn.shds, cn.nodes, cn.tris, cn.sphs, cn.objs, cn.snodes, cn.stris,
+                                    cn.wnodes, cn.fallbacks};
+        for (int k = 0; k < 11; ++k) {
             unsigned long long x = v[k];
             for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
             if ((threadIdx.x & 63) == 0 && x) atomicAdd(&((unsigned long long*)counters)[k], x);
@@ -1255,10 +1645,16 @@ DEV void flush_counters(Cnt<STATS>& cn, DevCounters* counters) {
 }
 
 // Shadow queue in per-block segments (rtg_wave.hip k_shade, rtg_tree.hip k_tree_shade):
-// one thread per queued shadow ray, CastShadowRay as early-exit any-hit (raytracer.cpp:585-623).
-template <bool STATS, int FEAT>
+// one thread per queued shadow ray, CastShadowRay (raytracer.cpp:585-623).
+// FAST (the wavefront pipeline): the RTG_SHADOW_MODE walk, its undecided rays by the
+// reference walk in place (moving them to a second kernel to shed the reference walk's
+// registers measured slower: the extra launch and the wide walk's own ~100 VGPRs); otherwise
+// (the ray-tree pipeline, or RTG_RENDER_EXACT_SHADOW) the reference walk per lane,
+// early-exit any-hit.
 // grid (shade blocks, slots): block (b, c) takes entries [256c, 256c+256) of segment b
-__global__ __launch_bounds__(256, RTG_TRACE_WAVES(FEAT)) void k_shadow(const DevScene S, const WaveBufs W, DevCounters* counters) {
+template <bool STATS, int FEAT, bool FAST>
+__global__ __launch_bounds__(256, FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(FEAT)) void k_shadow(const DevScene S, const WaveBufs W,
+                                                                                            DevCounters* counters) {
     const int k = blockIdx.y * 256 + threadIdx.x;
     const size_t q = ((size_t)blockIdx.x * W.num_slots) * 256 + k;
     Cnt<STATS> cn;
@@ -1267,8 +1663,33 @@ __global__ __launch_bounds__(256, RTG_TRACE_WAVES(FEAT)) void k_shadow(const Dev
         Ray r;
         r.o = mk(o.x, o.y, o.z);
         r.d = mk(d.x, d.y, d.z);
-        Hit h;
-        if (trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn)) W.occ[W.q_slot[q]] = 1;
+        int res = -1;
+        if constexpr (FAST) {
+#if RTG_SHADOW_MODE == 1
+            Hit h;
+            res = trace<true, STATS, FEAT, true>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
+#elif RTG_SHADOW_MODE == 2
+            const int slot = W.q_slot[q];
+            const int src = W.num_slots == 1 ? slot : slot / W.num_slots;
+            const int sobj = W.hit_obj ? W.hit_obj[src] : -1;
+            const int sface = sobj >= 0 ? W.hit_face[src] : -1;
+            res = trace_any_up<STATS, FEAT>(S, r, o.w, d.w, sobj, sface, cn);
+#elif RTG_SHADOW_MODE == 3
+            res = trace_any_wide<STATS, FEAT>(S, r, o.w, d.w, cn);
+#else
+            Hit h;
+            res = trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
+#endif
+            if (res < 0) {                           // undecided: the reference walk
+                cn.fallback();
+                Hit h;
+                res = trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
+            }
+        } else {
+            Hit h;
+            res = trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
+        }
+        if (res > 0) W.occ[W.q_slot[q]] = 1;
     }
     flush_counters<STATS>(cn, counters);
 }

@@ -40,8 +40,33 @@ struct DevObject {
     double baseInvT[12];            // base mesh's inverseTransposeTransform
     int id;                         // Shape::id (XML id; spheres: never a light's id)
     int group_end;                  // first object of an instance group: one past its last member
-    int pad3, pad4;
+    int wroot;                      // (base) mesh's root in the any-hit wide BVH (WNode), -1: none
+    int pad4;
 };
+
+// Any-hit acceleration for shadow rays (CastShadowRay, raytracer.cpp:585-623, is a boolean:
+// order-free).  A 4-wide BVH collapsed from the reference's own BVH: every child slot is a
+// reference node -- its box copied exactly -- and the leaves are the reference's leaves, so
+// each child box contains (exactly: unions of face boxes) every leaf box below it.  128 B,
+// one cache line pair: the four child boxes as SoA float4 rows, then the child references.
+struct WNode {
+    float4 lox, hix, loy, hiy, loz, hiz;
+    int4 child;                     // >= 0: wide node; WCHILD_EMPTY; <= -2: leaf, reference node -2 - child
+    int4 leaf;                      // leaf slots: (first << 8) | count, or LEAF_EXT (node_ext of the reference node)
+};
+enum : int { WCHILD_EMPTY = -1 };
+// Shadow-ray walk of the wavefront pipeline's k_shadow (rtg_common.hpp): 3 = any-hit on the
+// 4-wide BVH (trace_any_wide; undecided rays take the reference walk: default), 0 = the
+// reference walk per lane, 1 = the same walks as a wave packet (walk_bvh_packet), 2 = any-hit
+// climb from the ray's origin leaf (trace_any_up).  The ray-tree pipeline's k_shadow always
+// uses the per-lane reference walk (its secondary rays are incoherent: modes 1-3 measured
+// slower on C5).  Camera rays: RTG_PRIMARY_PACKET (0: per lane, default).  DESIGN.md §5.
+#ifndef RTG_SHADOW_MODE
+#define RTG_SHADOW_MODE 3
+#endif
+#ifndef RTG_PRIMARY_PACKET
+#define RTG_PRIMARY_PACKET 0
+#endif
 
 struct DevMaterial {
     int type, brdf, pad0, pad1;
@@ -134,6 +159,10 @@ struct DevScene {
     float ambient[3];
     int background[3];
     int coop;                        // the scene has large leaves (FEAT_BIGLEAF)
+    const WNode* __restrict__ wnodes;  // any-hit wide BVH (null: shadow rays take the reference walk)
+    const int2* __restrict__ node_up;  // per node: (parent, parent's skip); null: no up-walk
+    const int* __restrict__ face_leaf; // per face: its leaf node
+    int exact_shadow;                  // RTG_RENDER_EXACT_SHADOW: shadow rays take the reference walk
 };
 
 struct DevCamera {
@@ -214,7 +243,7 @@ struct TreeSegs {
 // Per-launch ray/traversal counters (RTG_RENDER_COUNT_STATS).
 struct DevCounters {
     unsigned long long camera_rays, secondary_rays, shadow_rays, node_visits, tri_tests, sphere_tests,
-        object_tests, shadow_node_visits, shadow_tri_tests, pad0;
+        object_tests, shadow_node_visits, shadow_tri_tests, shadow_wide_visits, shadow_fallbacks, pad0;
 };
 
 }  // namespace rtg

@@ -532,7 +532,9 @@ static hipError_t tree_pass(TreeState& T, const DevScene& S, const DevCamera& C,
             W.q_o = T.G.q_o; W.q_d = T.G.q_d; W.q_slot = T.G.q_slot; W.q_count = T.G.q_count;
             W.occ = L.occ;
             W.num_slots = ns;
-            hipLaunchKernelGGL((k_shadow<STATS, FEAT>), dim3(blocks, ns), dim3(256), 0, st, S, W, cnt);
+            W.hit_obj = L.obj;              // the hits the shadow rays leave (their origin leaf)
+            W.hit_face = L.face;
+            hipLaunchKernelGGL((k_shadow<STATS, FEAT, false>), dim3(blocks, ns), dim3(256), 0, st, S, W, cnt);
         }
         hipLaunchKernelGGL(k_tree_scan, dim3(1), dim3(1024), 0, st, T.G.c_count, blocks, T.offs);
         if ((e = hipMemcpyAsync(T.h_total, T.offs + blocks, sizeof(int), hipMemcpyDeviceToHost, st)) != hipSuccess)

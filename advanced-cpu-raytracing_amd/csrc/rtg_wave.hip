@@ -35,7 +35,7 @@ __global__ __launch_bounds__(256, RTG_TRACE_WAVES(FEAT)) void k_primary(const De
         Ray ray = camera_ray(C, px, py, key, mbTime);
         cn.cam();
         Hit h;
-        trace<false, STATS, FEAT>(S, ray, mbTime, INFINITY, INFINITY, h, cn);
+        trace<false, STATS, FEAT, RTG_PRIMARY_PACKET != 0 && !(FEAT & FEAT_BIGLEAF)>(S, ray, mbTime, INFINITY, INFINITY, h, cn);
         const int i = crow * C.width + px;
         W.hit_t[i] = h.t;
         W.hit_obj[i] = h.obj;
@@ -280,8 +280,18 @@ static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const Ren
         if (e5) (void)hipEventRecord(e5[1], st);
         hipLaunchKernelGGL((k_shade<STATS>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
         if (e5) (void)hipEventRecord(e5[2], st);
-        if (nshadow > 0)
-            hipLaunchKernelGGL((k_shadow<STATS, FEAT>), dim3(P.num_tiles, nshadow), dim3(256), 0, st, S, W, cnt);
+        if (nshadow > 0) {
+            // fast any-hit walk (RTG_SHADOW_MODE) unless RTG_RENDER_EXACT_SHADOW asks for the
+            // reference walk
+            const bool fast = (RTG_SHADOW_MODE == 3 ? S.wnodes != nullptr
+                                                    : RTG_SHADOW_MODE == 2 ? S.node_up != nullptr : S.nodes != nullptr) &&
+                              !(FEAT & FEAT_BIGLEAF) && !S.exact_shadow;
+            if (fast) {
+                hipLaunchKernelGGL((k_shadow<STATS, FEAT, true>), dim3(P.num_tiles, nshadow), dim3(256), 0, st, S, W, cnt);
+            } else {
+                hipLaunchKernelGGL((k_shadow<STATS, FEAT, false>), dim3(P.num_tiles, nshadow), dim3(256), 0, st, S, W, cnt);
+            }
+        }
         if (e5) (void)hipEventRecord(e5[3], st);
         hipLaunchKernelGGL(k_resolve, dim3((npix + 255) / 256), dim3(256), 0, st, C, P, s, first, last, W, hdr, l,
                            accum);

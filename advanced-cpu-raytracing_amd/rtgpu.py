@@ -29,6 +29,7 @@ RTG_RENDER_ACCUM_ONLY = 2
 RTG_RENDER_FUSED = 4
 RTG_RENDER_TIMING = 8
 RTG_RENDER_TREE = 16
+RTG_RENDER_EXACT_SHADOW = 32
 RTG_LOAD_DEVICE_BVH = 1
 
 
@@ -60,10 +61,11 @@ class RenderOpts(ctypes.Structure):
 class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "camera_rays", "secondary_rays", "shadow_rays", "node_visits", "tri_tests",
-        "sphere_tests", "object_tests", "shadow_node_visits", "shadow_tri_tests", "pad0")]
+        "sphere_tests", "object_tests", "shadow_node_visits", "shadow_tri_tests", "shadow_wide_visits",
+        "shadow_fallbacks")]
 
     def as_dict(self) -> dict:
-        return {n: int(getattr(self, n)) for n, _ in self._fields_ if n != "pad0"}
+        return {n: int(getattr(self, n)) for n, _ in self._fields_}
 
 
 # every symbol include/rtgpu.h declares

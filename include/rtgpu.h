@@ -291,10 +291,12 @@ enum rtg_render_flags {
                                      wavefront pipeline applies (for cross-checks)     */
     RTG_RENDER_TIMING = 8,        /* record HIP events around every kernel of the
                                      render (last sample pass); see rtg_scene_timings */
-    RTG_RENDER_TREE = 16          /* force the wavefront ray-tree pipeline for scenes with
+    RTG_RENDER_TREE = 16,         /* force the wavefront ray-tree pipeline for scenes with
                                      mirror / conductor / dielectric materials (default:
                                      frames of >= 2^21 pixel-samples; it synchronises the
                                      stream once per tree level)                       */
+    RTG_RENDER_EXACT_SHADOW = 32  /* shadow rays walk the reference BVH instead of the
+                                     any-hit wide BVH (same answers; for cross-checks)  */
 };
 
 typedef struct {
@@ -333,7 +335,10 @@ typedef struct {
     uint64_t object_tests;        /* per-object visits (all rays)                    */
     uint64_t shadow_node_visits;  /* BVH node box tests, shadow rays (early exit)    */
     uint64_t shadow_tri_tests;    /* triangle tests, shadow rays (early exit)        */
-    uint64_t pad0;
+    uint64_t shadow_wide_visits;  /* any-hit wide BVH nodes visited (shadow rays; each
+                                     tests four child boxes; A/B builds only)          */
+    uint64_t shadow_fallbacks;    /* shadow rays the fast any-hit walk left undecided,
+                                     answered by the reference walk                    */
 } rtg_stats;
 
 /* One call per camera, replacing main.cpp:164-185 (threads -> renderThreadMain ->

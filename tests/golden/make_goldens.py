@@ -42,6 +42,16 @@ FIXTURES = {
     "scienceTree": (f"{REF}/scienceTree.xml", 288, 144, "exact", None),
     "scienceTree_diamond": (f"{REF}/scienceTree_diamond.xml", 288, 144, "exact", None),
     "berserker": (f"{REF}/akif_uslu/berserker_smooth.xml", 96, 128, "exact", None),
+    # the rest of the shipped scenes the reference renders.  The akif_uslu scenes
+    # with an empty <TexCoordData /> crash the reference's parser (parser.cpp:279-291), so
+    # that element is removed; car_smooth_fixed's second camera is pinned by a copy whose
+    # first <Camera> is removed (no tonemapper / renderer params to inherit, parser.cpp:1504).
+    "car_smooth": (f"{REF}/akif_uslu/car_smooth_fixed.xml", 256, 192, "exact", None),
+    "car_smooth_front": (f"{REF}/akif_uslu/car_smooth_fixed.xml", 256, 192, "exact", "drop_first_camera"),
+    "low_poly": (f"{REF}/akif_uslu/low_poly_smooth.xml", 192, 192, "exact", None),
+    "ton_roosendaal": (f"{REF}/akif_uslu/ton_Roosendaal_smooth.xml", 216, 216, "exact", [("<TexCoordData />", "")]),
+    "tower": (f"{REF}/akif_uslu/tower_smooth.xml", 108, 192, "exact", [("<TexCoordData />", "")]),
+    "windmill": (f"{REF}/akif_uslu/windmill_smooth.xml", 200, 200, "exact", [("<TexCoordData />", "")]),
     "brdf_lights": ("authored", 200, 150, "exact", None),
     "transforms_textures": ("authored", 200, 150, "exact", None),
     "synth_10k": ("generated", 256, 144, "exact", None),
@@ -579,9 +589,20 @@ def prepare(name, src, w, h, edits):
         gen.with_resolution(dst, dst, w, h)
         return dst
     s = open(src).read()
+    if edits == "drop_first_camera":
+        a = s.index("<Camera ")
+        b = s.index("</Camera>", a) + len("</Camera>")
+        s = s[:a] + s[b:]
+        edits = None
     for a, b in edits or []:
         assert a in s, (name, a)
         s = s.replace(a, b)
+    # PLY assets next to the XML (parser.cpp:1404 opens them relative to the CWD)
+    for ply in sorted(set(re.findall(r'plyFile="([^"]*)"', s))):
+        dst_ply = os.path.join(SCENES, ply)
+        if not os.path.exists(dst_ply):
+            os.makedirs(os.path.dirname(dst_ply) or SCENES, exist_ok=True)
+            shutil.copyfile(os.path.join(os.path.dirname(src), ply), dst_ply)
     s = re.sub(r"<ImageResolution>[^<]*</ImageResolution>", f"<ImageResolution>{w} {h}</ImageResolution>", s)
     with open(dst, "w") as f:
         f.write(s)
