@@ -40,10 +40,23 @@ def test_abi_version():
     assert rtgpu.lib().rtg_abi_version() == 3
 
 
-def test_struct_layouts_are_plain_c():
-    # the opts/stats structs Python mirrors must match the header's sizes
+def test_struct_layouts_are_plain_c(tmp_path):
+    # the opts/stats structs Python mirrors must match the header's sizes (checked against a
+    # C compiler's view of include/rtgpu.h)
+    import shutil
     assert ctypes.sizeof(rtgpu.RenderOpts) == 40
-    assert ctypes.sizeof(rtgpu.Stats) == 80
+    assert ctypes.sizeof(rtgpu.Stats) == 88
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if not cc:
+        pytest.skip("no C compiler")
+    src = tmp_path / "sz.c"
+    src.write_text('#include "rtgpu.h"\n#include <stdio.h>\n#include <stddef.h>\nint main(void){printf("%zu %zu %zu\\n", '
+                   'sizeof(rtg_render_opts), sizeof(rtg_stats), offsetof(rtg_render_opts, part_index));return 0;}\n')
+    exe = tmp_path / "sz"
+    subprocess.run([cc, "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    opts, stats, part = map(int, subprocess.run([str(exe)], capture_output=True, text=True).stdout.split())
+    assert (opts, stats) == (ctypes.sizeof(rtgpu.RenderOpts), ctypes.sizeof(rtgpu.Stats))
+    assert part == rtgpu.RenderOpts.part_index.offset
 
 
 def test_errors_are_codes_not_crashes(tmp_path):
