@@ -107,6 +107,7 @@ struct rtg_scene {
     DevBuf<rtg::WNode> wnodes;
     DevBuf<int2> node_up;
     DevBuf<int> face_leaf;
+    DevBuf<int> guard;                // RTG_GUARD builds: index-violation bits
     DevBuf<int> perm;
     DevBuf<float> grad;
     bool wave_ok = false;             // scene renders on the wavefront pipeline
@@ -138,6 +139,11 @@ struct rtg_scene {
     ~rtg_scene() {
         for (rtg_scene* r : replicas) delete r;
         (void)hipSetDevice(device);
+        if (guard.p) {
+            int bits = 0;
+            if (hipMemcpy(&bits, guard.p, sizeof(int), hipMemcpyDeviceToHost) == hipSuccess && bits)
+                std::fprintf(stderr, "rtgpu guard: index violations, bits 0x%x\n", bits);
+        }
         if (tree) rtg::tree_destroy(tree);
         if (done) (void)hipEventDestroy(done);
         if (stream) (void)hipStreamDestroy(stream);
@@ -743,6 +749,13 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     for (int k = 0; k < 3; ++k) S.background[k] = d->background[k];
     S.coop = (sc->feat & rtg::FEAT_BIGLEAF) ? 1 : 0;
     S.wnodes = wide.empty() ? nullptr : sc->wnodes.p;
+    S.num_faces = (int)d->num_faces;
+    S.num_textures = d->num_textures;
+    S.num_images = d->num_images;
+    S.num_materials = d->num_materials;
+    HIP_TRY(sc->guard.alloc(1));
+    HIP_TRY(hipMemset(sc->guard.p, 0, sizeof(int)));
+    S.guard = sc->guard.p;
     S.node_up = nodeUp.empty() ? nullptr : sc->node_up.p;
     S.face_leaf = faceLeaf.empty() ? nullptr : sc->face_leaf.p;
     HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));

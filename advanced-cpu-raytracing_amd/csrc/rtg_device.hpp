@@ -163,6 +163,9 @@ struct DevScene {
     const int2* __restrict__ node_up;  // per node: (parent, parent's skip); null: no up-walk
     const int* __restrict__ face_leaf; // per face: its leaf node
     int exact_shadow;                  // RTG_RENDER_EXACT_SHADOW: shadow rays take the reference walk
+    // RTG_GUARD builds (fault hunting): table sizes and a violation bit mask (rtg_common.hpp GIDX)
+    int* guard;
+    int num_faces, num_textures, num_images, num_materials;
 };
 
 struct DevCamera {

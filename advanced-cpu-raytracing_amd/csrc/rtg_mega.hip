@@ -164,8 +164,8 @@ DEV bool shade_rest(const DevScene& S, const DevCamera& C, const ShadeCtx& c, f3
 // Shape::id of the object a GI ray hit, when its material is emissive (raytracer.cpp:171-176)
 DEV int emissive_hit_id(const DevScene& S, const Hit& h, bool hit) {
     if (!hit) return -1;
-    const DevObject& o = S.objects[h.obj];
-    return S.materials[o.material].type == 3 ? o.id : -1;
+    const DevObject& o = S.objects[GIDX(S, h.obj, S.num_objects, 4)];
+    return S.materials[GIDX(S, o.material, S.num_materials, 5)].type == 3 ? o.id : -1;
 }
 
 // Shades `cur` (PerformShading, raytracer.cpp:65-134).  Returns true and fills `f`/`ch` if
@@ -174,10 +174,10 @@ DEV int emissive_hit_id(const DevScene& S, const Hit& h, bool hit) {
 template <int MAXD, bool STATS, bool PT>
 DEV bool shade_node(const DevScene& S, const DevCamera& C, const Node& cur, int level, f3& out, FrameT<PT>& f, Child& ch,
                     Cnt<STATS>& cn) {
-    const DevObject& ob = S.objects[cur.h.obj];
+    const DevObject& ob = S.objects[GIDX(S, cur.h.obj, S.num_objects, 6)];
     ShadeCtx c;
     c.ob = &ob;
-    c.mat = &S.materials[ob.material];
+    c.mat = &S.materials[GIDX(S, ob.material, S.num_materials, 7)];
     c.s = surface<STATS>(S, cur.r, cur.mbTime, cur.h, cn);
     const DevMaterial& mat = *c.mat;
     const f3 w_o = makeUnit(sub(cur.eye, c.s.p));
@@ -186,7 +186,7 @@ DEV bool shade_node(const DevScene& S, const DevCamera& C, const Node& cur, int 
         return false;
     }
     if (ob.tex_replace_all >= 0) {
-        out = tex_rgb(S, S.textures[ob.tex_replace_all], c.s.u, c.s.v);
+        out = tex_rgb(S, S.textures[GIDX(S, ob.tex_replace_all, S.num_textures, 8)], c.s.u, c.s.v);
         return false;
     }
     f3 tp = cur.tp;
@@ -272,7 +272,7 @@ DEV f3 render_sample(const DevScene& S, const DevCamera& C, int px, int py, uint
         const bool hit = trace<false, STATS>(S, R, mbTime, INFINITY, INFINITY, cur.h, cn);
         if (pend == 0 && !hit) return miss_color(S, C, px, py, R.d);
         if constexpr (PT) {
-            if (pend == 3) stack[sp - 1].skip = emissive_hit_id(S, cur.h, hit);
+            if (pend == 3) stack[GIDX(S, sp - 1, MAXD, 9)].skip = emissive_hit_id(S, cur.h, hit);
         }
         if (hit) {
             cur.r = R;
@@ -284,9 +284,10 @@ DEV f3 render_sample(const DevScene& S, const DevCamera& C, int px, int py, uint
             cur.tp = rTp;
             // ---- shade; a node with children pushes a frame and continues with its first child
             Child ch;
-            const bool spawn = shade_node<MAXD, STATS, PT>(S, C, cur, sp, value, stack[MAXD > 0 ? sp : 0], ch, cn);
+            const bool spawn = shade_node<MAXD, STATS, PT>(S, C, cur, sp, value,
+                                                           stack[MAXD > 0 ? GIDX(S, sp, MAXD, 10) : 0], ch, cn);
             if (MAXD > 0 && spawn) {
-                const FrameT<PT>& f = stack[sp];
+                const FrameT<PT>& f = stack[GIDX(S, sp, MAXD, 11)];
                 ++sp;
                 cn.sec();
                 R = ch.r;
@@ -304,7 +305,7 @@ DEV f3 render_sample(const DevScene& S, const DevCamera& C, int px, int py, uint
             // a child missed (ComputeMirrorReflection :461-470, dielectric :351-356, :408 --
             // the refracted miss looks the environment up in the reflected direction; a GI
             // ray that misses contributes nothing, :169-189)
-            const FrameT<PT>& f = stack[MAXD > 0 ? sp - 1 : 0];
+            const FrameT<PT>& f = stack[MAXD > 0 ? GIDX(S, sp - 1, MAXD, 12) : 0];
             if (f.kind == FK_MIRROR || f.kind == FK_DIEL) value = env_or_zero(S, f.kind == FK_MIRROR ? R.d : f.reflDir);
             else value = mk(0, 0, 0);
             vHit = false;
@@ -312,14 +313,14 @@ DEV f3 render_sample(const DevScene& S, const DevCamera& C, int px, int py, uint
         // ---- propagate finished values up the stack
         bool descended = false;
         while (MAXD > 0 && sp > 0) {
-            FrameT<PT>& f = stack[sp - 1];
+            FrameT<PT>& f = stack[GIDX(S, sp - 1, MAXD, 13)];
             if constexpr (PT) {
               if (f.kind == FK_GI) {
                 // the GI ray's radiance: Shade(...) * 2 * pi (raytracer.cpp:177-188), then the
                 // rest of PerformShading with colour = 0 + GI
                 ShadeCtx c;
-                c.ob = &S.objects[f.obj];
-                c.mat = &S.materials[f.matIdx];
+                c.ob = &S.objects[GIDX(S, f.obj, S.num_objects, 14)];
+                c.mat = &S.materials[GIDX(S, f.matIdx, S.num_materials, 15)];
                 c.s = f.s;
                 f3 tp = f.tp;
                 f3 gi = mk(0, 0, 0);
@@ -349,7 +350,7 @@ DEV f3 render_sample(const DevScene& S, const DevCamera& C, int px, int py, uint
                 continue;
               }
             }
-            const DevMaterial& pm = S.materials[f.matIdx];
+            const DevMaterial& pm = S.materials[GIDX(S, f.matIdx, S.num_materials, 16)];
             if (f.kind == FK_DIEL && f.stage == 0) {
                 f.refl = (vHit && vMedium > 1.00001f) ? beer(vT, pm.absorption, value) : value;
                 f.stage = 1;
