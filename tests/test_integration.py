@@ -1,0 +1,71 @@
+"""The drop-in behind the reference's own parser and object model:
+integration/_build/dorkrt loads a scene with DorkTracer::Scene::loadFromXml (the reference's
+tinyxml2 parser, parser.cpp:26-577) and flattens the reference's objects into an
+rtg_scene_desc (integration/dork_adapter.cpp).
+
+* CPU: that description equals rtg_host_scene_load_xml's on every fixture scene, field by
+  field (the one tolerated difference: Mesh::surfaceArea, which the reference never
+  initialises, mesh.cpp:7-13 -- both sides sum the face areas, in different orders);
+* GPU: `dorkrt scene.xml` (the reference's CLI flow, main.cpp:132-202, rendering through
+  librtgpu) writes the PNG the library renders, on one device and dealt over replicas.
+
+dorkrt is built where /root/reference exists (__graft_entry__.build()); it travels to the GPU
+box like librtgpu.so.  Without it these tests skip."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SCENES = os.path.join(ROOT, "tests", "golden", "scenes")
+DORKRT = os.path.join(ROOT, "integration", "_build", "dorkrt")
+FIXTURES = sorted(f[:-4] for f in os.listdir(SCENES) if f.endswith(".xml"))
+
+needs_dorkrt = pytest.mark.skipif(not os.path.exists(DORKRT), reason="dorkrt not built (needs /root/reference)")
+
+
+@needs_dorkrt
+@pytest.mark.parametrize("name", FIXTURES)
+def test_adapter_description_equals_loader(name):
+    r = subprocess.run([DORKRT, "--compare", name + ".xml"], cwd=SCENES, capture_output=True, text=True, timeout=300)
+    report = [ln for ln in r.stdout.splitlines() if ln.startswith(("equal", "MISMATCH", "IDENTICAL", "DIFFERENT"))]
+    assert r.returncode == 0 and report[-1] == "IDENTICAL", "\n".join(report)
+
+
+def _stage(tmp_path, name):
+    """A working directory with the scene's assets (PLY paths and inputs/ are relative to the
+    CWD, parser.cpp:107-110,1404) so the outputs land in tmp_path."""
+    for f in os.listdir(SCENES):
+        if not f.endswith(".xml"):
+            os.symlink(os.path.join(SCENES, f), tmp_path / f)
+    src = open(os.path.join(SCENES, name + ".xml")).read()
+    (tmp_path / (name + ".xml")).write_text(src)
+    import re
+    return [os.path.splitext(m)[0] + ".png" for m in re.findall(r"<ImageName>\s*([^<\s]*)\s*</ImageName>", src)]
+
+
+@needs_dorkrt
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["cornell_dielectric", "transforms_textures", "car_smooth", "synth_10k", "c5_dragon"])
+@pytest.mark.parametrize("devices", [None, "0,0"])
+def test_dorkrt_renders_the_library_image(tmp_path, name, devices):
+    from PIL import Image
+
+    import rtgpu
+    pngs = _stage(tmp_path, name)
+    cmd = [DORKRT, name + ".xml"] + (["--devices", devices] if devices else [])
+    r = subprocess.run(cmd, cwd=tmp_path, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "Rendering took" in r.stdout
+    old = os.getcwd()
+    os.chdir(SCENES)
+    try:
+        hs = rtgpu.HostScene(name + ".xml")
+        ds = rtgpu.DeviceScene(hs, 0)
+        for cam, png in enumerate(pngs):
+            got = np.asarray(Image.open(tmp_path / png).convert("RGB"))
+            _, ldr = ds.render(cam)
+            assert np.array_equal(got, ldr), (name, cam)
+    finally:
+        os.chdir(old)
