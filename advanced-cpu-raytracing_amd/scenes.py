@@ -337,6 +337,63 @@ def config_c3(out_dir: str, K: int = 70000, width: int = 1920, height: int = 108
     return _write(out_dir, "c3_blob", xml)
 
 
+def config_c3_ton(out_dir: str, ply_dir: str, width: int = 1920, height: int = 1080, spp: int = 4) -> str:
+    """C3 on a real mesh (SURVEY §8d's stand-in for the missing bunny): the reference's own
+    archive/hw1_inputs/akif_uslu/ton_Roosendaal_smooth scene (62 160-triangle mesh_2.ply plus
+    mesh_1 / mesh_3; camera, materials as shipped, the empty <TexCoordData /> dropped), with its
+    point light replaced by an AreaLight of the same power at the same place, the materials on
+    an OriginalBlinnPhong BRDF, 4 spp, 16:9 at 1920x1080.  `ply_dir` holds the three PLYs
+    (tests/golden/scenes/ton_Roosendaal_smooth_ply); they are linked next to the XML."""
+    os.makedirs(out_dir, exist_ok=True)
+    dst = os.path.join(out_dir, "ton_Roosendaal_smooth_ply")
+    if not os.path.exists(dst):
+        os.symlink(os.path.abspath(ply_dir), dst)
+    aspect = width / height
+    xml = f"""<Scene>
+    <BackgroundColor>25 76 113</BackgroundColor>
+    <ShadowRayEpsilon>1e-3</ShadowRayEpsilon>
+    <Cameras>
+        <Camera id="1">
+            <Position>-3.916900157928467 -16.159503936767578 -1.0512659549713135</Position>
+            <Gaze>0.22766843438148499 0.971221923828125 -0.06996545195579529</Gaze>
+            <Up>-7.450580596923828e-09 0.07185239344835281 0.99741530418396</Up>
+            <NearPlane>{-aspect:.6f} {aspect:.6f} -1.0 1.0</NearPlane>
+            <NearDistance>3</NearDistance>
+            <ImageResolution>{width} {height}</ImageResolution>
+            <ImageName>c3_ton.png</ImageName>
+            <NumSamples>{spp}</NumSamples>
+        </Camera>
+    </Cameras>
+    <Lights>
+        <AmbientLight>0 0 0</AmbientLight>
+        <AreaLight id="1">
+            <Position>-6.154719352722168 -47.027748107910156 16.88732147216797</Position>
+            <Normal>0.07 0.93 -0.36</Normal>
+            <Radiance>5000 5000 5000</Radiance>
+            <Size>10</Size>
+        </AreaLight>
+    </Lights>
+    <BRDFs>
+        <OriginalBlinnPhong id="1">
+            <Exponent>30</Exponent>
+        </OriginalBlinnPhong>
+    </BRDFs>
+    <Materials>
+        <Material id="1" BRDF="1"><AmbientReflectance>1 1 1</AmbientReflectance><DiffuseReflectance>0.800000011920929 0.800000011920929 0.800000011920929</DiffuseReflectance><SpecularReflectance>0.5 0.5 0.5</SpecularReflectance><PhongExponent>1</PhongExponent></Material>
+        <Material id="2" BRDF="1"><AmbientReflectance>1 1 1</AmbientReflectance><DiffuseReflectance>0.8000000715255737 0.3557424247264862 0.04346328601241112</DiffuseReflectance><SpecularReflectance>0.5 0.5 0.5</SpecularReflectance><PhongExponent>1</PhongExponent></Material>
+        <Material id="3" BRDF="1"><AmbientReflectance>1 1 1</AmbientReflectance><DiffuseReflectance>0.8000000715255737 0.3774781823158264 0.04441830515861511</DiffuseReflectance><SpecularReflectance>0.5 0.5 0.5</SpecularReflectance><PhongExponent>1</PhongExponent></Material>
+    </Materials>
+    <VertexData>0 0 0</VertexData>
+    <Objects>
+        <Mesh id="1"><Material>2</Material><Faces plyFile="ton_Roosendaal_smooth_ply/mesh_1.ply" /></Mesh>
+        <Mesh id="2"><Material>1</Material><Faces plyFile="ton_Roosendaal_smooth_ply/mesh_2.ply" /></Mesh>
+        <Mesh id="3"><Material>3</Material><Faces plyFile="ton_Roosendaal_smooth_ply/mesh_3.ply" /></Mesh>
+    </Objects>
+</Scene>
+"""
+    return _write(out_dir, "c3_ton", xml)
+
+
 def octasphere_mesh(level: int, center=(0.0, 0.0, 0.0), radius: float = 1.0, seed: int = 11,
                     bumps: float = 0.2):
     """Displaced sphere from a subdivided octahedron: 8 * 4**level triangles, no pole fans."""

@@ -48,7 +48,7 @@ def parse():
     p.add_argument("--cpu-reps", type=int, default=3)
     p.add_argument("--no-sweep", action="store_true", help="skip the K sweep (rank 0, N=1 only)")
     p.add_argument("--no-extras", action="store_true", help="skip gather / host-frame timings")
-    p.add_argument("--config", default="headline", choices=["headline", "c2", "c3", "c4", "c5"],
+    p.add_argument("--config", default="headline", choices=["headline", "c2", "c3", "c3ton", "c4", "c5"],
                    help="BASELINE.json configuration (c2-c5: one frame = all camera samples)")
     return p.parse_args()
 
@@ -56,6 +56,8 @@ def parse():
 CONFIG_DESC = {
     "c2": "C2 conductor Cornell box + OriginalPhong BRDF, 800x800, 1 spp, depth 6",
     "c3": "C3 70k-triangle mesh + area light, OriginalBlinnPhong, 1920x1080, 4 spp",
+    "c3ton": "C3 on the reference's ton_Roosendaal scene (62k-triangle PLY + 2 meshes) + area light, "
+             "OriginalBlinnPhong, 1920x1080, 4 spp",
     "c4": "C4 10k-triangle tree x 100 MeshInstances (~1M effective) + spherical env light, "
           "TorranceSparrow kdfresnel, 1920x1080, 16 spp",
     "c5": "C5 870k-triangle dielectric mesh + mirror sphere + Perlin ground, depth 5, 3840x2160, 64 spp",
@@ -72,6 +74,8 @@ def make_workload(args, out_dir, K=None):
         return xml, desc
     if args.config == "c2":
         xml = scenes.config_c2(out_dir, os.path.join(ROOT, "tests", "golden", "scenes", "cornell_conductors.xml"))
+    elif args.config == "c3ton":
+        xml = scenes.config_c3_ton(out_dir, os.path.join(ROOT, "tests", "golden", "scenes", "ton_Roosendaal_smooth_ply"))
     else:
         xml = getattr(scenes, "config_" + args.config)(out_dir)
     return xml, CONFIG_DESC[args.config]
