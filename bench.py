@@ -194,10 +194,12 @@ def kernel_times(ds, torch, render_timed, steps):
 
 def kernel_bytes(st, W, H):
     """Algorithmic bytes per launch of each kernel (32 B per node visit,
-    36 B per triangle test, 64 B per ray = ray in + hit out, 15 B per pixel written)."""
+    36 B per triangle test, 64 B per ray = ray in + hit out, 15 B per pixel written; the
+    shadow rays' 4-wide BVH nodes are 128 B: four child boxes + references)."""
     ext_rays = st["camera_rays"] + st["secondary_rays"]
     ext = 32 * st["node_visits"] + 36 * st["tri_tests"] + 64 * ext_rays
-    shd = 32 * st["shadow_node_visits"] + 36 * st["shadow_tri_tests"] + 64 * st["shadow_rays"]
+    shd = (32 * st["shadow_node_visits"] + 128 * st.get("shadow_wide_visits", 0) + 36 * st["shadow_tri_tests"]
+           + 64 * st["shadow_rays"])
     return {"k_primary": ext, "k_shadow": shd, "k_render": ext + shd + 15 * W * H,
             "tree_levels": ext + shd, "frame": ext + shd + 15 * W * H}
 
@@ -389,6 +391,8 @@ def main():
                 "node_visits_per_extend_ray": round(st["node_visits"] / ext, 2),
                 "tri_tests_per_extend_ray": round(st["tri_tests"] / ext, 2),
                 "shadow_node_visits_per_ray": round(st["shadow_node_visits"] / max(st["shadow_rays"], 1), 2),
+                "shadow_wide_node_visits_per_ray": round(st.get("shadow_wide_visits", 0) / max(st["shadow_rays"], 1), 2),
+                "shadow_fallback_rays": int(st.get("shadow_fallbacks", 0)),
                 "shadow_tri_tests_per_ray": round(st["shadow_tri_tests"] / max(st["shadow_rays"], 1), 2),
                 "parallelism": f"image partition x{world}: 16-row bands dealt round-robin, rank r renders bands "
                                f"b % {world} == r (one frame per step)",
