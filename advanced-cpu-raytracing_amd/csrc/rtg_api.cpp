@@ -115,6 +115,7 @@ struct rtg_scene {
     rtg::TreeState* tree = nullptr;   // its buffers
     int feat = rtg::FEAT_ALL;         // scene feature bits (traversal specialisation)
     int num_slots = 0;                // lights per pixel (wavefront light slots)
+    int shade_sk = rtg::SK_ALL;       // shading features (k_shade variant, rtg_common.hpp SK_*)
     // wavefront buffers, grown on demand
     size_t wave_pixels = 0, wave_tiles = 0;
     int wave_slots = 0;
@@ -593,6 +594,21 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     sc->wave_ok = !blur && (d->max_recursion_depth <= 0 || !branching);
     sc->num_slots = d->num_point_lights + d->num_area_lights + d->num_env_lights + d->num_dir_lights +
                     d->num_spot_lights + d->num_mesh_lights;
+    // shading features: textures / maps (incl. a background texture), BRDFs, env / spot / mesh
+    // lights; RTG_SK_FORCE=<bits> ORs bits in (experiments: the general variant, same values)
+    {
+        int sk = 0;
+        for (int i = 0; i < d->num_objects; ++i)
+            if (objs[i].tex_diffuse >= 0 || objs[i].tex_specular >= 0 || objs[i].tex_replace_all >= 0 ||
+                (objs[i].flags & rtg::OBJF_MAPPED))
+                sk |= rtg::SK_TEX;
+        if (d->bg_texture >= 0) sk |= rtg::SK_TEX;
+        for (int i = 0; i < d->num_materials; ++i)
+            if (d->materials[i].brdf >= 0) sk |= rtg::SK_BRDF;
+        if (d->num_env_lights + d->num_spot_lights + d->num_mesh_lights > 0) sk |= rtg::SK_XLIGHT;
+        if (const char* e = std::getenv("RTG_SK_FORCE")) sk |= std::atoi(e) & rtg::SK_ALL;
+        sc->shade_sk = sk;
+    }
     // mesh lights (meshLight.h): their faces in MeshLight::faces order (the BVH-permuted one)
     std::vector<rtg::DevMeshLight> mls(d->num_mesh_lights);
     std::vector<rtg::DevLightFace> lfs;
@@ -915,10 +931,10 @@ static int ensure_wave(rtg_scene* s, size_t pixels, int slots, size_t tiles) {
     const size_t ns = pixels * (size_t)std::max(slots, 1);
     const size_t nq = tiles * 256 * (size_t)std::max(slots, 1);
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    size_t off[11], total = 0;
-    const size_t sz[11] = {pixels * 4, pixels * 4, pixels * 4, pixels * 16, ns * 16, ns, nq * 16, nq * 16, nq * 4,
-                           tiles * 4, pixels * 16};
-    for (int k = 0; k < 11; ++k) { off[k] = total; total += al(sz[k]); }
+    size_t off[12], total = 0;
+    const size_t sz[12] = {pixels * 4, pixels * 4, pixels * 4, pixels * 16, ns * 16, ns, nq * 16, nq * 16, nq * 4,
+                           tiles * 4, pixels * 16, slots <= 1 ? nq * 32 : 0};
+    for (int k = 0; k < 12; ++k) { off[k] = total; total += al(sz[k]); }
     HIP_TRY(hipMalloc(&s->wave_mem, total));
     char* b = (char*)s->wave_mem;
     rtg::WaveBufs& W = s->wave;
@@ -926,6 +942,7 @@ static int ensure_wave(rtg_scene* s, size_t pixels, int slots, size_t tiles) {
     W.base = (float4*)(b + off[3]); W.term = (float4*)(b + off[4]); W.occ = (unsigned char*)(b + off[5]);
     W.q_o = (float4*)(b + off[6]); W.q_d = (float4*)(b + off[7]); W.q_slot = (int*)(b + off[8]);
     W.q_count = (int*)(b + off[9]); W.accum = (float4*)(b + off[10]);
+    W.q_pay = slots <= 1 ? (float4*)(b + off[11]) : nullptr;
     s->wave_pixels = pixels;
     s->wave_slots = slots;
     s->wave_tiles = tiles;
@@ -978,7 +995,7 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
                 W.num_slots = s->num_slots;
             }
         }
-        HIP_TRY(rtg::launch_wave(ds, C, P, W, d_hdr, d_ldr, s->counters.p, stats, s->feat, stream, ev));
+        HIP_TRY(rtg::launch_wave(ds, C, P, W, d_hdr, d_ldr, s->counters.p, stats, s->feat, s->shade_sk, stream, ev));
         if (ev) s->timed_stages = rtg::WAVE_STAGES;
         return RTG_OK;
     }

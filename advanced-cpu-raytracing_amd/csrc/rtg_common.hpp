@@ -1009,7 +1009,8 @@ struct Surf {
 DEV f3 mesh_mapped_normal(const DevScene& S, const DevObject& ob, int face, f3 lp, float u, float v);
 DEV f3 sphere_bumped_normal(const DevScene& S, const DevObject& ob, f3 p, float phi, float theta, float u, float v);
 
-template <bool STATS>
+// MAPS = false: the scene has no normal / bump maps (OBJF_MAPPED never set; k_shade variants)
+template <bool STATS, bool MAPS = true>
 DEV Surf surface(const DevScene& S, const Ray& r, float mbTime, const Hit& h, Cnt<STATS>& c) {
     const DevObject& ob = S.objects[GIDX(S, h.obj, S.num_objects, 0)];
     Surf s;
@@ -1027,7 +1028,7 @@ DEV Surf surface(const DevScene& S, const Ray& r, float mbTime, const Hit& h, Cn
         float theta = acosf(p.y / ob.center[3]);
         s.u = (float)((-phi + RT_PI) / (2.0f * RT_PI));
         s.v = (float)(theta / RT_PI);
-        f3 n = (ob.flags & OBJF_MAPPED) ? sphere_bumped_normal(S, ob, p, phi, theta, s.u, s.v)
+        f3 n = (MAPS && (ob.flags & OBJF_MAPPED)) ? sphere_bumped_normal(S, ob, p, phi, theta, s.u, s.v)
                                         : makeUnit(sub(lp, center));
         s.n = makeUnit(xform(ob.invT, n, 0.0f));
         return s;
@@ -1042,7 +1043,7 @@ DEV Surf surface(const DevScene& S, const Ray& r, float mbTime, const Hit& h, Cn
         float v = a.y + bg[0] * (b.y - a.y) + bg[1] * (cc.y - a.y);
         s.u = tiledUV(u);
         s.v = tiledUV(v);
-        if (ob.flags & OBJF_MAPPED) {
+        if (MAPS && (ob.flags & OBJF_MAPPED)) {
             // IntersectFace's local hit point (mesh.cpp:242), then the base mesh's transform
             const f3 lp = add(lr.o, muls(lr.d, h.t));
             n = makeUnit(xform(ob.baseInvT, mesh_mapped_normal(S, ob, h.face, lp, s.u, s.v), 0.0f));
@@ -1328,9 +1329,10 @@ struct ShadeCtx {
     Surf s;
 };
 
+template <bool TEX = true>
 DEV f3 kd_coeff(const DevScene& S, const ShadeCtx& c) {                // raytracer.cpp:478-508
     f3 refl = ld3(c.mat->diffuse);
-    if (c.ob->tex_diffuse >= 0) {
+    if (TEX && c.ob->tex_diffuse >= 0) {
         const DevTexture tx = S.textures[GIDX(S, c.ob->tex_diffuse, S.num_textures, 2)];
         f3 t;
         if (tx.kind == 1) { float p = perlin(S, tx, c.s.p.x, c.s.p.y, c.s.p.z); t = mk(p, p, p); }
@@ -1339,9 +1341,10 @@ DEV f3 kd_coeff(const DevScene& S, const ShadeCtx& c) {                // raytra
     }
     return refl;
 }
+template <bool TEX = true>
 DEV f3 ks_coeff(const DevScene& S, const ShadeCtx& c) {                // raytracer.cpp:509-539 (reads diffuseTex)
     f3 refl = ld3(c.mat->specular);
-    if (c.ob->tex_specular >= 0 && c.ob->tex_diffuse >= 0) {
+    if (TEX && c.ob->tex_specular >= 0 && c.ob->tex_diffuse >= 0) {
         const DevTexture tx = S.textures[GIDX(S, c.ob->tex_diffuse, S.num_textures, 2)];
         f3 t;
         if (tx.kind == 1) { float p = perlin(S, tx, c.s.p.x, c.s.p.y, c.s.p.z); t = mk(p, p, p); }
@@ -1353,19 +1356,20 @@ DEV f3 ks_coeff(const DevScene& S, const ShadeCtx& c) {                // raytra
 
 // Shade (raytracer.cpp:192-206).  TP: also ray.throughput *= brdf (:202), which Russian
 // roulette reads (path tracing only).
-template <bool TP = false>
+template <bool TP = false, int SK = SK_ALL>
 DEV f3 shade(const DevScene& S, const ShadeCtx& c, f3 w_i, f3 w_o, f3 Li, f3* tp = nullptr) {
-    if (c.mat->brdf >= 0) {
+    constexpr bool TEX = (SK & SK_TEX) != 0;
+    if ((SK & SK_BRDF) && c.mat->brdf >= 0) {
         float costheta_i = fmax0(dot(w_i, c.s.n));
-        f3 kd = kd_coeff(S, c), ks = ks_coeff(S, c);
+        f3 kd = kd_coeff<TEX>(S, c), ks = ks_coeff<TEX>(S, c);
         f3 res = brdf_apply(S.brdfs[c.mat->brdf], c.mat->refractive_index, kd, ks, w_i, w_o, c.s.n);
         if (TP) *tp = mulv(*tp, res);
         return muls(mulv(res, Li), costheta_i);
     }
-    f3 kd = kd_coeff(S, c);                                             // GetDiffuse
+    f3 kd = kd_coeff<TEX>(S, c);                                        // GetDiffuse
     float costheta = fmax0(dot(w_i, c.s.n));
     f3 diff = muls(mulv(kd, Li), costheta);
-    f3 ks = ks_coeff(S, c);                                             // GetSpecular
+    f3 ks = ks_coeff<TEX>(S, c);                                        // GetSpecular
     f3 half = divs(add(w_i, w_o), len(add(w_i, w_o)));
     float cosAlpha = fmax0(dot(c.s.n, half));
     f3 spec = muls(mulv(ks, Li), powf(cosAlpha, c.mat->phong_exponent));
@@ -1578,12 +1582,13 @@ DEV Ray camera_ray(const DevCamera& C, int px, int py, uint64_t key, float& mbTi
 }
 
 // PerPixel miss branch (raytracer.cpp:49-62)
+template <int SK = SK_ALL>
 DEV f3 miss_color(const DevScene& S, const DevCamera& C, int px, int py, f3 dir) {
-    if (S.bg_texture >= 0) {
+    if ((SK & SK_TEX) && S.bg_texture >= 0) {
         float u = px / (float)C.width, v = py / (float)C.height;
         return tex_rgb(S, S.textures[S.bg_texture], u, v);
     }
-    if (S.num_env > 0) return env_sample(S, 0, dir);
+    if ((SK & SK_XLIGHT) && S.num_env > 0) return env_sample(S, 0, dir);
     return mk((float)S.background[0], (float)S.background[1], (float)S.background[2]);
 }
 
@@ -1666,6 +1671,41 @@ DEV void flush_counters(Cnt<STATS>& cn, DevCounters* counters) {
 // (the ray-tree pipeline, or RTG_RENDER_EXACT_SHADOW) the reference walk per lane,
 // early-exit any-hit.
 // grid (shade blocks, slots): block (b, c) takes entries [256c, 256c+256) of segment b
+// CastShadowRay's answer for queue entry q (origin + initial minT o, direction + limit d).
+template <bool STATS, int FEAT, bool FAST>
+DEV bool shadow_occluded(const DevScene& S, const WaveBufs& W, size_t q, float4 o, float4 d, Cnt<STATS>& cn) {
+    Ray r;
+    r.o = mk(o.x, o.y, o.z);
+    r.d = mk(d.x, d.y, d.z);
+    int res = -1;
+    if constexpr (FAST) {
+#if RTG_SHADOW_MODE == 1
+        Hit h;
+        res = trace<true, STATS, FEAT, true>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
+#elif RTG_SHADOW_MODE == 2
+        const int slot = W.q_slot[q];
+        const int src = W.num_slots == 1 ? slot : slot / W.num_slots;
+        const int sobj = W.hit_obj ? W.hit_obj[src] : -1;
+        const int sface = sobj >= 0 ? W.hit_face[src] : -1;
+        res = trace_any_up<STATS, FEAT>(S, r, o.w, d.w, sobj, sface, cn);
+#elif RTG_SHADOW_MODE == 3
+        res = trace_any_wide<STATS, FEAT>(S, r, o.w, d.w, cn);
+#else
+        Hit h;
+        res = trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
+#endif
+        if (res < 0) {                               // undecided: the reference walk
+            cn.fallback();
+            Hit h;
+            res = trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
+        }
+    } else {
+        Hit h;
+        res = trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
+    }
+    return res > 0;
+}
+
 template <bool STATS, int FEAT, bool FAST>
 __global__ __launch_bounds__(256, FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(FEAT)) void k_shadow(const DevScene S, const WaveBufs W,
                                                                                             DevCounters* counters) {
@@ -1673,37 +1713,7 @@ __global__ __launch_bounds__(256, FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(
     const size_t q = ((size_t)blockIdx.x * W.num_slots) * 256 + k;
     Cnt<STATS> cn;
     if (k < W.q_count[blockIdx.x]) {
-        const float4 o = W.q_o[q], d = W.q_d[q];
-        Ray r;
-        r.o = mk(o.x, o.y, o.z);
-        r.d = mk(d.x, d.y, d.z);
-        int res = -1;
-        if constexpr (FAST) {
-#if RTG_SHADOW_MODE == 1
-            Hit h;
-            res = trace<true, STATS, FEAT, true>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
-#elif RTG_SHADOW_MODE == 2
-            const int slot = W.q_slot[q];
-            const int src = W.num_slots == 1 ? slot : slot / W.num_slots;
-            const int sobj = W.hit_obj ? W.hit_obj[src] : -1;
-            const int sface = sobj >= 0 ? W.hit_face[src] : -1;
-            res = trace_any_up<STATS, FEAT>(S, r, o.w, d.w, sobj, sface, cn);
-#elif RTG_SHADOW_MODE == 3
-            res = trace_any_wide<STATS, FEAT>(S, r, o.w, d.w, cn);
-#else
-            Hit h;
-            res = trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
-#endif
-            if (res < 0) {                           // undecided: the reference walk
-                cn.fallback();
-                Hit h;
-                res = trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
-            }
-        } else {
-            Hit h;
-            res = trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
-        }
-        if (res > 0) W.occ[W.q_slot[q]] = 1;
+        if (shadow_occluded<STATS, FEAT, FAST>(S, W, q, W.q_o[q], W.q_d[q], cn)) W.occ[W.q_slot[q]] = 1;
     }
     flush_counters<STATS>(cn, counters);
 }

@@ -118,6 +118,10 @@ enum : int { LEAF_EXT = 0x7FFFFFFF };
 // Scene feature bits (kernel specialisation): spheres, mesh instances, any mesh with a
 // non-identity transform or motion blur, BVH leaves of more than kCoopLeaf faces.
 enum : int { FEAT_SPHERE = 1, FEAT_INSTANCE = 2, FEAT_XFORM = 4, FEAT_BIGLEAF = 8, FEAT_ALL = 15 };
+// Shading specialisation of the wavefront k_shade (the other kernels use SK_ALL): the scene
+// has textures or normal / bump maps (SK_TEX), BRDFs (SK_BRDF), env / spot / mesh lights
+// (SK_XLIGHT).  A variant without a feature compiles its code out; the values are the same.
+enum : int { SK_TEX = 1, SK_BRDF = 2, SK_XLIGHT = 4, SK_ALL = 7 };
 // A scene with a leaf wider than kBigLeaf faces takes the cooperative walk (FEAT_BIGLEAF);
 // inside it, every leaf of more than kCoopLeaf faces is tested by the whole wave (threshold
 // 8 / 4 / 2 / 1 / 0: C3 1494 / 1680 / 1781 / 1886 / 1912, C4 1481 / 1537 / 1613 / 1648 / 1555
@@ -206,6 +210,9 @@ struct WaveBufs {
     int* __restrict__ q_slot;           // light slot it decides
     int* __restrict__ q_count;          // per block: entries in its segment
     float4* __restrict__ accum;         // multi-sample: sum w*c, sum w
+    // one-slot scenes (at most one light): per queue entry the pixel's base colour + flags
+    // and its light term + pixel index, so k_shadow finishes the pixel itself (no k_resolve)
+    float4* __restrict__ q_pay;
     int num_slots;                      // lights per pixel
 };
 

@@ -14,7 +14,7 @@ hipError_t launch_mega(const DevScene& S, const DevCamera& C, const RenderParams
                        float* accum, DevCounters* counters, bool stats, hipStream_t stream, hipEvent_t* ev);
 // wavefront pipeline (rtg_wave.hip): scenes without secondary rays / motion blur
 hipError_t launch_wave(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W, float* hdr,
-                       unsigned char* ldr, DevCounters* counters, bool stats, int feat, hipStream_t stream,
+                       unsigned char* ldr, DevCounters* counters, bool stats, int feat, int sk, hipStream_t stream,
                        hipEvent_t* ev);
 // wavefront ray trees (rtg_tree.hip): scenes with mirror / conductor / dielectric materials;
 // host-synchronous per tree level (the next level's size); state (buffers) kept in `tree`

@@ -15,6 +15,8 @@
 //
 // The float operations and their order are those of the fused kernel / the reference
 // (only unshadowed terms are summed, left to right), so both paths produce the same bits.
+#include <cstdlib>
+
 #include "rtg_common.hpp"
 #include "rtg_kernels.hpp"
 
@@ -58,9 +60,68 @@ DEV int queue_append(bool want, int* lds_count) {
     return want ? base + rank : -1;
 }
 
-template <bool STATS>
-__global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_shade(const DevScene S, const DevCamera C, const RenderParams P,
-                                               const int sample, const WaveBufs W, DevCounters* counters) {
+// Output of a sample pass: final image (spp 1) or the multi-sample accumulator.
+struct PassOut {
+    float* hdr;
+    unsigned char* ldr;
+    float4* accum;
+    int first, last;
+};
+
+// renderThreadMain's per-pixel end of a sample pass (main.cpp:80-121): the colour itself at
+// 1 spp, else the Gaussian-weighted accumulation, divided out after the last sample.
+DEV void finish_pixel(const DevCamera& C, const RenderParams& P, int sample, const PassOut& O, int pixel, f3 color) {
+    if (C.spp <= 1 && !P.accum_only) {
+        const size_t idx = 3 * (size_t)pixel;
+        if (O.hdr) { O.hdr[idx] = color.x; O.hdr[idx + 1] = color.y; O.hdr[idx + 2] = color.z; }
+        if (O.ldr) { O.ldr[idx] = ldr(color.x); O.ldr[idx + 1] = ldr(color.y); O.ldr[idx + 2] = ldr(color.z); }
+        return;
+    }
+    const float gw = sample_weight(C.spp, sample, root_key(P.seed, pixel, sample));
+    float4 a = O.first ? make_float4(0.f, 0.f, 0.f, 0.f) : O.accum[pixel];
+    a.x += color.x * gw;
+    a.y += color.y * gw;
+    a.z += color.z * gw;
+    a.w += gw;
+    O.accum[pixel] = a;
+    if (O.last && !P.accum_only) {
+        const f3 c = mk(a.x / a.w, a.y / a.w, a.z / a.w);
+        const size_t idx = 3 * (size_t)pixel;
+        if (O.hdr) { O.hdr[idx] = c.x; O.hdr[idx + 1] = c.y; O.hdr[idx + 2] = c.z; }
+        if (O.ldr) { O.ldr[idx] = ldr(c.x); O.ldr[idx + 1] = ldr(c.y); O.ldr[idx + 2] = ldr(c.z); }
+    }
+}
+
+// PerformShading's sum for a pixel with at most one light (k_resolve's loop, one slot):
+// ambient + (0 + term if the light is unoccluded) [+ the zero child term].
+DEV f3 resolve_one(f3 base, int flags, bool has_term, f3 term, bool occluded) {
+    if (flags & BASE_FINAL) return base;
+    f3 sum = mk(0, 0, 0);
+    if (has_term && !occluded) sum = add(sum, term);
+    f3 color = add(base, sum);
+    if (flags & BASE_ADD_ZERO) color = add(color, mk(0, 0, 0));   // depth-0 mirror/dielectric/conductor
+    return color;
+}
+
+// SK: shading variant (rtg_common.hpp SK_*).  MODE:
+//   SH_GENERAL  every light slot's term and occlusion flag to the per-pixel buffers, shadow
+//               rays to the block's queue segment (k_shadow, k_resolve follow);
+//   SH_ONE      at most one light: the pixel is finished here when it casts no shadow ray,
+//               else its base colour and light term travel with the shadow ray in the queue
+//               (q_pay) and k_shadow_one finishes it;
+//   SH_FUSED    at most one light, plain shading (SK 0): the lane casts its own shadow ray
+//               (any-hit walk of FEAT, FAST) and finishes its pixel -- no queue.  Almost
+//               every pixel of a scene that fills the frame casts one, and the ones that do
+//               not leave whole waves idle only along silhouettes.
+enum { SH_GENERAL = 0, SH_ONE = 1, SH_FUSED = 2 };
+template <bool STATS, int SK, int MODE, int FEAT = 0, bool FAST = false>
+__global__ __launch_bounds__(256, MODE == SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(FEAT))
+                                                   : RTG_SHADE_WAVES) void k_shade(const DevScene S, const DevCamera C,
+                                                                                   const RenderParams P,
+                                                                                   const int sample, const WaveBufs W,
+                                                                                   const PassOut O,
+                                                                                   DevCounters* counters) {
+    constexpr bool ONE = MODE != SH_GENERAL;
     __shared__ int seg_count;
     if (threadIdx.x == 0) seg_count = 0;
     __syncthreads();
@@ -77,12 +138,20 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_shade(const DevScene S
     bool lit = false;
     ShadeCtx c;
     f3 w_o = mk(0, 0, 0);
+    f3 base = mk(0, 0, 0);           // ONE: the pixel's base colour, flags, light term
+    int bflags = 0;
+    f3 term1 = mk(0, 0, 0);
+    bool has_term = false, pushed = false;
+    float4 ro = make_float4(0.f, 0.f, 0.f, 0.f), rd = ro;      // SH_FUSED: the shadow ray
+    auto put_base = [&](f3 col, int flags) {
+        if (ONE) { base = col; bflags = flags; }
+        else W.base[i] = make_float4(col.x, col.y, col.z, __int_as_float(flags));
+    };
     if (valid) {
         float mbTime;
         Ray ray = camera_ray(C, px, py, key, mbTime);
         if (obj < 0) {
-            f3 m = miss_color(S, C, px, py, ray.d);
-            W.base[i] = make_float4(m.x, m.y, m.z, __int_as_float(BASE_FINAL));
+            put_base(miss_color<SK>(S, C, px, py, ray.d), BASE_FINAL);
         } else {
             const DevObject& ob = S.objects[obj];
             Hit h;
@@ -92,20 +161,18 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_shade(const DevScene S
             h.o = ray.o;
             c.ob = &ob;
             c.mat = &S.materials[ob.material];
-            c.s = surface<STATS>(S, ray, mbTime, h, cn);
+            c.s = surface<STATS, (SK & SK_TEX) != 0>(S, ray, mbTime, h, cn);
             w_o = makeUnit(sub(ld3(C.pos), c.s.p));
             const DevMaterial& mat = *c.mat;
             if (mat.type == 3) {                                    // Emissive (raytracer.cpp:81-84)
-                f3 e = muls(muls(ld3(mat.radiance), 2.0f), (float)RT_PI);
-                W.base[i] = make_float4(e.x, e.y, e.z, __int_as_float(BASE_FINAL));
-            } else if (ob.tex_replace_all >= 0) {                   // replace_all (:87-89)
-                f3 e = tex_rgb(S, S.textures[ob.tex_replace_all], c.s.u, c.s.v);
-                W.base[i] = make_float4(e.x, e.y, e.z, __int_as_float(BASE_FINAL));
+                put_base(muls(muls(ld3(mat.radiance), 2.0f), (float)RT_PI), BASE_FINAL);
+            } else if ((SK & SK_TEX) && ob.tex_replace_all >= 0) {  // replace_all (:87-89)
+                put_base(tex_rgb(S, S.textures[ob.tex_replace_all], c.s.u, c.s.v), BASE_FINAL);
             } else {
                 // primary rays travel in vacuum (medium 1.0): ambient + direct always apply
                 f3 color = add(mk(0, 0, 0), mulv(mk(S.ambient[0], S.ambient[1], S.ambient[2]), ld3(mat.ambient)));
                 const int flags = (mat.type == 0 || mat.type == 1 || mat.type == 2) ? BASE_ADD_ZERO : 0;
-                W.base[i] = make_float4(color.x, color.y, color.z, __int_as_float(flags));
+                put_base(color, flags);
                 lit = true;
             }
         }
@@ -131,22 +198,35 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_shade(const DevScene S
                 qd = make_float4(d.x, d.y, d.z, lightT);
             }
         }
+        if constexpr (MODE == SH_FUSED) {
+            if (want) { ro = qo; rd = qd; pushed = true; }
+            return;
+        }
         const int qi = queue_append(want, &seg_count);
         if (want) {
             const size_t q = seg + qi;
             W.q_o[q] = qo;
             W.q_d[q] = qd;
-            W.q_slot[q] = slot;
-            W.occ[slot] = 0;
+            if (ONE) {
+                W.q_pay[2 * q] = make_float4(base.x, base.y, base.z, __int_as_float(bflags));
+                W.q_pay[2 * q + 1] = make_float4(term1.x, term1.y, term1.z, __int_as_float(pixel));
+                pushed = true;
+            } else {
+                W.q_slot[q] = slot;
+                W.occ[slot] = 0;
+            }
         }
     };
-    auto put = [&](f3 t) { W.term[slot] = make_float4(t.x, t.y, t.z, 0.f); };
+    auto put = [&](f3 t) {
+        if (ONE) { term1 = t; has_term = true; }
+        else W.term[slot] = make_float4(t.x, t.y, t.z, 0.f);
+    };
     for (int l = 0; l < S.num_point; ++l, ++slot) {
         const f3 lp = ld3(S.point_lights[l].pos);
         if (lit) {
             f3 w_i = makeUnit(sub(lp, p));
             float dist = len(sub(lp, p));
-            put(shade(S, c, w_i, w_o, divs(ld3(S.point_lights[l].intensity), dist * dist)));
+            put(shade<false, SK>(S, c, w_i, w_o, divs(ld3(S.point_lights[l].intensity), dist * dist)));
         }
         push(lit, lp, false);
     }
@@ -163,68 +243,97 @@ __global__ __launch_bounds__(256, RTG_SHADE_WAVES) void k_shade(const DevScene S
             w_i = divs(w_i, dist);
             float lc = dot(ld3(L.normal), neg(w_i));
             if (lc < 0) lc = dot(ld3(L.normal), w_i);
-            put(shade(S, c, w_i, w_o, muls(ld3(L.radiance), L.area * lc / dSqr)));
+            put(shade<false, SK>(S, c, w_i, w_o, muls(ld3(L.radiance), L.area * lc / dSqr)));
         }
         push(lit, sp, false);
     }
-    for (int l = 0; l < S.num_env; ++l, ++slot) {
-        if (lit) {                                                   // no shadow ray (:741-755)
-            f3 sd = env_direction(n, key, l);
-            put(shade(S, c, n, w_o, env_sample(S, l, sd)));
-            W.occ[slot] = 0;
+    if constexpr ((SK & SK_XLIGHT) != 0) {
+        for (int l = 0; l < S.num_env; ++l, ++slot) {
+            if (lit) {                                               // no shadow ray (:741-755)
+                f3 sd = env_direction(n, key, l);
+                put(shade<false, SK>(S, c, n, w_o, env_sample(S, l, sd)));
+                if (!ONE) W.occ[slot] = 0;
+            }
         }
     }
     for (int l = 0; l < S.num_dir; ++l, ++slot) {
         const f3 ldir = ld3(S.dir_lights[l].dir);
-        if (lit) put(shade(S, c, neg(ldir), w_o, ld3(S.dir_lights[l].radiance)));
+        if (lit) put(shade<false, SK>(S, c, neg(ldir), w_o, ld3(S.dir_lights[l].radiance)));
         push(lit, ldir, true);
     }
-    for (int l = 0; l < S.num_spot; ++l, ++slot) {
-        const DevSpotLight& L = S.spot_lights[l];
-        const f3 lp = ld3(L.pos);
-        if (lit) {
-            f3 w_i = makeUnit(sub(lp, p));
-            float distToPoint = len(sub(p, lp));                     // spotLight.h:33-57
-            f3 toPoint = divs(sub(p, lp), distToPoint);
-            double alpha = angleBetween(ld3(L.dir), toPoint);
-            f3 E;
-            if (alpha <= 0 || alpha > (L.coverage_deg / 2.0f)) {
-                E = mk(0, 0, 0);
-            } else {
-                float distSqr = distToPoint * distToPoint;
-                E = divs(ld3(L.intensity), distSqr);
-                if (alpha > (L.falloff_deg / 2.0f)) {
-                    double cosAlpha = cos(alpha * (RT_PI / 180.0f));
-                    double sv = pow((cosAlpha - L.cos_half_coverage) / (L.cos_half_falloff - L.cos_half_coverage),
-                                    (double)4.0f);
-                    E = muls(E, (float)sv);
+    if constexpr ((SK & SK_XLIGHT) != 0) {
+        for (int l = 0; l < S.num_spot; ++l, ++slot) {
+            const DevSpotLight& L = S.spot_lights[l];
+            const f3 lp = ld3(L.pos);
+            if (lit) {
+                f3 w_i = makeUnit(sub(lp, p));
+                float distToPoint = len(sub(p, lp));                 // spotLight.h:33-57
+                f3 toPoint = divs(sub(p, lp), distToPoint);
+                double alpha = angleBetween(ld3(L.dir), toPoint);
+                f3 E;
+                if (alpha <= 0 || alpha > (L.coverage_deg / 2.0f)) {
+                    E = mk(0, 0, 0);
+                } else {
+                    float distSqr = distToPoint * distToPoint;
+                    E = divs(ld3(L.intensity), distSqr);
+                    if (alpha > (L.falloff_deg / 2.0f)) {
+                        double cosAlpha = cos(alpha * (RT_PI / 180.0f));
+                        double sv = pow((cosAlpha - L.cos_half_coverage) / (L.cos_half_falloff - L.cos_half_coverage),
+                                        (double)4.0f);
+                        E = muls(E, (float)sv);
+                    }
                 }
+                put(shade<false, SK>(S, c, w_i, w_o, E));
             }
-            put(shade(S, c, w_i, w_o, E));
+            push(lit, lp, false);
         }
-        push(lit, lp, false);
-    }
-    for (int l = 0; l < S.num_mesh; ++l, ++slot) {                  // mesh lights (:780-803)
-        f3 sp = mk(0, 0, 0);
-        if (lit) {
-            f3 E;
-            mesh_light_sample(S, l, key, sp, E);
-            f3 w_i = sub(sp, p);
-            float dist = len(w_i);
-            w_i = divs(w_i, dist);
-            put(shade(S, c, w_i, w_o, E));
+        for (int l = 0; l < S.num_mesh; ++l, ++slot) {              // mesh lights (:780-803)
+            f3 sp = mk(0, 0, 0);
+            if (lit) {
+                f3 E;
+                mesh_light_sample(S, l, key, sp, E);
+                f3 w_i = sub(sp, p);
+                float dist = len(w_i);
+                w_i = divs(w_i, dist);
+                put(shade<false, SK>(S, c, w_i, w_o, E));
+            }
+            push(lit, sp, false);
         }
-        push(lit, sp, false);
     }
+    if constexpr (MODE == SH_FUSED) {
+        if (pushed) {
+            const bool occluded = shadow_occluded<STATS, FEAT, FAST>(S, W, 0, ro, rd, cn);
+            finish_pixel(C, P, sample, O, pixel, resolve_one(base, bflags, true, term1, occluded));
+        } else if (valid) {
+            finish_pixel(C, P, sample, O, pixel, resolve_one(base, bflags, has_term, term1, false));
+        }
+    }
+    if (MODE == SH_ONE && valid && !pushed) finish_pixel(C, P, sample, O, pixel, resolve_one(base, bflags, has_term, term1, false));
     __syncthreads();
     if (threadIdx.x == 0) W.q_count[blockIdx.x] = seg_count;
     flush_counters<STATS>(cn, counters);
 }
 
+// One-light scenes: CastShadowRay for a queued pixel, then its PerformShading sum and the end
+// of the sample pass (what k_resolve does for the general case).
+template <bool STATS, int FEAT, bool FAST>
+__global__ __launch_bounds__(256, FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(FEAT)) void k_shadow_one(
+    const DevScene S, const DevCamera C, const RenderParams P, const int sample, const WaveBufs W, const PassOut O,
+    DevCounters* counters) {
+    const int k = threadIdx.x;
+    const size_t q = (size_t)blockIdx.x * 256 + k;
+    Cnt<STATS> cn;
+    if (k < W.q_count[blockIdx.x]) {
+        const bool occluded = shadow_occluded<STATS, FEAT, FAST>(S, W, q, W.q_o[q], W.q_d[q], cn);
+        const float4 b = W.q_pay[2 * q], t = W.q_pay[2 * q + 1];
+        const f3 color = resolve_one(mk(b.x, b.y, b.z), __float_as_int(b.w), true, mk(t.x, t.y, t.z), occluded);
+        finish_pixel(C, P, sample, O, __float_as_int(t.w), color);
+    }
+    flush_counters<STATS>(cn, counters);
+}
+
 __global__ __launch_bounds__(256) void k_resolve(const DevCamera C, const RenderParams P, const int sample,
-                                                 const int first, const int last, const WaveBufs W,
-                                                 float* __restrict__ hdr, unsigned char* __restrict__ ldrOut,
-                                                 float4* __restrict__ accum) {
+                                                 const WaveBufs W, const PassOut O) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     const int npix = P.part_rows * C.width;
     if (i >= npix) return;
@@ -243,58 +352,72 @@ __global__ __launch_bounds__(256) void k_resolve(const DevCamera C, const Render
         color = add(color, sum);
         if (flags & BASE_ADD_ZERO) color = add(color, mk(0, 0, 0));   // depth-0 mirror/dielectric/conductor
     }
-    if (C.spp <= 1 && !P.accum_only) {
-        const size_t idx = 3 * (size_t)pixel;
-        if (hdr) { hdr[idx] = color.x; hdr[idx + 1] = color.y; hdr[idx + 2] = color.z; }
-        if (ldrOut) { ldrOut[idx] = ldr(color.x); ldrOut[idx + 1] = ldr(color.y); ldrOut[idx + 2] = ldr(color.z); }
-        return;
-    }
-    // renderThreadMain multisampling (main.cpp:80-100), one sample pass per launch
-    const float gw = sample_weight(C.spp, sample, root_key(P.seed, pixel, sample));
-    float4 a = first ? make_float4(0.f, 0.f, 0.f, 0.f) : accum[pixel];
-    a.x += color.x * gw;
-    a.y += color.y * gw;
-    a.z += color.z * gw;
-    a.w += gw;
-    accum[pixel] = a;
-    if (last && !P.accum_only) {
-        const f3 c = mk(a.x / a.w, a.y / a.w, a.z / a.w);
-        const size_t idx = 3 * (size_t)pixel;
-        if (hdr) { hdr[idx] = c.x; hdr[idx + 1] = c.y; hdr[idx + 2] = c.z; }
-        if (ldrOut) { ldrOut[idx] = ldr(c.x); ldrOut[idx + 1] = ldr(c.y); ldrOut[idx + 2] = ldr(c.z); }
-    }
+    finish_pixel(C, P, sample, O, pixel, color);
 }
 
-template <bool STATS, int FEAT>
+static bool no_fused_shade() {
+    static const bool v = std::getenv("RTG_NO_FUSED_SHADE") != nullptr;
+    return v;
+}
+
+template <bool STATS, int FEAT, int SK>
 static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W,
                                 float* hdr, unsigned char* l, DevCounters* cnt, hipStream_t st, hipEvent_t* ev) {
     const int npix = P.part_rows * C.width;
     const int nshadow = S.num_point + S.num_area + S.num_dir + S.num_spot + S.num_mesh;
-    float4* accum = W.accum;
+    // at most one light: k_shade / k_shadow_one finish the pixels (no k_resolve); SK variants
+    // for this case only (every other scene takes the general k_shade)
+    const bool one = W.num_slots <= 1 && W.q_pay != nullptr;
+    // fast any-hit walk (RTG_SHADOW_MODE) unless RTG_RENDER_EXACT_SHADOW asks for the
+    // reference walk
+    const bool fast = (RTG_SHADOW_MODE == 3 ? S.wnodes != nullptr
+                                            : RTG_SHADOW_MODE == 2 ? S.node_up != nullptr : S.nodes != nullptr) &&
+                      !(FEAT & FEAT_BIGLEAF) && !S.exact_shadow;
+    // shading fused with the shadow ray: plain shading, the fast any-hit walk (RTG_NO_FUSED_SHADE=1
+    // keeps the queue: experiments)
+    const bool fused = SK == 0 && fast && !(FEAT & FEAT_BIGLEAF) && nshadow > 0 && !no_fused_shade();
     for (int s = P.sample_begin; s < P.sample_begin + P.sample_count; ++s) {
         const int first = s == P.sample_begin, last = s == P.sample_begin + P.sample_count - 1;
+        const PassOut O{hdr, l, W.accum, first, last};
         hipEvent_t* e5 = last ? ev : nullptr;
         hipError_t e;
         if (e5) (void)hipEventRecord(e5[0], st);
         hipLaunchKernelGGL((k_primary<STATS, FEAT>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
         if (e5) (void)hipEventRecord(e5[1], st);
-        hipLaunchKernelGGL((k_shade<STATS>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
-        if (e5) (void)hipEventRecord(e5[2], st);
-        if (nshadow > 0) {
-            // fast any-hit walk (RTG_SHADOW_MODE) unless RTG_RENDER_EXACT_SHADOW asks for the
-            // reference walk
-            const bool fast = (RTG_SHADOW_MODE == 3 ? S.wnodes != nullptr
-                                                    : RTG_SHADOW_MODE == 2 ? S.node_up != nullptr : S.nodes != nullptr) &&
-                              !(FEAT & FEAT_BIGLEAF) && !S.exact_shadow;
-            if (fast) {
-                hipLaunchKernelGGL((k_shadow<STATS, FEAT, true>), dim3(P.num_tiles, nshadow), dim3(256), 0, st, S, W, cnt);
-            } else {
-                hipLaunchKernelGGL((k_shadow<STATS, FEAT, false>), dim3(P.num_tiles, nshadow), dim3(256), 0, st, S, W, cnt);
+        if (one && fused) {
+            if constexpr (SK == 0 && !(FEAT & FEAT_BIGLEAF))
+                hipLaunchKernelGGL((k_shade<STATS, 0, SH_FUSED, FEAT, true>), dim3(P.num_tiles), dim3(256), 0, st, S, C,
+                                   P, s, W, O, cnt);
+            if (e5) (void)hipEventRecord(e5[2], st);
+            if (e5) (void)hipEventRecord(e5[3], st);
+        } else if (one) {
+            hipLaunchKernelGGL((k_shade<STATS, SK, SH_ONE>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, O, cnt);
+            if (e5) (void)hipEventRecord(e5[2], st);
+            if (nshadow > 0) {
+                if (fast)
+                    hipLaunchKernelGGL((k_shadow_one<STATS, FEAT, true>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P,
+                                       s, W, O, cnt);
+                else
+                    hipLaunchKernelGGL((k_shadow_one<STATS, FEAT, false>), dim3(P.num_tiles), dim3(256), 0, st, S, C,
+                                       P, s, W, O, cnt);
             }
+            if (e5) (void)hipEventRecord(e5[3], st);
+        } else {
+            hipLaunchKernelGGL((k_shade<STATS, SK_ALL, SH_GENERAL>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, O,
+                               cnt);
+            if (e5) (void)hipEventRecord(e5[2], st);
+            if (nshadow > 0) {
+                if (fast) {
+                    hipLaunchKernelGGL((k_shadow<STATS, FEAT, true>), dim3(P.num_tiles, nshadow), dim3(256), 0, st, S,
+                                       W, cnt);
+                } else {
+                    hipLaunchKernelGGL((k_shadow<STATS, FEAT, false>), dim3(P.num_tiles, nshadow), dim3(256), 0, st, S,
+                                       W, cnt);
+                }
+            }
+            if (e5) (void)hipEventRecord(e5[3], st);
+            hipLaunchKernelGGL(k_resolve, dim3((npix + 255) / 256), dim3(256), 0, st, C, P, s, W, O);
         }
-        if (e5) (void)hipEventRecord(e5[3], st);
-        hipLaunchKernelGGL(k_resolve, dim3((npix + 255) / 256), dim3(256), 0, st, C, P, s, first, last, W, hdr, l,
-                           accum);
         if (e5) (void)hipEventRecord(e5[4], st);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
@@ -302,15 +425,31 @@ static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const Ren
     return hipSuccess;
 }
 
+template <int FEAT>
+static hipError_t launch_wave_f(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W,
+                                float* hdr, unsigned char* l, DevCounters* cnt, bool stats, int sk, hipStream_t st,
+                                hipEvent_t* ev) {
+    // shading variants exist for one-light scenes only (the general k_shade otherwise)
+    if (!(W.num_slots <= 1 && W.q_pay != nullptr)) sk = SK_ALL;
+#define RTG_SK(K)                                                                      \
+    case K:                                                                            \
+        return stats ? launch_wave_t<true, FEAT, K>(S, C, P, W, hdr, l, cnt, st, ev)   \
+                     : launch_wave_t<false, FEAT, K>(S, C, P, W, hdr, l, cnt, st, ev)
+    switch (sk & SK_ALL) {
+        RTG_SK(0); RTG_SK(1); RTG_SK(2); RTG_SK(3); RTG_SK(4); RTG_SK(5); RTG_SK(6);
+        default: RTG_SK(SK_ALL);
+    }
+#undef RTG_SK
+}
+
 hipError_t launch_wave(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W, float* hdr,
-                       unsigned char* l, DevCounters* cnt, bool stats, int feat, hipStream_t stream, hipEvent_t* ev) {
+                       unsigned char* l, DevCounters* cnt, bool stats, int feat, int sk, hipStream_t stream,
+                       hipEvent_t* ev) {
     // traversal variants: meshes only (identity transforms) / + spheres / everything,
     // each with the sequential or the cooperative (large-leaf) BVH walk
     const bool big = (feat & FEAT_BIGLEAF) != 0;
     const int base = feat & ~FEAT_BIGLEAF;
-#define RTG_WAVE(F)                                                                    \
-    return stats ? launch_wave_t<true, F>(S, C, P, W, hdr, l, cnt, stream, ev)         \
-                 : launch_wave_t<false, F>(S, C, P, W, hdr, l, cnt, stream, ev)
+#define RTG_WAVE(F) return launch_wave_f<F>(S, C, P, W, hdr, l, cnt, stats, sk, stream, ev)
     if (base == 0) {
         if (big) RTG_WAVE(FEAT_BIGLEAF);
         RTG_WAVE(0);
