@@ -130,7 +130,7 @@ struct rtg_scene {
     int tm_x = -1, tm_y = -1, tm_mode = -1;
     // RTG_RENDER_TIMING events (stage k runs between ev[k] and ev[k+1])
     hipEvent_t ev[rtg::MAX_STAGES + 1] = {};
-    int timed_stages = 0;             // stages recorded by the last timed render
+    int timed_layout = -1;            // stage layout of the last timed render (rtg_kernels.hpp LAYOUT_*)
     // the scene's own stream (rtg_render) and the event marking the end of its last render
     // on whatever stream it was issued (rtg_scene_stats waits for it, not for the device)
     hipStream_t stream = nullptr;
@@ -976,7 +976,7 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
             acc = s->wave.accum;
         }
         HIP_TRY(rtg::launch_tree(s->tree, ds, C, P, d_hdr, d_ldr, acc, s->counters.p, stats, s->feat, stream, ev));
-        if (ev) s->timed_stages = rtg::TREE_STAGES;
+        if (ev) s->timed_layout = rtg::LAYOUT_TREE;
         return RTG_OK;
     }
     if (s->wave_ok && !fused_only) {
@@ -995,12 +995,14 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
                 W.num_slots = s->num_slots;
             }
         }
-        HIP_TRY(rtg::launch_wave(ds, C, P, W, d_hdr, d_ldr, s->counters.p, stats, s->feat, s->shade_sk, stream, ev));
-        if (ev) s->timed_stages = rtg::WAVE_STAGES;
+        int layout = rtg::LAYOUT_WAVE;
+        HIP_TRY(rtg::launch_wave(ds, C, P, W, d_hdr, d_ldr, s->counters.p, stats, s->feat, s->shade_sk, stream, ev,
+                                 &layout));
+        if (ev) s->timed_layout = layout;
         return RTG_OK;
     }
     HIP_TRY(rtg::launch_mega(ds, C, P, d_hdr, d_ldr, d_accum, s->counters.p, stats, stream, ev));
-    if (ev) s->timed_stages = rtg::MEGA_STAGES;
+    if (ev) s->timed_layout = rtg::LAYOUT_MEGA;
     return RTG_OK;
 }
 
@@ -1226,15 +1228,19 @@ int rtg_scene_reset_stats(rtg_scene* s) {
 }
 
 int rtg_scene_timings(rtg_scene* s, float* ms, const char** names, int32_t cap, int32_t* count) {
-    static const char* kWave[rtg::WAVE_STAGES] = {"k_primary", "k_shade", "k_shadow", "k_resolve"};
-    static const char* kMega[rtg::MEGA_STAGES] = {"k_render"};
-    static const char* kTree[rtg::TREE_STAGES] = {"tree_levels", "tree_resolve"};
+    // stage names per layout (rtg_kernels.hpp LAYOUT_*)
+    static const char* kNames[5][rtg::MAX_STAGES] = {{"k_primary", "k_shade", "k_shadow", "k_resolve"},
+                                                     {"k_primary", "k_shade", "k_shadow"},
+                                                     {"k_primary", "k_shade_shadow"},
+                                                     {"tree_levels", "tree_resolve"},
+                                                     {"k_render"}};
+    static const int kCount[5] = {rtg::WAVE_STAGES, 3, 2, rtg::TREE_STAGES, rtg::MEGA_STAGES};
     if (!s || !count) return set_err(RTG_ERR_INVALID, "null argument");
-    if (!s->timed_stages) return set_err(RTG_ERR_INVALID, "no render was issued with RTG_RENDER_TIMING");
+    if (s->timed_layout < 0) return set_err(RTG_ERR_INVALID, "no render was issued with RTG_RENDER_TIMING");
     HIP_TRY(hipSetDevice(s->device));
-    const int n = s->timed_stages;
+    const int n = kCount[s->timed_layout];
     HIP_TRY(hipEventSynchronize(s->ev[n]));
-    const char** nm = n == rtg::WAVE_STAGES ? kWave : (n == rtg::TREE_STAGES ? kTree : kMega);
+    const char* const* nm = kNames[s->timed_layout];
     for (int k = 0; k < n && k < cap; ++k) {
         float t = 0.f;
         HIP_TRY(hipEventElapsedTime(&t, s->ev[k], s->ev[k + 1]));

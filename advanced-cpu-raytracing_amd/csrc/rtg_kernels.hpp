@@ -15,7 +15,7 @@ hipError_t launch_mega(const DevScene& S, const DevCamera& C, const RenderParams
 // wavefront pipeline (rtg_wave.hip): scenes without secondary rays / motion blur
 hipError_t launch_wave(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W, float* hdr,
                        unsigned char* ldr, DevCounters* counters, bool stats, int feat, int sk, hipStream_t stream,
-                       hipEvent_t* ev);
+                       hipEvent_t* ev, int* layout);
 // wavefront ray trees (rtg_tree.hip): scenes with mirror / conductor / dielectric materials;
 // host-synchronous per tree level (the next level's size); state (buffers) kept in `tree`
 struct TreeState;
@@ -36,5 +36,10 @@ hipError_t build_mesh_bvh(const rtg_face* d_faces, int n, const float root_mn[3]
                           float2* d_fuv, float4* d_v12, int* d_perm, int* nodeCount, bool* bigleaf,
                           hipStream_t st);
 enum { WAVE_STAGES = 4, MEGA_STAGES = 1, TREE_STAGES = 2, MAX_STAGES = 4 };
+// Timed stage layouts (RTG_RENDER_TIMING): which kernels ran between the recorded events.
+enum { LAYOUT_WAVE = 0,          // k_primary, k_shade, k_shadow, k_resolve
+       LAYOUT_WAVE_ONE = 1,      // k_primary, k_shade, k_shadow (k_shadow_one finishes pixels)
+       LAYOUT_WAVE_FUSED = 2,    // k_primary, k_shade_shadow
+       LAYOUT_TREE = 3, LAYOUT_MEGA = 4 };
 
 }  // namespace rtg

@@ -362,7 +362,8 @@ static bool no_fused_shade() {
 
 template <bool STATS, int FEAT, int SK>
 static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W,
-                                float* hdr, unsigned char* l, DevCounters* cnt, hipStream_t st, hipEvent_t* ev) {
+                                float* hdr, unsigned char* l, DevCounters* cnt, hipStream_t st, hipEvent_t* ev,
+                                int* layout) {
     const int npix = P.part_rows * C.width;
     const int nshadow = S.num_point + S.num_area + S.num_dir + S.num_spot + S.num_mesh;
     // at most one light: k_shade / k_shadow_one finish the pixels (no k_resolve); SK variants
@@ -376,6 +377,7 @@ static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const Ren
     // shading fused with the shadow ray: plain shading, the fast any-hit walk (RTG_NO_FUSED_SHADE=1
     // keeps the queue: experiments)
     const bool fused = SK == 0 && fast && !(FEAT & FEAT_BIGLEAF) && nshadow > 0 && !no_fused_shade();
+    *layout = one ? (fused ? LAYOUT_WAVE_FUSED : LAYOUT_WAVE_ONE) : LAYOUT_WAVE;
     for (int s = P.sample_begin; s < P.sample_begin + P.sample_count; ++s) {
         const int first = s == P.sample_begin, last = s == P.sample_begin + P.sample_count - 1;
         const PassOut O{hdr, l, W.accum, first, last};
@@ -389,7 +391,6 @@ static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const Ren
                 hipLaunchKernelGGL((k_shade<STATS, 0, SH_FUSED, FEAT, true>), dim3(P.num_tiles), dim3(256), 0, st, S, C,
                                    P, s, W, O, cnt);
             if (e5) (void)hipEventRecord(e5[2], st);
-            if (e5) (void)hipEventRecord(e5[3], st);
         } else if (one) {
             hipLaunchKernelGGL((k_shade<STATS, SK, SH_ONE>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, O, cnt);
             if (e5) (void)hipEventRecord(e5[2], st);
@@ -417,8 +418,8 @@ static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const Ren
             }
             if (e5) (void)hipEventRecord(e5[3], st);
             hipLaunchKernelGGL(k_resolve, dim3((npix + 255) / 256), dim3(256), 0, st, C, P, s, W, O);
+            if (e5) (void)hipEventRecord(e5[4], st);
         }
-        if (e5) (void)hipEventRecord(e5[4], st);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -428,13 +429,13 @@ static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const Ren
 template <int FEAT>
 static hipError_t launch_wave_f(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W,
                                 float* hdr, unsigned char* l, DevCounters* cnt, bool stats, int sk, hipStream_t st,
-                                hipEvent_t* ev) {
+                                hipEvent_t* ev, int* layout) {
     // shading variants exist for one-light scenes only (the general k_shade otherwise)
     if (!(W.num_slots <= 1 && W.q_pay != nullptr)) sk = SK_ALL;
 #define RTG_SK(K)                                                                      \
     case K:                                                                            \
-        return stats ? launch_wave_t<true, FEAT, K>(S, C, P, W, hdr, l, cnt, st, ev)   \
-                     : launch_wave_t<false, FEAT, K>(S, C, P, W, hdr, l, cnt, st, ev)
+        return stats ? launch_wave_t<true, FEAT, K>(S, C, P, W, hdr, l, cnt, st, ev, layout)   \
+                     : launch_wave_t<false, FEAT, K>(S, C, P, W, hdr, l, cnt, st, ev, layout)
     switch (sk & SK_ALL) {
         RTG_SK(0); RTG_SK(1); RTG_SK(2); RTG_SK(3); RTG_SK(4); RTG_SK(5); RTG_SK(6);
         default: RTG_SK(SK_ALL);
@@ -444,12 +445,12 @@ static hipError_t launch_wave_f(const DevScene& S, const DevCamera& C, const Ren
 
 hipError_t launch_wave(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W, float* hdr,
                        unsigned char* l, DevCounters* cnt, bool stats, int feat, int sk, hipStream_t stream,
-                       hipEvent_t* ev) {
+                       hipEvent_t* ev, int* layout) {
     // traversal variants: meshes only (identity transforms) / + spheres / everything,
     // each with the sequential or the cooperative (large-leaf) BVH walk
     const bool big = (feat & FEAT_BIGLEAF) != 0;
     const int base = feat & ~FEAT_BIGLEAF;
-#define RTG_WAVE(F) return launch_wave_f<F>(S, C, P, W, hdr, l, cnt, stats, sk, stream, ev)
+#define RTG_WAVE(F) return launch_wave_f<F>(S, C, P, W, hdr, l, cnt, stats, sk, stream, ev, layout)
     if (base == 0) {
         if (big) RTG_WAVE(FEAT_BIGLEAF);
         RTG_WAVE(0);

@@ -200,7 +200,7 @@ def kernel_bytes(st, W, H):
     ext = 32 * st["node_visits"] + 36 * st["tri_tests"] + 64 * ext_rays
     shd = (32 * st["shadow_node_visits"] + 128 * st.get("shadow_wide_visits", 0) + 36 * st["shadow_tri_tests"]
            + 64 * st["shadow_rays"])
-    return {"k_primary": ext, "k_shadow": shd, "k_render": ext + shd + 15 * W * H,
+    return {"k_primary": ext, "k_shadow": shd, "k_shade_shadow": shd + 15 * W * H, "k_render": ext + shd + 15 * W * H,
             "tree_levels": ext + shd, "frame": ext + shd + 15 * W * H}
 
 

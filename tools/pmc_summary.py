@@ -20,10 +20,13 @@ def per_kernel(d, counter):
     for r in csv.DictReader(open(path)):
         if r["Counter_Name"] != counter:
             continue
-        m = re.search(r"rtg::(k_\w+)(<(\w+)[^>]*>)?", r["Kernel_Name"])
+        m = re.search(r"rtg::(k_\w+)(<([^>]*)>)?", r["Kernel_Name"])
         if not m:
             continue
-        name = m.group(1) + ("" if not m.group(3) else f"<{m.group(3)}>")
+        base, targs = m.group(1), [t.strip() for t in (m.group(3) or "").split(",") if t.strip()]
+        if base == "k_shade" and len(targs) >= 3 and targs[2] == "2":
+            base = "k_shade_shadow"                      # SH_FUSED: shading + the shadow ray
+        name = base + (f"<{targs[0]}>" if targs else "")
         acc[name].append(float(r["Counter_Value"]))
     return {k: (sum(v) / len(v), len(v)) for k, v in acc.items()}
 
