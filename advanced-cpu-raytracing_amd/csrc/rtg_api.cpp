@@ -955,6 +955,7 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
     // RTG_RENDER_EXACT_SHADOW: shadow rays walk the reference BVH (cross-checks of the wide one)
     rtg::DevScene ds = s->ds;
     if (o->flags & RTG_RENDER_EXACT_SHADOW) ds.exact_shadow = 1;
+    if ((o->flags & RTG_RENDER_ORDERED) && ds.wnodes && ds.face_leaf) ds.ordered = 1;
     hipEvent_t* ev = nullptr;
     if (o->flags & RTG_RENDER_TIMING) {
         for (auto& e : s->ev)
@@ -1211,6 +1212,8 @@ int rtg_scene_stats(rtg_scene* s, rtg_stats* out) {
         out->shadow_tri_tests += c.shadow_tri_tests;
         out->shadow_wide_visits += c.shadow_wide_visits;
         out->shadow_fallbacks += c.shadow_fallbacks;
+        out->extend_wide_visits += c.extend_wide_visits;
+        out->extend_fallbacks += c.extend_fallbacks;
     }
     return RTG_OK;
 }

@@ -138,11 +138,15 @@ template <bool STATS> struct Cnt {
     DEV void cam() {} DEV void sec() {} DEV void shd() {}
     DEV void wnode() {}
     DEV void fallback() {}
+    DEV void ewnode() {}
+    DEV void efallback() {}
 };
 template <> struct Cnt<true> {
     uint32_t nodes = 0, tris = 0, sphs = 0, objs = 0, cams = 0, secs = 0, shds = 0, snodes = 0, stris = 0, wnodes = 0,
-             fallbacks = 0;
+             fallbacks = 0, ewnodes = 0, efallbacks = 0;
     DEV void wnode() { ++wnodes; }
+    DEV void ewnode() { ++ewnodes; }
+    DEV void efallback() { ++efallbacks; }
     DEV void fallback() { ++fallbacks; }
     template <bool ANY> DEV void node() { if (ANY) ++snodes; else ++nodes; }
     template <bool ANY> DEV void tri() { if (ANY) ++stris; else ++tris; }
@@ -879,6 +883,143 @@ DEV int trace_any_wide(const DevScene& S, const Ray& r, float minT0, float limit
         undecided |= res < 0;
     }
     return undecided ? -1 : 0;
+}
+
+// ---------------------------------------------------------------------------
+// Opt-in ordered closest hit (RTG_RENDER_ORDERED; meshes with identity transforms only)
+// ---------------------------------------------------------------------------
+// IntersectObjects' answer is the last face it accepts.  Let C be the faces IntersectFace
+// accepts at minT = inf whose reference leaf box passes the slab test at inf, and f* the
+// minimum of C in the (t, object, face) order.  Every accepted face is in C, faces before f*
+// in the walk have larger t (a smaller or equal t would precede f* in that order), so when
+// the reference reaches f* its minT exceeds t* and f* is accepted, and nothing after it can
+// be.  It reaches f* for certain if f*'s leaf box passes at t* (tmin <= t*: every ancestor
+// box contains it, the slab test is monotone in box and minT).  This walk visits the 4-wide
+// BVH nearest child first and culls a child only when its conservative entry distance is
+// beyond the best t so far, so it finds f* unless a face of C hides in a culled box with
+// t below the box's entry -- rounding on a box boundary or an ill-conditioned triangle, which
+// no cheap test excludes.  The result is therefore checked, not proven: the winner's leaf box
+// must pass exactly at t* and no box may have been culled within 2^-16 (relative) of t*;
+// otherwise (or on a stack overflow) the caller runs the reference walk.  No hit at all is
+// exact (nothing is culled before a face is found).  Off by default; tests report its
+// agreement with the reference order (tests/test_gpu_ordered.py).
+// Smallest float above a positive x (inf stays inf): "minT = next_up(t)" accepts t' <= t.
+DEV float next_up(float x) { return x == INFINITY ? x : __uint_as_float(__float_as_uint(x) + 1u); }
+#ifndef RTG_ORD_STACK
+#define RTG_ORD_STACK 12
+#endif
+template <bool STATS>
+DEV bool trace_ordered(const DevScene& S, const Ray& r, Hit& h, Cnt<STATS>& c) {
+    __shared__ int s_node[RTG_ORD_STACK][256];
+    __shared__ float s_tn[RTG_ORD_STACK][256];
+    h.t = INFINITY;
+    h.obj = -1;
+    h.face = -1;
+    h.o = r.o;
+    const RayRcp q = ray_rcp(r);
+    if (!q.fast) return false;
+    const SlabRay sr = slab_ray(r, q);
+    const int tid = threadIdx.x;
+    float bestT = INFINITY, cullMin = INFINITY;
+    int bestF = -1, bestK = -1;
+    for (int k = 0; k < S.num_objects; ++k) {
+        const DevObject& ob = S.objects[k];
+        c.obj();
+        if (ob.wroot < 0) continue;
+        int node = ob.wroot, sp = 0;
+        while (true) {
+            const WNode* N = S.wnodes + node;
+            const float4 lox = N->lox, hix = N->hix, loy = N->loy, hiy = N->hiy, loz = N->loz, hiz = N->hiz;
+            const int4 ch = N->child, lf = N->leaf;
+            c.ewnode();
+            // a child passes when its conservative entry is at most the best t (ties may still win)
+            const float minTc = bestT * (1.0f + 0x1p-21f);
+            float tn[4];
+            bool hinf[4];
+            const float inf = INFINITY;
+            hinf[0] = slab_cons(lox.x, loy.x, loz.x, hix.x, hiy.x, hiz.x, sr, inf, tn[0]) & (ch.x != WCHILD_EMPTY);
+            hinf[1] = slab_cons(lox.y, loy.y, loz.y, hix.y, hiy.y, hiz.y, sr, inf, tn[1]) & (ch.y != WCHILD_EMPTY);
+            hinf[2] = slab_cons(lox.z, loy.z, loz.z, hix.z, hiy.z, hiz.z, sr, inf, tn[2]) & (ch.z != WCHILD_EMPTY);
+            hinf[3] = slab_cons(lox.w, loy.w, loz.w, hix.w, hiy.w, hiz.w, sr, inf, tn[3]) & (ch.w != WCHILD_EMPTY);
+            const int cidx[4] = {ch.x, ch.y, ch.z, ch.w};
+            const int lidx[4] = {lf.x, lf.y, lf.z, lf.w};
+            // leaves first (they can only lower bestT), then the inner children nearest first
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (!hinf[j] || cidx[j] >= 0) continue;
+                if (!(tn[j] < minTc)) { cullMin = fminf(cullMin, tn[j]); continue; }
+                const int ref = -2 - cidx[j];
+                int first = lidx[j] >> 8, cnt = lidx[j] & 255;
+                if (lidx[j] == LEAF_EXT) {
+                    const int2 e = S.node_ext[ref];
+                    first = e.x;
+                    cnt = e.y;
+                }
+                for (int f = first; f < first + cnt; ++f) {
+                    c.template tri<false>();
+                    float t;
+                    // accepted at minT just above bestT: t <= bestT
+                    if (!tri_test_fast(S, f, r, next_up(bestT), t)) continue;
+                    // (t, object, face) order; t <= bestT here, objects come in order
+                    if (t < bestT || (k == bestK && f < bestF)) {
+                        bestT = t;
+                        bestF = f;
+                        bestK = k;
+                    }
+                }
+            }
+            const float minTc2 = bestT * (1.0f + 0x1p-21f);
+            int next = -1;
+            float nextT = INFINITY;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (!hinf[j] || cidx[j] < 0) continue;
+                if (!(tn[j] < minTc2)) { cullMin = fminf(cullMin, tn[j]); continue; }
+                int spillN = cidx[j];
+                float spillT = tn[j];
+                if (tn[j] < nextT) {
+                    spillN = next;
+                    spillT = nextT;
+                    next = cidx[j];
+                    nextT = tn[j];
+                }
+                if (spillN >= 0) {
+                    if (sp >= RTG_ORD_STACK) return false;            // stack full: reference walk
+                    s_node[sp][tid] = spillN;
+                    s_tn[sp][tid] = spillT;
+                    ++sp;
+                }
+            }
+            if (next >= 0) {
+                node = next;
+                continue;
+            }
+            // pop the nearest remaining entry still in front of the best hit
+            bool found = false;
+            while (sp > 0) {
+                --sp;
+                const float t = s_tn[sp][tid];
+                if (t < bestT * (1.0f + 0x1p-21f)) {
+                    node = s_node[sp][tid];
+                    found = true;
+                    break;
+                }
+                cullMin = fminf(cullMin, t);
+            }
+            if (!found) break;
+        }
+    }
+    if (bestF < 0) return true;                                        // no hit: exact
+    // certificate: the winner's reference leaf box passes exactly at t* (tmin <= t*), and
+    // nothing was culled within 2^-16 of t*
+    if (!(cullMin > bestT * (1.0f + 0x1p-16f))) return false;
+    const int leaf = S.face_leaf[bestF];
+    const float4 a = S.nodes[2 * leaf], b = S.nodes[2 * leaf + 1];
+    if (!box_hit(a.x, a.y, a.z, a.w, b.x, b.y, r, next_up(bestT))) return false;
+    h.t = bestT;
+    h.obj = bestK;
+    h.face = bestF;
+    return true;
 }
 
 // The same decision on the reference BVH itself, walked from the shadow ray's origin
@@ -1653,9 +1794,9 @@ DEV void tile_pixel(const RenderParams& P, int& px, int& py) {
 template <bool STATS>
 DEV void flush_counters(Cnt<STATS>& cn, DevCounters* counters) {
     if constexpr (STATS) {
-        unsigned long long v[11] = {cn.cams, cn.secs, cn.shds, cn.nodes, cn.tris, cn.sphs, cn.objs, cn.snodes, cn.stris,
-                                    cn.wnodes, cn.fallbacks};
-        for (int k = 0; k < 11; ++k) {
+        unsigned long long v[13] = {cn.cams, cn.secs, cn.shds, cn.nodes, cn.tris, cn.sphs, cn.objs, cn.snodes, cn.stris,
+                                    cn.wnodes, cn.fallbacks, cn.ewnodes, cn.efallbacks};
+        for (int k = 0; k < 13; ++k) {
             unsigned long long x = v[k];
             for (int off = 32; off > 0; off >>= 1) x += __shfl_xor(x, off);
             if ((threadIdx.x & 63) == 0 && x) atomicAdd(&((unsigned long long*)counters)[k], x);

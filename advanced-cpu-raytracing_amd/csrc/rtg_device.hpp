@@ -167,6 +167,7 @@ struct DevScene {
     const int2* __restrict__ node_up;  // per node: (parent, parent's skip); null: no up-walk
     const int* __restrict__ face_leaf; // per face: its leaf node
     int exact_shadow;                  // RTG_RENDER_EXACT_SHADOW: shadow rays take the reference walk
+    int ordered;                       // RTG_RENDER_ORDERED (plain mesh scenes with a wide BVH)
     // RTG_GUARD builds (fault hunting): table sizes and a violation bit mask (rtg_common.hpp GIDX)
     int* guard;
     int num_faces, num_textures, num_images, num_materials;
@@ -253,7 +254,8 @@ struct TreeSegs {
 // Per-launch ray/traversal counters (RTG_RENDER_COUNT_STATS).
 struct DevCounters {
     unsigned long long camera_rays, secondary_rays, shadow_rays, node_visits, tri_tests, sphere_tests,
-        object_tests, shadow_node_visits, shadow_tri_tests, shadow_wide_visits, shadow_fallbacks, pad0;
+        object_tests, shadow_node_visits, shadow_tri_tests, shadow_wide_visits, shadow_fallbacks, extend_wide_visits,
+        extend_fallbacks, pad0, pad1;
 };
 
 }  // namespace rtg

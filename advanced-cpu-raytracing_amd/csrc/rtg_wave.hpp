@@ -1,4 +1,4 @@
-// Wavefront render pipeline for scenes whose rays do not branch (no reflection /
+// Wavefront render pipeline (kernels; launched from rtg_wave_*.hip) for scenes whose rays do not branch (no reflection /
 // refraction children, no motion blur): every camera ray is one closest-hit query, and
 // every hit spawns one shadow query per light.  Per sample pass:
 //
@@ -15,6 +15,7 @@
 //
 // The float operations and their order are those of the fused kernel / the reference
 // (only unshadowed terms are summed, left to right), so both paths produce the same bits.
+#pragma once
 #include <cstdlib>
 
 #include "rtg_common.hpp"
@@ -24,9 +25,12 @@ namespace rtg {
 
 enum { BASE_FINAL = 1, BASE_ADD_ZERO = 2 };
 
-template <bool STATS, int FEAT>
-__global__ __launch_bounds__(256, RTG_TRACE_WAVES(FEAT)) void k_primary(const DevScene S, const DevCamera C, const RenderParams P,
-                                                 const int sample, const WaveBufs W, DevCounters* counters) {
+// ORD: RTG_RENDER_ORDERED (plain mesh scenes): the checked nearest-first wide walk
+// (trace_ordered), the reference walk where its check fails
+template <bool STATS, int FEAT, bool ORD = false>
+__global__ __launch_bounds__(256, ORD ? RTG_WIDE_WAVES_PLAIN : RTG_TRACE_WAVES(FEAT)) void k_primary(
+    const DevScene S, const DevCamera C, const RenderParams P, const int sample, const WaveBufs W,
+    DevCounters* counters) {
     int px, py, crow;
     tile_pixel(P, px, py, crow);
     Cnt<STATS> cn;
@@ -37,7 +41,15 @@ __global__ __launch_bounds__(256, RTG_TRACE_WAVES(FEAT)) void k_primary(const De
         Ray ray = camera_ray(C, px, py, key, mbTime);
         cn.cam();
         Hit h;
-        trace<false, STATS, FEAT, RTG_PRIMARY_PACKET != 0 && !(FEAT & FEAT_BIGLEAF)>(S, ray, mbTime, INFINITY, INFINITY, h, cn);
+        if constexpr (ORD) {
+            if (!trace_ordered<STATS>(S, ray, h, cn)) {
+                cn.efallback();
+                trace<false, STATS, FEAT>(S, ray, mbTime, INFINITY, INFINITY, h, cn);
+            }
+        } else {
+            trace<false, STATS, FEAT, RTG_PRIMARY_PACKET != 0 && !(FEAT & FEAT_BIGLEAF)>(S, ray, mbTime, INFINITY,
+                                                                                       INFINITY, h, cn);
+        }
         const int i = crow * C.width + px;
         W.hit_t[i] = h.t;
         W.hit_obj[i] = h.obj;
@@ -332,43 +344,26 @@ __global__ __launch_bounds__(256, FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(
     flush_counters<STATS>(cn, counters);
 }
 
-__global__ __launch_bounds__(256) void k_resolve(const DevCamera C, const RenderParams P, const int sample,
-                                                 const WaveBufs W, const PassOut O) {
-    const int i = blockIdx.x * 256 + threadIdx.x;
-    const int npix = P.part_rows * C.width;
-    if (i >= npix) return;
-    const int pixel = part_pixel(P, C.width, i);
-    const float4 b = W.base[i];
-    const int flags = __float_as_int(b.w);
-    f3 color = mk(b.x, b.y, b.z);
-    if (!(flags & BASE_FINAL)) {
-        f3 sum = mk(0, 0, 0);
-        const int s0 = i * W.num_slots;
-        for (int l = 0; l < W.num_slots; ++l)
-            if (!W.occ[s0 + l]) {
-                const float4 t = W.term[s0 + l];
-                sum = add(sum, mk(t.x, t.y, t.z));
-            }
-        color = add(color, sum);
-        if (flags & BASE_ADD_ZERO) color = add(color, mk(0, 0, 0));   // depth-0 mirror/dielectric/conductor
-    }
-    finish_pixel(C, P, sample, O, pixel, color);
-}
 
-static bool no_fused_shade() {
-    static const bool v = std::getenv("RTG_NO_FUSED_SHADE") != nullptr;
-    return v;
-}
 
-template <bool STATS, int FEAT, int SK>
-static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W,
-                                float* hdr, unsigned char* l, DevCounters* cnt, hipStream_t st, hipEvent_t* ev,
-                                int* layout) {
+// Shading / resolve launches (rtg_wave_shade.hip): k_shade<STATS, sk, SH_ONE or SH_GENERAL>
+// for the scene's shading variant, and k_resolve.
+hipError_t wave_shade(bool stats, int sk, bool one, const DevScene& S, const DevCamera& C, const RenderParams& P,
+                      int sample, const WaveBufs& W, const PassOut& O, DevCounters* cnt, hipStream_t st);
+void wave_resolve(const DevCamera& C, const RenderParams& P, int sample, const WaveBufs& W, const PassOut& O,
+                  hipStream_t st);
+bool no_fused_shade();
+
+// One traversal variant's pass sequence (instantiated in rtg_wave_a.hip / rtg_wave_b.hip).
+template <bool STATS, int FEAT>
+hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W, float* hdr,
+                         unsigned char* l, DevCounters* cnt, int sk, hipStream_t st, hipEvent_t* ev, int* layout) {
     const int npix = P.part_rows * C.width;
     const int nshadow = S.num_point + S.num_area + S.num_dir + S.num_spot + S.num_mesh;
-    // at most one light: k_shade / k_shadow_one finish the pixels (no k_resolve); SK variants
-    // for this case only (every other scene takes the general k_shade)
+    // at most one light: k_shade / k_shadow_one finish the pixels (no k_resolve); shading
+    // variants for this case only (every other scene takes the general k_shade)
     const bool one = W.num_slots <= 1 && W.q_pay != nullptr;
+    if (!one) sk = SK_ALL;
     // fast any-hit walk (RTG_SHADOW_MODE) unless RTG_RENDER_EXACT_SHADOW asks for the
     // reference walk
     const bool fast = (RTG_SHADOW_MODE == 3 ? S.wnodes != nullptr
@@ -376,7 +371,7 @@ static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const Ren
                       !(FEAT & FEAT_BIGLEAF) && !S.exact_shadow;
     // shading fused with the shadow ray: plain shading, the fast any-hit walk (RTG_NO_FUSED_SHADE=1
     // keeps the queue: experiments)
-    const bool fused = SK == 0 && fast && !(FEAT & FEAT_BIGLEAF) && nshadow > 0 && !no_fused_shade();
+    const bool fused = sk == 0 && fast && !(FEAT & FEAT_BIGLEAF) && nshadow > 0 && !no_fused_shade();
     *layout = one ? (fused ? LAYOUT_WAVE_FUSED : LAYOUT_WAVE_ONE) : LAYOUT_WAVE;
     for (int s = P.sample_begin; s < P.sample_begin + P.sample_count; ++s) {
         const int first = s == P.sample_begin, last = s == P.sample_begin + P.sample_count - 1;
@@ -384,15 +379,24 @@ static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const Ren
         hipEvent_t* e5 = last ? ev : nullptr;
         hipError_t e;
         if (e5) (void)hipEventRecord(e5[0], st);
-        hipLaunchKernelGGL((k_primary<STATS, FEAT>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
+        bool ordered = false;
+        if constexpr (FEAT == 0) {
+            if (S.ordered) {
+                hipLaunchKernelGGL((k_primary<STATS, 0, true>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
+                ordered = true;
+            }
+        }
+        if (!ordered)
+            hipLaunchKernelGGL((k_primary<STATS, FEAT>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
         if (e5) (void)hipEventRecord(e5[1], st);
         if (one && fused) {
-            if constexpr (SK == 0 && !(FEAT & FEAT_BIGLEAF))
+            if constexpr (!(FEAT & FEAT_BIGLEAF))
                 hipLaunchKernelGGL((k_shade<STATS, 0, SH_FUSED, FEAT, true>), dim3(P.num_tiles), dim3(256), 0, st, S, C,
                                    P, s, W, O, cnt);
             if (e5) (void)hipEventRecord(e5[2], st);
         } else if (one) {
-            hipLaunchKernelGGL((k_shade<STATS, SK, SH_ONE>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, O, cnt);
+            e = wave_shade(STATS, sk, true, S, C, P, s, W, O, cnt, st);
+            if (e != hipSuccess) return e;
             if (e5) (void)hipEventRecord(e5[2], st);
             if (nshadow > 0) {
                 if (fast)
@@ -404,8 +408,8 @@ static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const Ren
             }
             if (e5) (void)hipEventRecord(e5[3], st);
         } else {
-            hipLaunchKernelGGL((k_shade<STATS, SK_ALL, SH_GENERAL>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, O,
-                               cnt);
+            e = wave_shade(STATS, SK_ALL, false, S, C, P, s, W, O, cnt, st);
+            if (e != hipSuccess) return e;
             if (e5) (void)hipEventRecord(e5[2], st);
             if (nshadow > 0) {
                 if (fast) {
@@ -417,7 +421,7 @@ static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const Ren
                 }
             }
             if (e5) (void)hipEventRecord(e5[3], st);
-            hipLaunchKernelGGL(k_resolve, dim3((npix + 255) / 256), dim3(256), 0, st, C, P, s, W, O);
+            wave_resolve(C, P, s, W, O, st);
             if (e5) (void)hipEventRecord(e5[4], st);
         }
         e = hipGetLastError();
@@ -427,41 +431,23 @@ static hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const Ren
 }
 
 template <int FEAT>
-static hipError_t launch_wave_f(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W,
-                                float* hdr, unsigned char* l, DevCounters* cnt, bool stats, int sk, hipStream_t st,
-                                hipEvent_t* ev, int* layout) {
-    // shading variants exist for one-light scenes only (the general k_shade otherwise)
-    if (!(W.num_slots <= 1 && W.q_pay != nullptr)) sk = SK_ALL;
-#define RTG_SK(K)                                                                      \
-    case K:                                                                            \
-        return stats ? launch_wave_t<true, FEAT, K>(S, C, P, W, hdr, l, cnt, st, ev, layout)   \
-                     : launch_wave_t<false, FEAT, K>(S, C, P, W, hdr, l, cnt, st, ev, layout)
-    switch (sk & SK_ALL) {
-        RTG_SK(0); RTG_SK(1); RTG_SK(2); RTG_SK(3); RTG_SK(4); RTG_SK(5); RTG_SK(6);
-        default: RTG_SK(SK_ALL);
-    }
-#undef RTG_SK
+hipError_t launch_wave_f(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W, float* hdr,
+                         unsigned char* l, DevCounters* cnt, bool stats, int sk, hipStream_t st, hipEvent_t* ev,
+                         int* layout) {
+    return stats ? launch_wave_t<true, FEAT>(S, C, P, W, hdr, l, cnt, sk, st, ev, layout)
+                 : launch_wave_t<false, FEAT>(S, C, P, W, hdr, l, cnt, sk, st, ev, layout);
 }
-
-hipError_t launch_wave(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W, float* hdr,
-                       unsigned char* l, DevCounters* cnt, bool stats, int feat, int sk, hipStream_t stream,
-                       hipEvent_t* ev, int* layout) {
-    // traversal variants: meshes only (identity transforms) / + spheres / everything,
-    // each with the sequential or the cooperative (large-leaf) BVH walk
-    const bool big = (feat & FEAT_BIGLEAF) != 0;
-    const int base = feat & ~FEAT_BIGLEAF;
-#define RTG_WAVE(F) return launch_wave_f<F>(S, C, P, W, hdr, l, cnt, stats, sk, stream, ev, layout)
-    if (base == 0) {
-        if (big) RTG_WAVE(FEAT_BIGLEAF);
-        RTG_WAVE(0);
-    }
-    if (base == FEAT_SPHERE) {
-        if (big) RTG_WAVE(FEAT_SPHERE | FEAT_BIGLEAF);
-        RTG_WAVE(FEAT_SPHERE);
-    }
-    if (big) RTG_WAVE(FEAT_ALL);
-    RTG_WAVE(FEAT_ALL & ~FEAT_BIGLEAF);
-#undef RTG_WAVE
-}
+// traversal variants, split over two translation units (compile time)
+#define RTG_WAVE_DECL(F)                                                                                          \
+    extern template hipError_t launch_wave_f<F>(const DevScene&, const DevCamera&, const RenderParams&,             \
+                                                const WaveBufs&, float*, unsigned char*, DevCounters*, bool, int, \
+                                                hipStream_t, hipEvent_t*, int*);
+RTG_WAVE_DECL(0)
+RTG_WAVE_DECL(FEAT_SPHERE)
+RTG_WAVE_DECL(FEAT_BIGLEAF)
+RTG_WAVE_DECL(FEAT_SPHERE | FEAT_BIGLEAF)
+RTG_WAVE_DECL(FEAT_ALL)
+RTG_WAVE_DECL(FEAT_ALL & ~FEAT_BIGLEAF)
+#undef RTG_WAVE_DECL
 
 }  // namespace rtg

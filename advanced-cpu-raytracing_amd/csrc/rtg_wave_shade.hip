@@ -1,0 +1,87 @@
+// Wavefront shading kernels (k_shade variants, k_resolve) and the pipeline dispatcher.
+#include "rtg_wave.hpp"
+
+namespace rtg {
+
+__global__ __launch_bounds__(256) void k_resolve(const DevCamera C, const RenderParams P, const int sample,
+                                                 const WaveBufs W, const PassOut O) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int npix = P.part_rows * C.width;
+    if (i >= npix) return;
+    const int pixel = part_pixel(P, C.width, i);
+    const float4 b = W.base[i];
+    const int flags = __float_as_int(b.w);
+    f3 color = mk(b.x, b.y, b.z);
+    if (!(flags & BASE_FINAL)) {
+        f3 sum = mk(0, 0, 0);
+        const int s0 = i * W.num_slots;
+        for (int l = 0; l < W.num_slots; ++l)
+            if (!W.occ[s0 + l]) {
+                const float4 t = W.term[s0 + l];
+                sum = add(sum, mk(t.x, t.y, t.z));
+            }
+        color = add(color, sum);
+        if (flags & BASE_ADD_ZERO) color = add(color, mk(0, 0, 0));   // depth-0 mirror/dielectric/conductor
+    }
+    finish_pixel(C, P, sample, O, pixel, color);
+}
+
+bool no_fused_shade() {
+    static const bool v = std::getenv("RTG_NO_FUSED_SHADE") != nullptr;
+    return v;
+}
+
+template <bool STATS>
+static hipError_t wave_shade_t(int sk, bool one, const DevScene& S, const DevCamera& C, const RenderParams& P,
+                               int s, const WaveBufs& W, const PassOut& O, DevCounters* cnt, hipStream_t st) {
+    if (!one) {
+        hipLaunchKernelGGL((k_shade<STATS, SK_ALL, SH_GENERAL>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, O,
+                           cnt);
+        return hipGetLastError();
+    }
+#define RTG_SK(K)                                                                                                  \
+    case K:                                                                                                        \
+        hipLaunchKernelGGL((k_shade<STATS, K, SH_ONE>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, O, cnt); \
+        break
+    switch (sk & SK_ALL) {
+        RTG_SK(0); RTG_SK(1); RTG_SK(2); RTG_SK(3); RTG_SK(4); RTG_SK(5); RTG_SK(6);
+        default: RTG_SK(SK_ALL);
+    }
+#undef RTG_SK
+    return hipGetLastError();
+}
+
+hipError_t wave_shade(bool stats, int sk, bool one, const DevScene& S, const DevCamera& C, const RenderParams& P,
+                      int sample, const WaveBufs& W, const PassOut& O, DevCounters* cnt, hipStream_t st) {
+    return stats ? wave_shade_t<true>(sk, one, S, C, P, sample, W, O, cnt, st)
+                 : wave_shade_t<false>(sk, one, S, C, P, sample, W, O, cnt, st);
+}
+
+void wave_resolve(const DevCamera& C, const RenderParams& P, int sample, const WaveBufs& W, const PassOut& O,
+                  hipStream_t st) {
+    const int npix = P.part_rows * C.width;
+    hipLaunchKernelGGL(k_resolve, dim3((npix + 255) / 256), dim3(256), 0, st, C, P, sample, W, O);
+}
+
+hipError_t launch_wave(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W, float* hdr,
+                       unsigned char* l, DevCounters* cnt, bool stats, int feat, int sk, hipStream_t stream,
+                       hipEvent_t* ev, int* layout) {
+    // traversal variants: meshes only (identity transforms) / + spheres / everything,
+    // each with the sequential or the cooperative (large-leaf) BVH walk
+    const bool big = (feat & FEAT_BIGLEAF) != 0;
+    const int base = feat & ~FEAT_BIGLEAF;
+#define RTG_WAVE(F) return launch_wave_f<F>(S, C, P, W, hdr, l, cnt, stats, sk, stream, ev, layout)
+    if (base == 0) {
+        if (big) RTG_WAVE(FEAT_BIGLEAF);
+        RTG_WAVE(0);
+    }
+    if (base == FEAT_SPHERE) {
+        if (big) RTG_WAVE(FEAT_SPHERE | FEAT_BIGLEAF);
+        RTG_WAVE(FEAT_SPHERE);
+    }
+    if (big) RTG_WAVE(FEAT_ALL);
+    RTG_WAVE(FEAT_ALL & ~FEAT_BIGLEAF);
+#undef RTG_WAVE
+}
+
+}  // namespace rtg

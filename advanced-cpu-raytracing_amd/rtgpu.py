@@ -30,6 +30,7 @@ RTG_RENDER_FUSED = 4
 RTG_RENDER_TIMING = 8
 RTG_RENDER_TREE = 16
 RTG_RENDER_EXACT_SHADOW = 32
+RTG_RENDER_ORDERED = 64
 RTG_LOAD_DEVICE_BVH = 1
 
 
@@ -62,7 +63,7 @@ class Stats(ctypes.Structure):
     _fields_ = [(n, ctypes.c_uint64) for n in (
         "camera_rays", "secondary_rays", "shadow_rays", "node_visits", "tri_tests",
         "sphere_tests", "object_tests", "shadow_node_visits", "shadow_tri_tests", "shadow_wide_visits",
-        "shadow_fallbacks")]
+        "shadow_fallbacks", "extend_wide_visits", "extend_fallbacks")]
 
     def as_dict(self) -> dict:
         return {n: int(getattr(self, n)) for n, _ in self._fields_}

@@ -440,6 +440,29 @@ def main():
                 pl.close()
                 if ph:
                     ph.close()
+            if world == 1:
+                # opt-in ordered closest hit (RTG_RENDER_ORDERED): same frame, its agreement with
+                # the reference-order walk measured here (pixels whose float bits differ)
+                torch.cuda.synchronize()
+                ref_hdr = hdr.clone()
+                render(rtgpu.RTG_RENDER_ORDERED)
+                torch.cuda.synchronize()
+                n_fail = int((hdr.view(torch.int32) != ref_hdr.view(torch.int32)).any(dim=2).sum().item())
+                o_st, o_rays = frame_stats(ds, torch, lambda: render(rtgpu.RTG_RENDER_ORDERED | rtgpu.RTG_RENDER_COUNT_STATS),
+                                           lambda s: s)
+                o_el, _ = measure(lambda: render(rtgpu.RTG_RENDER_ORDERED), torch, args.steps, 1, barrier)
+                o_kt = kernel_times(ds, torch, lambda: render(rtgpu.RTG_RENDER_ORDERED | rtgpu.RTG_RENDER_TIMING),
+                                    args.steps)
+                result["ordered"] = {
+                    "mrays_s": round(o_rays * args.steps / o_el / 1e6, 2),
+                    "ms_per_frame": round(o_el / args.steps * 1e3, 4),
+                    "kernels_ms": {k: round(v, 4) for k, v in o_kt.items()},
+                    "n_fail_pixels": n_fail, "pixels": int(H * W),
+                    "wide_visits_per_camera_ray": round(o_st["extend_wide_visits"] / max(o_st["camera_rays"], 1), 2),
+                    "checked_out_rays": int(o_st["extend_fallbacks"]),
+                    "what": "opt-in RTG_RENDER_ORDERED: camera rays walk the 4-wide BVH nearest child first with a "
+                            "checked (t, object, face) minimum, the reference walk where the check fails; "
+                            "not the headline value (agreement measured, not proven)"}
 
         if rank == 0 and world == 1 and not args.no_sweep and args.config == "headline":
             sweep = {}

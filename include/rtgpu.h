@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 3
+#define RTG_ABI_VERSION 4
 
 enum rtg_status {
     RTG_OK = 0,
@@ -295,8 +295,13 @@ enum rtg_render_flags {
                                      mirror / conductor / dielectric materials (default:
                                      frames of >= 2^21 pixel-samples; it synchronises the
                                      stream once per tree level)                       */
-    RTG_RENDER_EXACT_SHADOW = 32  /* shadow rays walk the reference BVH instead of the
+    RTG_RENDER_EXACT_SHADOW = 32, /* shadow rays walk the reference BVH instead of the
                                      any-hit wide BVH (same answers; for cross-checks)  */
+    RTG_RENDER_ORDERED = 64       /* opt-in (ABI 4): camera rays of plain mesh scenes walk
+                                     the 4-wide BVH nearest child first with a checked
+                                     result (the reference walk where the check fails);
+                                     agreement with the reference order is measured, not
+                                     proven -- DESIGN.md §5                          */
 };
 
 typedef struct {
@@ -339,6 +344,10 @@ typedef struct {
                                      tests four child boxes; A/B builds only)          */
     uint64_t shadow_fallbacks;    /* shadow rays the fast any-hit walk left undecided,
                                      answered by the reference walk                    */
+    uint64_t extend_wide_visits;  /* RTG_RENDER_ORDERED: wide BVH nodes visited by
+                                     camera rays (ABI 4)                               */
+    uint64_t extend_fallbacks;    /* RTG_RENDER_ORDERED: camera rays whose check failed,
+                                     answered by the reference walk (ABI 4)           */
 } rtg_stats;
 
 /* One call per camera, replacing main.cpp:164-185 (threads -> renderThreadMain ->

@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert rtgpu.lib().rtg_abi_version() == 3
+    assert rtgpu.lib().rtg_abi_version() == 4
 
 
 def test_struct_layouts_are_plain_c(tmp_path):
@@ -45,7 +45,7 @@ def test_struct_layouts_are_plain_c(tmp_path):
     # C compiler's view of include/rtgpu.h)
     import shutil
     assert ctypes.sizeof(rtgpu.RenderOpts) == 40
-    assert ctypes.sizeof(rtgpu.Stats) == 88
+    assert ctypes.sizeof(rtgpu.Stats) == 104
     cc = shutil.which("gcc") or shutil.which("cc")
     if not cc:
         pytest.skip("no C compiler")
