@@ -649,14 +649,19 @@ void Loader::parseTextures(XmlNode* root, RefStream& stream) {   // parser.cpp:8
             std::string filename;
             stream.line(im->Attribute("id")); stream.get(id);
             stream.line(im->GetText()); stream.get(filename);
-            if (filename.find(".exr") != std::string::npos)
-                fail(RTG_ERR_UNSUPPORTED, "EXR images are not supported: " + filename);
-            Image8 img;
-            std::string err;
-            if (!load_image8("inputs/" + filename, img, err)) fail(RTG_ERR_IO, err);
             HostScene::ImageStore st;
-            st.width = img.width; st.height = img.height; st.channels = img.channels;
-            st.texels.assign(img.data.begin(), img.data.end());
+            std::string err;
+            if (filename.find(".exr") != std::string::npos) {          // HDRImage (parser.cpp:103-107)
+                if (!load_exr("inputs/" + filename, st.width, st.height, st.texels, err))
+                    fail(err.find("not supported") != std::string::npos ? RTG_ERR_UNSUPPORTED : RTG_ERR_IO, err);
+                st.channels = 3;
+                st.is_hdr = 1;
+            } else {                                                    // LDRImage (parser.cpp:110)
+                Image8 img;
+                if (!load_image8("inputs/" + filename, img, err)) fail(RTG_ERR_IO, err);
+                st.width = img.width; st.height = img.height; st.channels = img.channels;
+                st.texels.assign(img.data.begin(), img.data.end());
+            }
             st.id = id;
             S.imageStore.push_back(std::move(st));
             imageIds.push_back(id);
@@ -1108,7 +1113,7 @@ void HostScene::finalize() {
         rtg_image im;
         std::memset(&im, 0, sizeof(im));
         im.id = st.id; im.width = st.width; im.height = st.height; im.channels = st.channels;
-        im.is_hdr = 0;
+        im.is_hdr = st.is_hdr;
         im.texels = st.texels.data();
         images.push_back(im);
     }

@@ -11,7 +11,7 @@ namespace rtg {
 // Owner of every array an rtg_scene_desc points into.
 struct HostScene {
     struct ImageStore {
-        int id = 0, width = 0, height = 0, channels = 0;
+        int id = 0, width = 0, height = 0, channels = 0, is_hdr = 0;
         std::vector<float> texels;
     };
     int background[3] = {0, 0, 0};

@@ -105,6 +105,7 @@ struct rtg_scene {
     DevBuf<rtg::DevSpotLight> spot_lights;
     DevBuf<rtg::DevCounters> counters;
     DevBuf<rtg::WNode> wnodes;
+    DevBuf<rtg::CWNode> cwnodes;
     DevBuf<int2> node_up;
     DevBuf<int> face_leaf;
     DevBuf<int> guard;                // RTG_GUARD builds: index-violation bits
@@ -338,6 +339,70 @@ static int build_wide(const std::vector<float4>& nodes, int root, std::vector<rt
     return rootIdx;
 }
 
+// Compressed copy of a wide node (rtg_device.hpp CWNode).  Per axis, a grid of spacing 2^e
+// over the children's extent with one spare cell on each side (251 cells for the extent):
+// each child's lo / hi plane goes to the grid line at least one cell beyond it, so the
+// dequantised box contains the child box with a cell to spare -- the margin the device's
+// rounding needs (walk_cwide_any).  Checked in exact double arithmetic; a grid too coarse
+// for that (cannot happen for float inputs) doubles the spacing.
+static rtg::CWNode compress_wide(const rtg::WNode& W) {
+    rtg::CWNode C;
+    std::memset(&C, 0, sizeof(C));
+    const float* lo[3] = {&W.lox.x, &W.loy.x, &W.loz.x};
+    const float* hi[3] = {&W.hix.x, &W.hiy.x, &W.hiz.x};
+    const int* ch = &W.child.x;
+    float* org = &C.org.x;
+    unsigned qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
+    int ebits = 0;
+    for (int a = 0; a < 3; ++a) {
+        double plo = INFINITY, phi = -INFINITY;
+        for (int k = 0; k < 4; ++k)
+            if (ch[k] != rtg::WCHILD_EMPTY) { plo = std::min(plo, (double)lo[a][k]); phi = std::max(phi, (double)hi[a][k]); }
+        if (!(plo <= phi)) plo = phi = 0.0;
+        const double ext = phi - plo;
+        int e;
+        if (ext > 0) e = (int)std::ceil(std::log2(ext / 251.0));
+        else e = (plo != 0.0 ? std::ilogb(plo) : -40) - 16;
+        e = std::max(-100, std::min(100, e));
+        for (;; ++e) {
+            const double sc = std::ldexp(1.0, e);
+            double ov = plo - 2.0 * sc;
+            float of = (float)ov;
+            if ((double)of > ov) of = std::nextafter(of, -INFINITY);
+            bool ok = true;
+            unsigned ql = 0, qh = 0;
+            for (int k = 0; k < 4; ++k) {
+                unsigned l = 255, h = 0;                 // empty slot: an inverted box
+                if (ch[k] != rtg::WCHILD_EMPTY) {
+                    const double fl = std::floor(((double)lo[a][k] - of) / sc) - 1.0;
+                    const double fh = std::ceil(((double)hi[a][k] - of) / sc) + 1.0;
+                    if (fl < 0.0 || fh > 255.0 || !((double)of + fl * sc <= (double)lo[a][k] - sc) ||
+                        !((double)of + fh * sc >= (double)hi[a][k] + sc)) {
+                        ok = false;
+                        break;
+                    }
+                    l = (unsigned)fl;
+                    h = (unsigned)fh;
+                }
+                ql |= l << (8 * k);
+                qh |= h << (8 * k);
+            }
+            if (ok || e >= 100) {
+                org[a] = of;
+                qlo[a] = ql;
+                qhi[a] = qh;
+                ebits |= (e + 128) << (8 * a);
+                break;
+            }
+        }
+    }
+    std::memcpy(&C.org.w, &ebits, 4);
+    C.qxy = make_uint4(qlo[0], qhi[0], qlo[1], qhi[1]);
+    C.qz = make_uint4(qlo[2], qhi[2], 0u, 0u);
+    C.child = W.child;
+    return C;
+}
+
 int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     if (!d || !out) return set_err(RTG_ERR_INVALID, "null argument");
     *out = nullptr;
@@ -512,7 +577,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     std::vector<int2> nodeUp;
     std::vector<int> faceLeaf;
     for (int i = 0; i < d->num_objects; ++i) objs[i].wroot = -1;
-    if (!std::getenv("RTG_NO_FAST_SHADOW") && d->num_meshes > 0 && (RTG_SHADOW_MODE == 2 || RTG_SHADOW_MODE == 3)) {
+    if (!std::getenv("RTG_NO_FAST_SHADOW") && d->num_meshes > 0 && RTG_SHADOW_MODE >= 2) {
         std::vector<float4> dn;
         std::vector<int2> dx;
         if (gpuBuild) {
@@ -542,9 +607,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
                     for (int f = first; f < first + cnt; ++f) faceLeaf[f] = p;
                 }
             }
-#if RTG_SHADOW_MODE == 3
             if (meshEnd[m] > meshBegin[m]) wroot[m] = build_wide(nd, meshBegin[m], wide);
-#endif
         }
         for (int i = 0; i < d->num_objects; ++i)
             objs[i].wroot = d->objects[i].kind != RTG_OBJ_SPHERE ? wroot[d->objects[i].mesh] : -1;
@@ -731,6 +794,11 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     HIP_TRY(sc->spot_lights.upload(sls)); HIP_TRY(sc->env_images.upload(envs));
     HIP_TRY(sc->mesh_lights.upload(mls)); HIP_TRY(sc->light_faces.upload(lfs));
     HIP_TRY(sc->wnodes.upload(wide));
+    if (RTG_SHADOW_MODE == 4) {
+        std::vector<rtg::CWNode> cw(wide.size());
+        for (size_t i = 0; i < wide.size(); ++i) cw[i] = compress_wide(wide[i]);
+        HIP_TRY(sc->cwnodes.upload(cw));
+    }
     HIP_TRY(sc->node_up.upload(nodeUp));
     HIP_TRY(sc->face_leaf.upload(faceLeaf));
     std::vector<rtg::DevCounters> zero(1);
@@ -765,6 +833,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     for (int k = 0; k < 3; ++k) S.background[k] = d->background[k];
     S.coop = (sc->feat & rtg::FEAT_BIGLEAF) ? 1 : 0;
     S.wnodes = wide.empty() ? nullptr : sc->wnodes.p;
+    S.cwnodes = wide.empty() || RTG_SHADOW_MODE != 4 ? nullptr : sc->cwnodes.p;
     S.num_faces = (int)d->num_faces;
     S.num_textures = d->num_textures;
     S.num_images = d->num_images;

@@ -845,10 +845,114 @@ DEV int walk_wide_any(const DevScene& S, int node, const Ray& lr, float minT0, f
     return undecided ? -1 : 0;
 }
 
+// The same walk on the compressed nodes (CWNode).  Per node and axis the grid spacing and the
+// origin become a = 2^e / d and b = (org - o) / d, and each child plane is t = fma(q, a, b)
+// for its 8-bit index q (the near / far plane rows picked once per node by the direction's
+// sign).  Conservative: the dequantised box contains the child box with one grid cell to
+// spare on every side (host side, compress_wide); the computed t of a plane differs from
+// (plane - o) / d by at most ~2^-23 (|b| + |q a|) + 2^-23 |t| (the rcp, two roundings in b,
+// one in the fma), and |b| <= |t| + 255 |a|, so everything but the |t|-relative part is far
+// inside the spare cell, and the |t|-relative part is covered by 2^-19 margins below.
+// Leaf slots carry the reference node, whose record gives the face range (one load per
+// leaf reached); the exact leaf decisions are those of walk_wide_any.
+template <bool STATS>
+DEV int walk_cwide_any(const DevScene& S, int node, const Ray& lr, float minT0, float limit, bool inst_conf,
+                       Cnt<STATS>& c) {
+    __shared__ int stack[RTG_WIDE_STACK][256];
+    const RayRcp q = ray_rcp(lr);
+    if (!q.fast) return -1;                          // zero / tiny direction component: reference walk
+    const float minTc = minT0 * (1.0f + 0x1p-19f);
+    const bool nx = q.ix < 0.f, ny = q.iy < 0.f, nz = q.iz < 0.f;
+    const int tid = threadIdx.x;
+    int sp = 0;
+    bool undecided = false;
+    while (true) {
+        const CWNode* N = S.cwnodes + node;
+        const float4 org = N->org;
+        const uint4 qxy = N->qxy;
+        const uint2 qz = *(const uint2*)&N->qz;
+        const int4 ch = N->child;
+        c.wnode();
+        const int eb = __float_as_int(org.w);
+        const float ax = __builtin_ldexpf(q.ix, (eb & 255) - 128);
+        const float ay = __builtin_ldexpf(q.iy, ((eb >> 8) & 255) - 128);
+        const float az = __builtin_ldexpf(q.iz, ((eb >> 16) & 255) - 128);
+        const float bx = (org.x - lr.o.x) * q.ix, by = (org.y - lr.o.y) * q.iy, bz = (org.z - lr.o.z) * q.iz;
+        // near / far plane rows by the sign of the direction
+        const unsigned nX = nx ? qxy.y : qxy.x, fX = nx ? qxy.x : qxy.y;
+        const unsigned nY = ny ? qxy.w : qxy.z, fY = ny ? qxy.z : qxy.w;
+        const unsigned nZ = nz ? qz.y : qz.x, fZ = nz ? qz.x : qz.y;
+        float tn[4];
+        bool h[4];
+        const int cidx[4] = {ch.x, ch.y, ch.z, ch.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int sh = 8 * k;
+            const float tnx = __builtin_fmaf((float)((nX >> sh) & 255u), ax, bx);
+            const float tfx = __builtin_fmaf((float)((fX >> sh) & 255u), ax, bx);
+            const float tny = __builtin_fmaf((float)((nY >> sh) & 255u), ay, by);
+            const float tfy = __builtin_fmaf((float)((fY >> sh) & 255u), ay, by);
+            const float tnz = __builtin_fmaf((float)((nZ >> sh) & 255u), az, bz);
+            const float tfz = __builtin_fmaf((float)((fZ >> sh) & 255u), az, bz);
+            const float tmin = fmaxf(fmaxf(tnx, tny), tnz);
+            const float tmax = fminf(fminf(tfx, tfy), tfz);
+            tn[k] = tmin;
+            h[k] = (tmax > -1e-30f) & (tmax >= tmin * (1.0f - 0x1p-19f) - 1e-30f) & (tmin < minTc) &
+                   (cidx[k] != WCHILD_EMPTY);
+        }
+        int next = -1;
+        float nextT = INFINITY;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            if (!h[k]) continue;
+            const int cr = cidx[k];
+            if (cr >= 0) {
+                int spill = cr;
+                if (tn[k] < nextT) {
+                    spill = next;
+                    next = cr;
+                    nextT = tn[k];
+                }
+                if (spill >= 0) {
+                    if (sp < RTG_WIDE_STACK) stack[sp++][tid] = spill;
+                    else undecided = true;
+                }
+                continue;
+            }
+            const int ref = -2 - cr;
+            const float4 b = S.nodes[2 * ref + 1];
+            const int lf = __float_as_int(b.w);
+            int first = lf >> 8, cnt = lf & 255;
+            if (lf == LEAF_EXT) {
+                const int2 e = S.node_ext[ref];
+                first = e.x;
+                cnt = e.y;
+            }
+            for (int f = first; f < first + cnt; ++f) {
+                c.template tri<true>();
+                float t;
+                if (!tri_test_fast(S, f, lr, limit, t)) continue;
+                // exact decisions on the leaf's own (reference) box
+                const float4 a = S.nodes[2 * ref];
+                if (!box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, minT0)) break;   // leaf unreachable
+                if (inst_conf && box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, limit)) return 1;
+                undecided = true;
+            }
+        }
+        if (next >= 0) {
+            node = next;
+            continue;
+        }
+        if (sp == 0) break;
+        node = stack[--sp][tid];
+    }
+    return undecided ? -1 : 0;
+}
+
 // CastShadowRay on the wide BVH: objects in any order (the answer is a boolean), spheres
 // exactly (a sphere hit with t < limit is accepted at any minT_cur >= limit, one with
 // t >= limit never decides).  Returns 1 / 0 / -1 (undecided: run trace<true>).
-template <bool STATS, int FEAT>
+template <bool STATS, int FEAT, bool CW = false>
 DEV int trace_any_wide(const DevScene& S, const Ray& r, float minT0, float limit, Cnt<STATS>& c) {
     const RayRcp rq = (FEAT & FEAT_INSTANCE) ? ray_rcp(r) : RayRcp{};
     if ((FEAT & FEAT_INSTANCE) && !rq.fast) return -1;
@@ -878,7 +982,8 @@ DEV int trace_any_wide(const DevScene& S, const Ray& r, float minT0, float limit
             conf = box_hit_fast(ob.bmin[0], ob.bmin[1], ob.bmin[2], ob.bmax[0], ob.bmax[1], ob.bmax[2], r, rq, limit);
         }
         const Ray lr = (FEAT & FEAT_XFORM) ? trav_ray(ob, r, 0.f) : r;
-        const int res = walk_wide_any<STATS>(S, ob.wroot, lr, minT0, limit, conf, c);
+        const int res = CW ? walk_cwide_any<STATS>(S, ob.wroot, lr, minT0, limit, conf, c)
+                           : walk_wide_any<STATS>(S, ob.wroot, lr, minT0, limit, conf, c);
         if (res > 0) return 1;
         undecided |= res < 0;
     }
@@ -1831,6 +1936,8 @@ DEV bool shadow_occluded(const DevScene& S, const WaveBufs& W, size_t q, float4 
         res = trace_any_up<STATS, FEAT>(S, r, o.w, d.w, sobj, sface, cn);
 #elif RTG_SHADOW_MODE == 3
         res = trace_any_wide<STATS, FEAT>(S, r, o.w, d.w, cn);
+#elif RTG_SHADOW_MODE == 4
+        res = trace_any_wide<STATS, FEAT, true>(S, r, o.w, d.w, cn);
 #else
         Hit h;
         res = trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;

@@ -55,8 +55,20 @@ struct WNode {
     int4 leaf;                      // leaf slots: (first << 8) | count, or LEAF_EXT (node_ext of the reference node)
 };
 enum : int { WCHILD_EMPTY = -1 };
+// The same node compressed to 64 B (two per cache line; RTG_SHADOW_MODE 4, an A/B build): each child box on
+// a per-node grid -- origin org.xyz, spacing 2^e per axis -- as 8-bit plane indices padded one
+// cell outward (so the dequantised box contains the child box with a cell to spare, which
+// covers the rounding of the device's fma(q, 2^e / d, (org - o) / d)), child j in byte j.
+// Leaf slots carry only the reference node (-2 - ref); its record gives the face range.
+struct CWNode {
+    float4 org;                     // w: int bits (e_x + 128) | (e_y + 128) << 8 | (e_z + 128) << 16
+    uint4 qxy;                      // lo.x, hi.x, lo.y, hi.y
+    uint4 qz;                       // lo.z, hi.z, 0, 0
+    int4 child;                     // as WNode
+};
 // Shadow-ray walk of the wavefront pipeline's k_shadow (rtg_common.hpp): 3 = any-hit on the
-// 4-wide BVH (trace_any_wide; undecided rays take the reference walk: default), 0 = the
+// 4-wide BVH (trace_any_wide; undecided rays take the reference walk: default), 4 = the same on
+// the compressed 64-B nodes (measured slower: 0.311 vs 0.273 ms), 0 = the
 // reference walk per lane, 1 = the same walks as a wave packet (walk_bvh_packet), 2 = any-hit
 // climb from the ray's origin leaf (trace_any_up).  The ray-tree pipeline's k_shadow always
 // uses the per-lane reference walk (its secondary rays are incoherent: modes 1-3 measured
@@ -164,6 +176,7 @@ struct DevScene {
     int background[3];
     int coop;                        // the scene has large leaves (FEAT_BIGLEAF)
     const WNode* __restrict__ wnodes;  // any-hit wide BVH (null: shadow rays take the reference walk)
+    const CWNode* __restrict__ cwnodes; // the same, compressed (same node indices)
     const int2* __restrict__ node_up;  // per node: (parent, parent's skip); null: no up-walk
     const int* __restrict__ face_leaf; // per face: its leaf node
     int exact_shadow;                  // RTG_RENDER_EXACT_SHADOW: shadow rays take the reference walk

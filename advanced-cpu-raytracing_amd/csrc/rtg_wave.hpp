@@ -366,7 +366,8 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
     if (!one) sk = SK_ALL;
     // fast any-hit walk (RTG_SHADOW_MODE) unless RTG_RENDER_EXACT_SHADOW asks for the
     // reference walk
-    const bool fast = (RTG_SHADOW_MODE == 3 ? S.wnodes != nullptr
+    const bool fast = (RTG_SHADOW_MODE == 4 ? S.cwnodes != nullptr
+                       : RTG_SHADOW_MODE == 3 ? S.wnodes != nullptr
                                             : RTG_SHADOW_MODE == 2 ? S.node_up != nullptr : S.nodes != nullptr) &&
                       !(FEAT & FEAT_BIGLEAF) && !S.exact_shadow;
     // shading fused with the shadow ray: plain shading, the fast any-hit walk (RTG_NO_FUSED_SHADE=1

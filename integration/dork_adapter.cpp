@@ -26,6 +26,7 @@
 #include "imageTexture.h"
 #include "perlinTexture.h"
 #include "LDRImage.h"
+#include "HDRImage.h"
 #include "brdfBlinnPhong.h"
 #include "brdfModifiedBlinnPhong.h"
 #include "brdfModifiedPhong.h"
@@ -130,18 +131,22 @@ int desc_from_scene(Scene& S, DescOwner& D, std::string& err) {
         o.cos_half_coverage = l->cosHalfCoverage; o.cos_half_falloff = l->cosHalfFalloff;
         D.spot_lights.push_back(o);
     }
-    // ---- images (LDRImage.h: raw 0..255 bytes; HDR / EXR images are outside the GPU path)
+    // ---- images (LDRImage.h: raw 0..255 bytes; HDRImage.h: LoadEXR's R, G, B floats)
     for (Image* im : S.images) {
-        auto* ldr = dynamic_cast<LDRImage*>(im);
-        if (!ldr) {
-            err = "image " + std::to_string(im->id) + ": HDR (EXR) images are not supported";
-            return RTG_ERR_UNSUPPORTED;
-        }
-        const size_t n = (size_t)ldr->width * ldr->height * ldr->channels;
-        D.texels.emplace_back(ldr->image, ldr->image + n);
         rtg_image o;
         std::memset(&o, 0, sizeof(o));
-        o.id = ldr->id; o.width = ldr->width; o.height = ldr->height; o.channels = ldr->channels;
+        if (auto* ldr = dynamic_cast<LDRImage*>(im)) {
+            const size_t n = (size_t)ldr->width * ldr->height * ldr->channels;
+            D.texels.emplace_back(ldr->image, ldr->image + n);
+            o.id = ldr->id; o.width = ldr->width; o.height = ldr->height; o.channels = ldr->channels;
+        } else if (auto* hdr = dynamic_cast<HDRImage*>(im)) {
+            D.texels.emplace_back(hdr->src.begin(), hdr->src.end());
+            o.id = hdr->id; o.width = hdr->width; o.height = hdr->height; o.channels = 3;
+            o.is_hdr = 1;
+        } else {
+            err = "image " + std::to_string(im->id) + ": unknown image class";
+            return RTG_ERR_UNSUPPORTED;
+        }
         D.images.push_back(o);
     }
     for (size_t i = 0; i < D.images.size(); ++i) D.images[i].texels = D.texels[i].data();

@@ -1253,4 +1253,14 @@ int oracle_tonemap(const float* hdr, int width, int height, float key, float bur
     return 0;
 }
 
+// Test helper: image i of a parsed description (texels as the loader stored them, for the
+// image-decoder parity tests).  info = {width, height, channels, is_hdr}; out may be null.
+int oracle_image(const rtg_scene_desc* d, int i, int32_t* info, float* out) {
+    if (!d || i < 0 || i >= d->num_images) return -1;
+    const rtg_image& im = d->images[i];
+    info[0] = im.width; info[1] = im.height; info[2] = im.channels; info[3] = im.is_hdr;
+    if (out) std::memcpy(out, im.texels, sizeof(float) * (size_t)im.width * im.height * im.channels);
+    return 0;
+}
+
 }  // extern "C"

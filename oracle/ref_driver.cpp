@@ -17,6 +17,10 @@
 //       (rows [t*(H/T), (t+1)*(H/T)) per thread; spawn -> join), spp==1 per pixel via
 //       RenderPixel, and the reference-equivalent span main.cpp:138-199 (Raytracer copy +
 //       render + PNG encode); prints one JSON line with the per-rep seconds of both.
+//   refdriver imgdump <image file> <out.bin>
+//       The reference's own image classes as parser.cpp:103-110 picks them: HDRImage (tinyexr
+//       LoadEXR) for a ".exr" name, else LDRImage (stbi_load).  Writes "RTGI" int32 w, h,
+//       channels, is_hdr, then w*h*channels float32 (the texel values GetSample reads).
 //   refdriver tonemap <in.bin> <key> <burn%> <saturation> <gamma> <out.bin>
 //       The reference's own Tonemapper::Tonemap (tonemapper.h:28-60) on an "RTGF" float
 //       image (as dump writes); writes "RTGL" int32 w, int32 h, w*h*3 uint8 (the LDR
@@ -35,8 +39,38 @@
 #include <vector>
 
 #include "raytracer.hpp"
+#undef STB_IMAGE_IMPLEMENTATION          // emitted once above (raytracer.hpp -> image.h)
+#include "LDRImage.h"
 
 using namespace DorkTracer;
+
+static int imgdump(const char* file, const char* out) {
+    std::string name(file);
+    int w = 0, h = 0, c = 0, hdr = 0;
+    std::vector<float> t;
+    if (name.find(".exr") != std::string::npos) {
+        HDRImage im(name, 0);
+        w = im.width; h = im.height; c = 3; hdr = 1;
+        t.assign(im.src.begin(), im.src.end());
+    } else {
+        struct Peek : LDRImage {               // the loaded bytes (protected members)
+            using LDRImage::LDRImage;
+            const unsigned char* bytes() const { return image; }
+            int nch() const { return channels; }
+        } im(name, 0);
+        if (!im.bytes()) return 1;
+        w = im.width; h = im.height; c = im.nch();
+        t.assign(im.bytes(), im.bytes() + (size_t)w * h * c);
+    }
+    FILE* f = std::fopen(out, "wb");
+    if (!f) { std::perror(out); return 1; }
+    int32_t hd[4] = {w, h, c, hdr};
+    std::fwrite("RTGI", 1, 4, f);
+    std::fwrite(hd, 4, 4, f);
+    std::fwrite(t.data(), 4, t.size(), f);
+    std::fclose(f);
+    return 0;
+}
 
 static int dump(const char* xml, const char* out, int ci) {
     Scene scene;
@@ -174,6 +208,7 @@ int main(int argc, char** argv) {
     if (argc >= 8 && !std::strcmp(argv[1], "tonemap"))
         return tonemap(argv[2], std::atof(argv[3]), std::atof(argv[4]), std::atof(argv[5]), std::atof(argv[6]), argv[7]);
     if (argc >= 4 && !std::strcmp(argv[1], "dump")) return dump(argv[2], argv[3], argc > 4 ? std::atoi(argv[4]) : 0);
+    if (argc >= 4 && !std::strcmp(argv[1], "imgdump")) return imgdump(argv[2], argv[3]);
     if (argc >= 5 && !std::strcmp(argv[1], "dumpavg"))
         return dumpavg(argv[2], argv[3], std::atoi(argv[4]), argc > 5 ? std::atoi(argv[5]) : 0);
     if (argc >= 5 && !std::strcmp(argv[1], "bench"))

@@ -57,6 +57,9 @@ FIXTURES = {
     "synth_10k": ("generated", 256, 144, "exact", None),
     "ply_quads": ("generated", 160, 120, "exact", None),
     "bump_normal": ("generated", 200, 150, "exact", None),
+    # JPEG textures (stbi_load, nearest / bilinear, replace_kd / blend_kd) and an OpenEXR
+    # background (HDRImage, tinyexr): the image-decoder fixtures of make_images.py in a scene
+    "hdr_jpeg": ("generated", 160, 120, "exact", None),
     # path tracing (raytracer.cpp:135-191): per-pixel mean of AVG_SAMPLES reference samples
     "pt_cornell": ("generated", 64, 64, "stochastic_avg", None),
     "pt_nee": ("generated", 64, 64, "stochastic_avg", None),
@@ -136,6 +139,97 @@ def make_ply_quads():
 </Scene>
 """
     with open(os.path.join(SCENES, "ply_quads.xml"), "w") as f:
+        f.write(xml)
+
+
+def make_hdr_jpeg():
+    """Two textured quads (4:2:0 baseline and progressive JPEGs) in front of an OpenEXR
+    replace_background texture; copies the decoder fixtures to scenes/inputs/."""
+    for f in ("jpg_420.jpg", "jpg_progressive.jpg", "exr_half_zip.exr"):
+        shutil.copyfile(os.path.join(HERE, "images", f), os.path.join(SCENES, "inputs", f))
+    xml = """<Scene>
+    <MaxRecursionDepth>1</MaxRecursionDepth>
+    <BackgroundColor>0 0 0</BackgroundColor>
+    <Cameras>
+        <Camera id="1">
+            <Position>0 0 6</Position>
+            <Gaze>0 0 -1</Gaze>
+            <Up>0 1 0</Up>
+            <NearPlane>-1 1 -0.75 0.75</NearPlane>
+            <NearDistance>2</NearDistance>
+            <ImageResolution>160 120</ImageResolution>
+            <ImageName>hdr_jpeg.png</ImageName>
+        </Camera>
+    </Cameras>
+    <Lights>
+        <AmbientLight>25 25 25</AmbientLight>
+        <PointLight id="1"><Position>0 2 5</Position><Intensity>900 900 900</Intensity></PointLight>
+    </Lights>
+    <Materials>
+        <Material id="1">
+            <AmbientReflectance>0.2 0.2 0.2</AmbientReflectance>
+            <DiffuseReflectance>0.8 0.8 0.8</DiffuseReflectance>
+            <SpecularReflectance>0.3 0.3 0.3</SpecularReflectance>
+            <PhongExponent>20</PhongExponent>
+        </Material>
+    </Materials>
+    <Textures>
+        <Images>
+            <Image id="1">jpg_420.jpg</Image>
+            <Image id="2">jpg_progressive.jpg</Image>
+            <Image id="3">exr_half_zip.exr</Image>
+        </Images>
+        <TextureMap id="1" type="image">
+            <ImageId>1</ImageId>
+            <DecalMode>replace_kd</DecalMode>
+            <Interpolation>bilinear</Interpolation>
+        </TextureMap>
+        <TextureMap id="2" type="image">
+            <ImageId>2</ImageId>
+            <DecalMode>blend_kd</DecalMode>
+            <Interpolation>nearest</Interpolation>
+        </TextureMap>
+        <TextureMap id="3" type="image">
+            <ImageId>3</ImageId>
+            <DecalMode>replace_background</DecalMode>
+            <Interpolation>bilinear</Interpolation>
+        </TextureMap>
+    </Textures>
+    <VertexData>
+        -2.1 -1.2 0
+        -0.1 -1.2 0
+        -0.1 1.2 0
+        -2.1 1.2 0
+        0.1 -1.0 -0.5
+        2.1 -1.0 0
+        2.1 1.0 0
+        0.1 1.0 -0.5
+    </VertexData>
+    <TexCoordData>
+        0 1
+        1 1
+        1 0
+        0 0
+        0 1
+        1 1
+        1 0
+        0 0
+    </TexCoordData>
+    <Objects>
+        <Mesh id="1">
+            <Material>1</Material>
+            <Textures>1</Textures>
+            <Faces>1 2 3 1 3 4</Faces>
+        </Mesh>
+        <Mesh id="2">
+            <Material>1</Material>
+            <Textures>2</Textures>
+            <Faces>5 6 7 5 7 8</Faces>
+        </Mesh>
+    </Objects>
+</Scene>
+"""
+    with open(os.path.join(SCENES, "hdr_jpeg.xml"), "w") as f:
         f.write(xml)
 
 
@@ -576,6 +670,8 @@ def prepare(name, src, w, h, edits):
             make_ply_quads()
         elif name == "bump_normal":
             make_bump_normal()
+        elif name == "hdr_jpeg":
+            make_hdr_jpeg()
         elif name in PT_SCENES:
             make_pt(name)
         elif name == "c2_cornell":
