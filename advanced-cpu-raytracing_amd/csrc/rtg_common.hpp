@@ -491,6 +491,9 @@ DEV bool walk_bvh(const DevScene& S, int i, const int end, const Ray& r, float& 
         if (coop) {
             const uint64_t best = coop_leaf_tests(S, coop, r, minT, coopFirst, coopCnt);
             if (coopCnt > 0) {
+                // counted as the whole leaf: the wave tests every face of it, also for any-hit
+                // rays, where the sequential walk stops at the first accepted face (so C3/C4
+                // shadow tri_tests depend on RTG_COOP_LEAF; images do not)
                 c.template tri_n<ANY>((uint32_t)coopCnt);
                 if (best != ~0ull) {
                     minT = __uint_as_float((uint32_t)(best >> 32));

@@ -128,7 +128,7 @@ struct DevLightFace {
 enum : int { LEAF_EXT = 0x7FFFFFFF };
 
 // Scene feature bits (kernel specialisation): spheres, mesh instances, any mesh with a
-// non-identity transform or motion blur, BVH leaves of more than kCoopLeaf faces.
+// non-identity transform or motion blur, BVH leaves of more than kBigLeaf faces.
 enum : int { FEAT_SPHERE = 1, FEAT_INSTANCE = 2, FEAT_XFORM = 4, FEAT_BIGLEAF = 8, FEAT_ALL = 15 };
 // Shading specialisation of the wavefront k_shade (the other kernels use SK_ALL): the scene
 // has textures or normal / bump maps (SK_TEX), BRDFs (SK_BRDF), env / spot / mesh lights

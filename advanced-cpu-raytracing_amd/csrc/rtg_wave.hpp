@@ -358,7 +358,6 @@ bool no_fused_shade();
 template <bool STATS, int FEAT>
 hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W, float* hdr,
                          unsigned char* l, DevCounters* cnt, int sk, hipStream_t st, hipEvent_t* ev, int* layout) {
-    const int npix = P.part_rows * C.width;
     const int nshadow = S.num_point + S.num_area + S.num_dir + S.num_spot + S.num_mesh;
     // at most one light: k_shade / k_shadow_one finish the pixels (no k_resolve); shading
     // variants for this case only (every other scene takes the general k_shade)
