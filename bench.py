@@ -159,24 +159,31 @@ def cpu_baseline(xml_dir, xml, rays_per_frame, reps):
 
 # ----------------------------------------------------------------------------- timing
 def measure(render, torch, steps, warmup, barrier):
+    """Wall time of exactly `steps` frames between barrier + synchronize on both sides (no
+    event records inside the timed loop: they cost ~0.01 ms per frame, tools/diag_streams.py),
+    and, from a separate untimed pass with an event pair around each frame, the mean GPU time
+    per frame."""
     stream = torch.cuda.current_stream()
     for k in range(warmup):
         render()
         torch.cuda.synchronize()
         log(f"warmup {k + 1}/{warmup}")
     torch.cuda.synchronize()
-    starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
-    ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    for k in range(steps):
+        render()
+    torch.cuda.synchronize()
+    barrier()
+    elapsed = time.perf_counter() - t0
+    starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
+    ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
     for k in range(steps):
         starts[k].record(stream)
         render()
         ends[k].record(stream)
     torch.cuda.synchronize()
-    barrier()
-    elapsed = time.perf_counter() - t0
     kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / steps
     return elapsed, kern_ms
 
