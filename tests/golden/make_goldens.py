@@ -747,6 +747,22 @@ def make_tonemap_goldens():
     print("tonemap goldens", len(out))
 
 
+# The stochastic 1-spp fixtures also get a statistical golden: the reference's per-pixel mean
+# of AVG_SAMPLES RenderPixel calls and the variance of that mean (<name>_avg.npz), against
+# which the oracle and the GPU are z-tested at many samples per pixel.
+STOCH_AVG = ("area_light", "env_light", "dof_motion", "c3_blob")
+
+
+def make_stoch_avg(names):
+    man = {}
+    for name in names:
+        img, var, n = dump_avg(name, AVG_SAMPLES)
+        np.savez_compressed(os.path.join(HERE, name + "_avg.npz"), hdr=img, var=var)
+        man[name] = n
+        print(name, "avg", img.shape, n)
+    return man
+
+
 def main():
     if not os.path.exists(DRIVER):
         sys.exit(f"{DRIVER} missing: build it with `make -C {os.path.join(ROOT, 'oracle')}` (needs /root/reference)")
@@ -754,6 +770,14 @@ def main():
     only = set(sys.argv[1:])
     if only == {"tonemap"}:
         make_tonemap_goldens()
+        return
+    if only and only <= {n + "_avg" for n in STOCH_AVG}:
+        path = os.path.join(HERE, "manifest.json")
+        man = json.load(open(path))
+        for name, n in make_stoch_avg([o[:-4] for o in sorted(only)]).items():
+            man[name]["avg_samples"] = n
+        with open(path, "w") as f:
+            json.dump(man, f, indent=1, sort_keys=True)
         return
     for name in ORACLE_ONLY:
         if not only or name in only:

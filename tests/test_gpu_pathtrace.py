@@ -4,8 +4,9 @@
 * Per pixel, GPU == CPU oracle on the same counter-RNG keys (tolerance 1e-4 relative,
   north_star's bound); a GI direction computed with a last-ulp different sinf/acosf can
   flip a grazing hit, so a sliver of pixels may differ (<= 0.5 %).
-* Against the reference itself: statistical goldens (tests/golden/pt_*.npz, the per-pixel
-  mean of 1024 reference samples and its variance) vs the GPU at 4096 spp, 8x8-block
+* Against the reference itself: statistical goldens (tests/golden/pt_*.npz, and
+  <name>_avg.npz for the area-light, environment-light, DOF + motion-blur and C3 fixtures: the
+  per-pixel mean of 1024 reference samples and its variance) vs the GPU at 4096 spp, 8x8-block
   z-scores.
 * Mesh-light sampling has no reference golden (the reference's face draw is out of range
   in 1 of faceCount+1 draws): GPU == oracle only, on every render path.
@@ -29,7 +30,12 @@ PARITY = AVG + ["pt_meshlight", "mesh_light"]
 def _scene(tmp_path, name, spp):
     xml = tmp_path / (name + ".xml")
     xml.write_text(ob.with_samples(open(os.path.join(SCENES, name + ".xml")).read(), spp))
-    return rtgpu.HostScene(str(xml))
+    old = os.getcwd()
+    os.chdir(SCENES)                  # PLY files resolve from the current directory (parser.cpp:1404)
+    try:
+        return rtgpu.HostScene(str(xml))
+    finally:
+        os.chdir(old)
 
 
 @pytest.mark.parametrize("name", PARITY)
@@ -48,7 +54,10 @@ def test_gpu_equals_oracle(name, tmp_path):
         assert abs(st[k] - ost[k]) <= max(8, 0.002 * ost[k]), (k, st[k], ost[k])
 
 
-@pytest.mark.parametrize("name", AVG)
+STOCH = sorted(k for k, v in ob.manifest().items() if v["kind"] == "stochastic" and "avg_samples" in v)
+
+
+@pytest.mark.parametrize("name", AVG + STOCH)
 def test_gpu_statistical_vs_reference(name, tmp_path):
     hs = _scene(tmp_path, name, 4096)
     ds = rtgpu.DeviceScene(hs, 0)

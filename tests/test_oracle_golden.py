@@ -76,6 +76,21 @@ def test_oracle_statistical_vs_reference(name):
     assert rel < 0.05, rel
 
 
+@pytest.mark.parametrize("name", STOCH)
+def test_oracle_stochastic_vs_reference_mean(name, tmp_path):
+    """The stochastic fixtures (area / environment light, DOF + motion blur, C3) against the
+    reference's per-pixel mean of 1024 RenderPixel samples (<name>_avg.npz, refdriver
+    dumpavg): the oracle at 64 spp, 8x8-block z-scores with the reference's own per-pixel
+    variance -- rms below 1.5 and at most 2 % of blocks beyond 4 sigma (ob.zscore_ok)."""
+    xml = tmp_path / (name + ".xml")
+    xml.write_text(ob.with_samples(open(os.path.join(SCENES, name + ".xml")).read(), 64))
+    hs = rtgpu.HostScene(str(xml))
+    hdr, _, _ = ob.render(hs, seed=21)
+    ok, info = ob.zscore_ok(ob.block_zscores(hdr, name, 64))
+    print(name, info)
+    assert ok, info
+
+
 def test_oracle_threads_and_row_bands_are_deterministic():
     hs = rtgpu.HostScene("spheres_mirror.xml")
     a, _, sa = ob.render(hs, threads=1)
