@@ -353,6 +353,7 @@ hipError_t wave_shade(bool stats, int sk, bool one, const DevScene& S, const Dev
 void wave_resolve(const DevCamera& C, const RenderParams& P, int sample, const WaveBufs& W, const PassOut& O,
                   hipStream_t st);
 bool no_fused_shade();
+bool wide_bigleaf();
 
 // One traversal variant's pass sequence (instantiated in rtg_wave_a.hip / rtg_wave_b.hip).
 template <bool STATS, int FEAT>
@@ -368,7 +369,7 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
     const bool fast = (RTG_SHADOW_MODE == 4 ? S.cwnodes != nullptr
                        : RTG_SHADOW_MODE == 3 ? S.wnodes != nullptr
                                             : RTG_SHADOW_MODE == 2 ? S.node_up != nullptr : S.nodes != nullptr) &&
-                      !(FEAT & FEAT_BIGLEAF) && !S.exact_shadow;
+                      (!(FEAT & FEAT_BIGLEAF) || wide_bigleaf()) && !S.exact_shadow;
     // shading fused with the shadow ray: plain shading, the fast any-hit walk (RTG_NO_FUSED_SHADE=1
     // keeps the queue: experiments)
     const bool fused = sk == 0 && fast && !(FEAT & FEAT_BIGLEAF) && nshadow > 0 && !no_fused_shade();

@@ -26,6 +26,13 @@ __global__ __launch_bounds__(256) void k_resolve(const DevCamera C, const Render
     finish_pixel(C, P, sample, O, pixel, color);
 }
 
+// RTG_WIDE_BIGLEAF=1: shadow rays of large-leaf scenes also take the any-hit wide walk
+// (experiment; by default they take the cooperative reference walk)
+bool wide_bigleaf() {
+    static const bool v = std::getenv("RTG_WIDE_BIGLEAF") != nullptr;
+    return v;
+}
+
 bool no_fused_shade() {
     static const bool v = std::getenv("RTG_NO_FUSED_SHADE") != nullptr;
     return v;

@@ -1253,6 +1253,19 @@ int oracle_tonemap(const float* hdr, int width, int height, float key, float bur
     return 0;
 }
 
+// Test / diagnostics helper: histogram of leaf sizes of the description's BVHs (hist[k] =
+// leaves with k faces, k < n; larger leaves land in hist[n-1]); returns the largest leaf.
+int oracle_leaf_hist(const rtg_scene_desc* d, int64_t* hist, int n) {
+    int mx = 0;
+    for (int64_t i = 0; i < d->num_nodes; ++i) {
+        const rtg_bvh_node& b = d->nodes[i];
+        if (b.left >= 0) continue;
+        mx = std::max(mx, (int)b.count);
+        if (hist && n > 0) ++hist[std::min(n - 1, (int)b.count)];
+    }
+    return mx;
+}
+
 // Test helper: image i of a parsed description (texels as the loader stored them, for the
 // image-decoder parity tests).  info = {width, height, channels, is_hdr}; out may be null.
 int oracle_image(const rtg_scene_desc* d, int i, int32_t* info, float* out) {
