@@ -915,7 +915,12 @@ static std::vector<int> build_tile_map(int tx, int ty, int mode) {
     std::vector<int> order(n);
     for (int t = 0; t < n; ++t) order[t] = t;
     if (mode == 2) {
-        const int S = 4, stx = (tx + S - 1) / S;
+        // super-tile side in tiles (RTG_TILE_SUPER overrides, experiments)
+        static const int kSuper = [] {
+            const char* e = std::getenv("RTG_TILE_SUPER");
+            return e ? std::max(1, std::atoi(e)) : 4;
+        }();
+        const int S = kSuper, stx = (tx + S - 1) / S;
         auto key = [&](int t) {
             const int x = t % tx, y = t / tx;
             const int st = (y / S) * stx + x / S;
