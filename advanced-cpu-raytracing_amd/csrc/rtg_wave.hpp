@@ -115,6 +115,14 @@ DEV f3 resolve_one(f3 base, int flags, bool has_term, f3 term, bool occluded) {
     return color;
 }
 
+// PerformShading's sum with the unoccluded light terms already summed in light order.
+DEV f3 resolve_sum(f3 base, int flags, f3 sum) {
+    if (flags & BASE_FINAL) return base;
+    f3 color = add(base, sum);
+    if (flags & BASE_ADD_ZERO) color = add(color, mk(0, 0, 0));   // depth-0 mirror/dielectric/conductor
+    return color;
+}
+
 // SK: shading variant (rtg_common.hpp SK_*).  MODE:
 //   SH_GENERAL  every light slot's term and occlusion flag to the per-pixel buffers, shadow
 //               rays to the block's queue segment (k_shadow, k_resolve follow);
@@ -125,9 +133,13 @@ DEV f3 resolve_one(f3 base, int flags, bool has_term, f3 term, bool occluded) {
 //               (any-hit walk of FEAT, FAST) and finishes its pixel -- no queue.  Almost
 //               every pixel of a scene that fills the frame casts one, and the ones that do
 //               not leave whole waves idle only along silhouettes.
-enum { SH_GENERAL = 0, SH_ONE = 1, SH_FUSED = 2 };
+//   SH_FUSED_N  the same for plain scenes with several point / area / directional lights:
+//               each light's Shade term and its shadow ray in turn, the unoccluded terms
+//               summed in light order as k_resolve sums them (a separate instantiation: the
+//               loop costs the one-light kernel 15 %)
+enum { SH_GENERAL = 0, SH_ONE = 1, SH_FUSED = 2, SH_FUSED_N = 3 };
 template <bool STATS, int SK, int MODE, int FEAT = 0, bool FAST = false>
-__global__ __launch_bounds__(256, MODE == SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(FEAT))
+__global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(FEAT))
                                                    : RTG_SHADE_WAVES) void k_shade(const DevScene S, const DevCamera C,
                                                                                    const RenderParams P,
                                                                                    const int sample, const WaveBufs W,
@@ -192,6 +204,58 @@ __global__ __launch_bounds__(256, MODE == SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
     // ---- lights, in SampleDirectLighting's order (raytracer.cpp:706-803)
     int slot = i * W.num_slots;
     const f3 p = lit ? c.s.p : mk(0, 0, 0), n = lit ? c.s.n : mk(0, 0, 1);
+    if constexpr (MODE == SH_FUSED_N) {
+        // SK 0: point, area and directional lights only, in that order; one shadow-walk call site
+        f3 sum = mk(0, 0, 0);
+        const int np = S.num_point, na = S.num_area, nsl = np + na + S.num_dir;
+        for (int sl = 0; sl < nsl && lit; ++sl) {
+            f3 term, tgt;
+            bool directional = false;
+            if (sl < np) {
+                const f3 lp = ld3(S.point_lights[sl].pos);
+                f3 w_i = makeUnit(sub(lp, p));
+                float dist = len(sub(lp, p));
+                term = shade<false, SK>(S, c, w_i, w_o, divs(ld3(S.point_lights[sl].intensity), dist * dist));
+                tgt = lp;
+            } else if (sl < np + na) {
+                const int l = sl - np;
+                const DevAreaLight& L = S.area_lights[l];
+                float offU = rnd(key, RP_AREA, 2 * l) - 0.5f;
+                float offV = rnd(key, RP_AREA, 2 * l + 1) - 0.5f;
+                const f3 sp = add(add(ld3(L.pos), muls(ld3(L.u), L.extent * offU)), muls(ld3(L.v), L.extent * offV));
+                f3 w_i = sub(sp, p);
+                float dist = len(w_i);
+                float dSqr = dist * dist;
+                w_i = divs(w_i, dist);
+                float lc = dot(ld3(L.normal), neg(w_i));
+                if (lc < 0) lc = dot(ld3(L.normal), w_i);
+                term = shade<false, SK>(S, c, w_i, w_o, muls(ld3(L.radiance), L.area * lc / dSqr));
+                tgt = sp;
+            } else {
+                const f3 ldir = ld3(S.dir_lights[sl - np - na].dir);
+                term = shade<false, SK>(S, c, neg(ldir), w_o, ld3(S.dir_lights[sl - np - na].radiance));
+                tgt = ldir;
+                directional = true;
+            }
+            // IsInShadow / IsInShadowDirectional (raytracer.cpp:555-584)
+            cn.shd();
+            const f3 o = add(p, muls(n, S.eps));
+            float4 qo, qd;
+            if (directional) {
+                const f3 d = neg(tgt);
+                qo = make_float4(o.x, o.y, o.z, INFINITY);
+                qd = make_float4(d.x, d.y, d.z, INFINITY);
+            } else {
+                const f3 dir = sub(tgt, p);
+                const float lightT = len(dir);
+                const f3 d = divs(dir, lightT);
+                qo = make_float4(o.x, o.y, o.z, lightT + 0.01f);
+                qd = make_float4(d.x, d.y, d.z, lightT);
+            }
+            if (!shadow_occluded<STATS, FEAT, FAST>(S, W, 0, qo, qd, cn)) sum = add(sum, term);
+        }
+        if (valid) finish_pixel(C, P, sample, O, pixel, resolve_sum(base, bflags, sum));
+    } else {
     auto push = [&](bool want, f3 target_dir_or_pos, bool directional) {
         // IsInShadow / IsInShadowDirectional shadow-ray set-up (raytracer.cpp:555-584)
         float4 qo, qd;
@@ -321,6 +385,7 @@ __global__ __launch_bounds__(256, MODE == SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
         }
     }
     if (MODE == SH_ONE && valid && !pushed) finish_pixel(C, P, sample, O, pixel, resolve_one(base, bflags, has_term, term1, false));
+    }
     __syncthreads();
     if (threadIdx.x == 0) W.q_count[blockIdx.x] = seg_count;
     flush_counters<STATS>(cn, counters);
@@ -363,6 +428,7 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
     // at most one light: k_shade / k_shadow_one finish the pixels (no k_resolve); shading
     // variants for this case only (every other scene takes the general k_shade)
     const bool one = W.num_slots <= 1 && W.q_pay != nullptr;
+    const int scene_sk = sk;
     if (!one) sk = SK_ALL;
     // fast any-hit walk (RTG_SHADOW_MODE) unless RTG_RENDER_EXACT_SHADOW asks for the
     // reference walk
@@ -372,8 +438,8 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
                       (!(FEAT & FEAT_BIGLEAF) || wide_bigleaf()) && !S.exact_shadow;
     // shading fused with the shadow ray: plain shading, the fast any-hit walk (RTG_NO_FUSED_SHADE=1
     // keeps the queue: experiments)
-    const bool fused = sk == 0 && fast && !(FEAT & FEAT_BIGLEAF) && nshadow > 0 && !no_fused_shade();
-    *layout = one ? (fused ? LAYOUT_WAVE_FUSED : LAYOUT_WAVE_ONE) : LAYOUT_WAVE;
+    const bool fused = scene_sk == 0 && fast && !(FEAT & FEAT_BIGLEAF) && nshadow > 0 && !no_fused_shade();
+    *layout = fused ? LAYOUT_WAVE_FUSED : (one ? LAYOUT_WAVE_ONE : LAYOUT_WAVE);
     for (int s = P.sample_begin; s < P.sample_begin + P.sample_count; ++s) {
         const int first = s == P.sample_begin, last = s == P.sample_begin + P.sample_count - 1;
         const PassOut O{hdr, l, W.accum, first, last};
@@ -390,10 +456,15 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
         if (!ordered)
             hipLaunchKernelGGL((k_primary<STATS, FEAT>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
         if (e5) (void)hipEventRecord(e5[1], st);
-        if (one && fused) {
-            if constexpr (!(FEAT & FEAT_BIGLEAF))
-                hipLaunchKernelGGL((k_shade<STATS, 0, SH_FUSED, FEAT, true>), dim3(P.num_tiles), dim3(256), 0, st, S, C,
-                                   P, s, W, O, cnt);
+        if (fused) {
+            if constexpr (!(FEAT & FEAT_BIGLEAF)) {
+                if (one)
+                    hipLaunchKernelGGL((k_shade<STATS, 0, SH_FUSED, FEAT, true>), dim3(P.num_tiles), dim3(256), 0, st, S,
+                                       C, P, s, W, O, cnt);
+                else
+                    hipLaunchKernelGGL((k_shade<STATS, 0, SH_FUSED_N, FEAT, true>), dim3(P.num_tiles), dim3(256), 0, st,
+                                       S, C, P, s, W, O, cnt);
+            }
             if (e5) (void)hipEventRecord(e5[2], st);
         } else if (one) {
             e = wave_shade(STATS, sk, true, S, C, P, s, W, O, cnt, st);
