@@ -1,10 +1,14 @@
 // Photographic tonemapper (Tonemapper::Tonemap, tonemapper.h:28-60) on the GPU:
 //
-//   k_tm_logsum / k_tm_avg   log-average luminance: sum of log(delta + Y) in double,
-//                            per-block partial sums in a fixed order, then one block
-//                            adds the partials in a fixed order (deterministic; the
-//                            reference adds sequentially, so the two sums differ in
-//                            the last bits only)
+//   k_tm_log / k_tm_seqsum   log-average luminance: log(delta + Y) per pixel in double,
+//                            then the reference's sequential sum (tonemapper.h:35-48) in
+//                            pixel order by one wave -- the same rounding sequence as
+//                            the reference, so the average is its average bit for bit
+//                            wherever the device log agrees with the host's.  A
+//                            dependent chain of W*H double adds: ~3.5 ns per pixel.
+//   k_tm_logsum / k_tm_avg   (RTG_TM_SEQSUM=0) the same sum as per-block partials in a
+//                            fixed parallel order: ~50x faster, differs from the
+//                            reference's sum in the last bits
 //   k_tm_hist / k_tm_pick    the burn threshold: the k-th smallest of all 3*W*H channel
 //                            values (the reference's std::sort + index), found by an
 //                            MSB-first radix select over the order-preserving bit image
@@ -25,6 +29,10 @@ namespace rtg {
 namespace {
 
 constexpr int kTmThreads = 256;
+
+#ifndef RTG_TM_SEQSUM
+#define RTG_TM_SEQSUM 1
+#endif
 
 __device__ __forceinline__ uint32_t float_key(float x) {
     const uint32_t b = __float_as_uint(x);
@@ -51,6 +59,77 @@ __global__ __launch_bounds__(kTmThreads) void k_tm_logsum(const float* __restric
         __syncthreads();
     }
     if (threadIdx.x == 0) partial[blockIdx.x] = red[0];
+}
+
+// log(delta + luminance) of every pixel (tonemapper.h:37-44), in pixel order
+__global__ __launch_bounds__(kTmThreads) void k_tm_log(const float* __restrict__ hdr, long long n,
+                                                       double* __restrict__ logs) {
+    const long long i = blockIdx.x * (long long)kTmThreads + threadIdx.x;
+    if (i >= n) return;
+    const double delta = 0.01f;
+    const double r = hdr[3 * i], g = hdr[3 * i + 1], b = hdr[3 * i + 2];
+    const double lum = 0.2126 * r + 0.7152 * g + 0.0722 * b;
+    logs[i] = log(delta + lum);
+}
+
+// logLuminancesSum += log(...) for i = 0 .. n-1 (tonemapper.h:35-47), one wave.  Each chunk
+// of kSeqChunk terms is loaded by the whole wave (coalesced) and staged in LDS; every lane then
+// runs the same in-order chain over it (uniform LDS addresses: broadcast reads), while the next
+// chunk's loads are already in flight.  avg = exp(sum / pixelCount).
+constexpr int kSeqPerLane = 16;
+constexpr int kSeqChunk = 64 * kSeqPerLane;
+__global__ __launch_bounds__(64) void k_tm_seqsum(const double* __restrict__ logs, long long n,
+                                                  double* __restrict__ avg, uint32_t* __restrict__ sel,
+                                                  uint32_t k) {
+    __shared__ double buf[kSeqChunk];
+    const int lane = threadIdx.x;
+    double r[kSeqPerLane];
+#pragma unroll
+    for (int u = 0; u < kSeqPerLane; ++u) {
+        const long long idx = (long long)u * 64 + lane;
+        r[u] = idx < n ? logs[idx] : 0.0;
+    }
+    double s = 0.0;
+    for (long long b = 0; b < n; b += kSeqChunk) {
+#pragma unroll
+        for (int u = 0; u < kSeqPerLane; ++u) buf[u * 64 + lane] = r[u];
+        __syncthreads();
+        if (b + kSeqChunk < n) {
+#pragma unroll
+            for (int u = 0; u < kSeqPerLane; ++u) {
+                const long long idx = b + kSeqChunk + (long long)u * 64 + lane;
+                r[u] = idx < n ? logs[idx] : 0.0;
+            }
+        }
+        const int m = (n - b) < kSeqChunk ? (int)(n - b) : kSeqChunk;
+        if (m == kSeqChunk) {
+            // software-pipelined: the next 16 terms are read from LDS while the chain adds
+            // the current 16 (the chain is bound by the dependent double-add latency)
+            double a[16], c[16];
+#pragma unroll
+            for (int k = 0; k < 16; ++k) a[k] = buf[k];
+            for (int j = 0; j < kSeqChunk; j += 32) {
+#pragma unroll
+                for (int k = 0; k < 16; ++k) c[k] = buf[j + 16 + k];
+#pragma unroll
+                for (int k = 0; k < 16; ++k) s += a[k];
+                if (j + 32 < kSeqChunk) {
+#pragma unroll
+                    for (int k = 0; k < 16; ++k) a[k] = buf[j + 32 + k];
+                }
+#pragma unroll
+                for (int k = 0; k < 16; ++k) s += c[k];
+            }
+        } else {
+            for (int j = 0; j < m; ++j) s += buf[j];
+        }
+        __syncthreads();
+    }
+    if (lane == 0) {
+        avg[0] = exp(s / (double)n);
+        sel[0] = 0;
+        sel[1] = k;
+    }
 }
 
 // sum of the block partials in a fixed order; avg = exp(sum / pixelCount)
@@ -145,8 +224,8 @@ __global__ __launch_bounds__(kTmThreads) void k_tm_map(const float* __restrict__
 }  // namespace
 
 size_t tonemap_scratch_bytes(long long pixels) {
-    (void)pixels;
-    return 1024 * sizeof(double) + 2 * sizeof(double) + 258 * sizeof(uint32_t) + 256;
+    return 1024 * sizeof(double) + 2 * sizeof(double) + 258 * sizeof(uint32_t) + 256 +
+           (RTG_TM_SEQSUM ? (size_t)pixels * sizeof(double) : 0);
 }
 
 hipError_t launch_tonemap(const float* hdr, int width, int height, float key, float burn, float saturation,
@@ -157,6 +236,7 @@ hipError_t launch_tonemap(const float* hdr, int width, int height, float key, fl
     double* avg = partial + 1024;
     uint32_t* sel = (uint32_t*)(avg + 2);
     uint32_t* hist = sel + 2;
+    double* logs = (double*)(p + 1024 * sizeof(double) + 2 * sizeof(double) + 258 * sizeof(uint32_t) + 256);
     hipError_t e = hipMemsetAsync(hist, 0, 256 * sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     // burn threshold index exactly as tonemapper.h:104-107 (float * int -> float -> int)
@@ -166,8 +246,14 @@ hipError_t launch_tonemap(const float* hdr, int width, int height, float key, fl
     if (idx > lastIdx) idx = lastIdx;
     if (idx < 0) idx = 0;
     const int nb = (int)((n + kTmThreads - 1) / kTmThreads < 1024 ? (n + kTmThreads - 1) / kTmThreads : 1024);
-    hipLaunchKernelGGL(k_tm_logsum, dim3(nb), dim3(kTmThreads), 0, st, hdr, n, partial);
-    hipLaunchKernelGGL(k_tm_avg, dim3(1), dim3(kTmThreads), 0, st, partial, nb, n, avg, sel, (uint32_t)idx);
+    if (RTG_TM_SEQSUM) {
+        hipLaunchKernelGGL(k_tm_log, dim3((unsigned)((n + kTmThreads - 1) / kTmThreads)), dim3(kTmThreads), 0, st,
+                           hdr, n, logs);
+        hipLaunchKernelGGL(k_tm_seqsum, dim3(1), dim3(64), 0, st, logs, n, avg, sel, (uint32_t)idx);
+    } else {
+        hipLaunchKernelGGL(k_tm_logsum, dim3(nb), dim3(kTmThreads), 0, st, hdr, n, partial);
+        hipLaunchKernelGGL(k_tm_avg, dim3(1), dim3(kTmThreads), 0, st, partial, nb, n, avg, sel, (uint32_t)idx);
+    }
     if (burn > 0.01) {
         const long long m = 3 * n;
         const int hb = (int)((m + kTmThreads - 1) / kTmThreads < 2048 ? (m + kTmThreads - 1) / kTmThreads : 2048);
