@@ -1249,6 +1249,30 @@ int rtg_tonemap(const float* hdr, int32_t w, int32_t h, const rtg_tonemap_params
     return rc;
 }
 
+int rtg_tonemap_log_average(const float* hdr, int32_t w, int32_t h, int32_t mode, double* avg_out, int32_t device) {
+    if (!hdr || !avg_out || w <= 0 || h <= 0 || mode > 2) return set_err(RTG_ERR_INVALID, "bad log-average arguments");
+    HIP_TRY(hipSetDevice(device));
+    const size_t n = (size_t)w * h;
+    float* dh = nullptr;
+    void* scratch = nullptr;
+    HIP_TRY(hipMalloc(&dh, 3 * n * sizeof(float)));
+    if (hipMalloc(&scratch, rtg::tonemap_scratch_bytes((long long)n)) != hipSuccess) {
+        (void)hipFree(dh);
+        return set_err(RTG_ERR_NOMEM, "device allocation failed");
+    }
+    int rc = RTG_OK;
+    if (hipMemcpy(dh, hdr, 3 * n * sizeof(float), hipMemcpyHostToDevice) != hipSuccess) rc = set_err(RTG_ERR_HIP, "copy failed");
+    if (!rc) {
+        rtg::launch_log_average(dh, (long long)n, mode, 0, scratch, nullptr);
+        if (hipGetLastError() != hipSuccess ||
+            hipMemcpy(avg_out, (char*)scratch + rtg::tonemap_avg_offset(), sizeof(double), hipMemcpyDeviceToHost) != hipSuccess)
+            rc = set_err(RTG_ERR_HIP, "log-average failed");
+    }
+    (void)hipFree(dh);
+    (void)hipFree(scratch);
+    return rc;
+}
+
 int rtg_resolve_accum(const float* accum, int32_t w, int32_t h, float* hdr, uint8_t* ldr) {
     if (!accum || w <= 0 || h <= 0) return set_err(RTG_ERR_INVALID, "bad accumulation buffer");
     for (size_t p = 0; p < (size_t)w * h; ++p) {

@@ -25,6 +25,8 @@ hipError_t launch_tree(TreeState*& tree, const DevScene& S, const DevCamera& C, 
                        hipStream_t stream, hipEvent_t* ev);
 // photographic tonemapper (rtg_tonemap.hip); scratch of tonemap_scratch_bytes()
 size_t tonemap_scratch_bytes(long long pixels);
+size_t tonemap_avg_offset();   // byte offset of the log-average luminance (double) in the scratch
+void launch_log_average(const float* hdr, long long n, int mode, uint32_t idx, void* scratch, hipStream_t st);
 hipError_t launch_tonemap(const float* hdr, int width, int height, float key, float burn, float saturation,
                           float gamma, unsigned char* ldr, void* scratch, hipStream_t stream);
 // device scene ingest (rtg_bvh.hip): the reference's midpoint BVH of one mesh built on the

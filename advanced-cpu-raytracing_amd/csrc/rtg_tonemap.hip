@@ -1,11 +1,13 @@
 // Photographic tonemapper (Tonemapper::Tonemap, tonemapper.h:28-60) on the GPU:
 //
-//   k_tm_log / k_tm_seqsum   log-average luminance: log(delta + Y) per pixel in double,
+//   k_tm_log + k_tm_winsum   log-average luminance: log(delta + Y) per pixel in double,
 //                            then the reference's sequential sum (tonemapper.h:35-48) in
-//                            pixel order by one wave -- the same rounding sequence as
-//                            the reference, so the average is its average bit for bit
-//                            wherever the device log agrees with the host's.  A
-//                            dependent chain of W*H double adds: ~3.5 ns per pixel.
+//                            pixel order -- the same rounding sequence as the reference,
+//                            so the average is its average bit for bit wherever the
+//                            device log agrees with the host's.  k_tm_winsum advances a
+//                            8 192-term window per step by exact integer arithmetic
+//                            inside a binade (see there); k_tm_seqsum (RTG_TM_SEQSUM=1)
+//                            is the plain dependent chain of W*H double adds.
 //   k_tm_logsum / k_tm_avg   (RTG_TM_SEQSUM=0) the same sum as per-block partials in a
 //                            fixed parallel order: ~50x faster, differs from the
 //                            reference's sum in the last bits
@@ -21,6 +23,7 @@
 // HBM-bound: 12 B/pixel per pass over the float image, 6 passes + 3 B/pixel written.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 #include "rtg_kernels.hpp"
 
@@ -30,8 +33,11 @@ namespace {
 
 constexpr int kTmThreads = 256;
 
+// log-sum mode: 2 = windowed exact sum (k_tm_winsum), 1 = the plain chain (k_tm_seqsum),
+// 0 = parallel fixed-order reduction (not the reference's rounding).  The environment
+// variable RTG_TM_SEQSUM overrides it at run time (A/B and diagnostics).
 #ifndef RTG_TM_SEQSUM
-#define RTG_TM_SEQSUM 1
+#define RTG_TM_SEQSUM 2
 #endif
 
 __device__ __forceinline__ uint32_t float_key(float x) {
@@ -132,6 +138,145 @@ __global__ __launch_bounds__(64) void k_tm_seqsum(const double* __restrict__ log
     }
 }
 
+// The same sequential sum, an 8 192-term window per step (one block of eight waves, 16
+// consecutive terms per thread) instead of an 8 192-add chain.  While
+// the running sum s keeps one binade [2^(e-1), 2^e), every representable value there is a
+// multiple of u = 2^(e-53), so RN(s + x) = s + u * round(x / u) exactly -- unless x / u is a
+// tie (then the parity of s decides) or s + x leaves the binade.  Each thread takes 16
+// consecutive terms: k = rint(x / u) (an exact power-of-two scale), a lane-sequential prefix
+// and a block scan of the integer-valued k give the running sum in units of u after every term; the
+// first term whose result is not strictly inside the binade (or is a tie, or s = 0) stops
+// the window.  s jumps to that term's exact running value, the stopping term is added with
+// one rounded double add (the reference's own step), and the next window starts after it.
+// A window that stops within its first 64 terms (|s| small or near a power of two) is
+// finished with the plain rounded chain, so the worst case is the chain's cost.  The
+// result is the reference's sum bit for bit on any input.
+constexpr int kWinPer = 16;
+constexpr int kWinWaves = 8;
+constexpr int kWinThreads = 64 * kWinWaves;
+constexpr int kWin = kWinThreads * kWinPer;
+__global__ __launch_bounds__(kWinThreads) void k_tm_winsum(const double* __restrict__ logs, long long n,
+                                                           double* __restrict__ avg, uint32_t* __restrict__ sel,
+                                                           uint32_t k) {
+    __shared__ double buf[kWin];
+    __shared__ double wtot[kWinWaves];
+    __shared__ int wmin[kWinWaves];
+    __shared__ double pshare;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    auto load = [&](double* v, long long at) {
+#pragma unroll
+        for (int t = 0; t < kWinPer; ++t) {
+            const long long idx = at + tid * kWinPer + t;
+            v[t] = idx < n ? logs[idx] : 0.0;
+        }
+    };
+    double cur[kWinPer], nxt[kWinPer];
+    load(cur, 0);
+    double s = 0.0;   // the running sum: the same value in every thread
+    long long a = 0;
+    while (a < n) {
+#pragma unroll
+        for (int t = 0; t < kWinPer; ++t) buf[tid * kWinPer + t] = cur[t];
+        load(nxt, a + kWin);   // speculative: the next window if this one is consumed whole
+        const long long rem = n - a;
+        int e = 0;
+        const double fr = frexp(s, &e);
+        // integers in units of u, held in doubles: every running value of a valid prefix lies in
+        // [2^52, 2^53) and every partial sum of its k is a difference of two such values, so all
+        // of it is exact; sums that run past the first failing term may round, but nothing past
+        // that term is used
+        const double M = s != 0.0 ? ldexp(fr, 53) : 0.0;
+        const bool neg = s < 0.0;
+        const double lo = 4503599627370497.0, hi = 9007199254740990.0;   // 2^52 + 1, 2^53 - 2
+        double kk[kWinPer];
+        double tot = 0.0;
+        int bad = kWinPer;   // first term of this thread that cannot take the shortcut
+#pragma unroll
+        for (int t = 0; t < kWinPer; ++t) {
+            const double y = ldexp(cur[t], 53 - e);
+            const double r = rint(y);
+            const bool tie = fabs(y - r) == 0.5;
+            const bool ok = s != 0.0 && fabs(y) < 4503599627370496.0 && !tie && (long long)(tid * kWinPer + t) < rem;
+            kk[t] = ok ? r : 0.0;
+            if (!ok && bad == kWinPer) bad = t;
+            tot += kk[t];
+        }
+        // block scan of the thread totals: wave scans, then the wave totals in wave order
+        double incl = tot;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const double o = __shfl_up(incl, d);
+            if (lane >= d) incl += o;
+        }
+        if (lane == 63) wtot[wave] = incl;
+        __syncthreads();
+        double woff = 0.0, all = 0.0;
+#pragma unroll
+        for (int w = 0; w < kWinWaves; ++w) {
+            if (w < wave) woff += wtot[w];
+            all += wtot[w];
+        }
+        double excl = __shfl_up(incl, 1);
+        if (lane == 0) excl = 0.0;
+        excl += woff;
+        double P = M + excl;   // running sum (units of u) before this thread's terms
+#pragma unroll
+        for (int t = 0; t < kWinPer; ++t) {
+            P += kk[t];
+            const double mag = neg ? -P : P;
+            if (t < bad && (mag < lo || mag > hi)) bad = t;
+        }
+        int f = bad < kWinPer ? tid * kWinPer + bad : kWin;
+#pragma unroll
+        for (int d = 32; d > 0; d >>= 1) {
+            const int o = __shfl_xor(f, d);
+            f = o < f ? o : f;
+        }
+        if (lane == 0) wmin[wave] = f;
+        __syncthreads();
+#pragma unroll
+        for (int w = 0; w < kWinWaves; ++w) f = wmin[w] < f ? wmin[w] : f;
+        // exact running value before term f, from the thread that holds term f
+        if (f < kWin && tid == f / kWinPer) {
+            double pf = M + excl;
+            const int tf = f % kWinPer;
+#pragma unroll
+            for (int t = 0; t < kWinPer; ++t)
+                if (t < tf) pf += kk[t];
+            pshare = pf;
+        }
+        __syncthreads();
+        const double pf = f >= kWin ? M + all : pshare;
+        if (f > 0) s = ldexp(pf, e - 53);
+        if (f >= kWin) {   // the whole window took the shortcut
+            a += kWin;
+#pragma unroll
+            for (int t = 0; t < kWinPer; ++t) cur[t] = nxt[t];
+            __syncthreads();
+            continue;
+        }
+        if ((long long)f >= rem) break;   // every remaining term took the shortcut
+        s = s + buf[f];                    // the stopping term: the reference's rounded add
+        if (f < 64) {                      // slow region: finish the window as a chain
+            const int m = rem < kWin ? (int)rem : kWin;
+#pragma unroll 8
+            for (int j = f + 1; j < m; ++j) s = s + buf[j];
+            a += kWin;
+#pragma unroll
+            for (int t = 0; t < kWinPer; ++t) cur[t] = nxt[t];
+        } else {
+            a += f + 1;
+            load(cur, a);
+        }
+        __syncthreads();
+    }
+    if (tid == 0) {
+        avg[0] = exp(s / (double)n);
+        sel[0] = 0;
+        sel[1] = k;
+    }
+}
+
 // sum of the block partials in a fixed order; avg = exp(sum / pixelCount)
 __global__ __launch_bounds__(kTmThreads) void k_tm_avg(const double* __restrict__ partial, int nb, long long n,
                                                        double* __restrict__ avg, uint32_t* __restrict__ sel,
@@ -225,8 +370,35 @@ __global__ __launch_bounds__(kTmThreads) void k_tm_map(const float* __restrict__
 
 size_t tonemap_scratch_bytes(long long pixels) {
     return 1024 * sizeof(double) + 2 * sizeof(double) + 258 * sizeof(uint32_t) + 256 +
-           (RTG_TM_SEQSUM ? (size_t)pixels * sizeof(double) : 0);
+           (size_t)pixels * sizeof(double);
 }
+
+// avg = exp(sum of log(delta + Y) / pixelCount) into the scratch's avg slot (tonemap_avg_offset);
+// mode < 0: the build / RTG_TM_SEQSUM default
+void launch_log_average(const float* hdr, long long n, int mode, uint32_t idx, void* scratch, hipStream_t st) {
+    char* p = (char*)scratch;
+    double* partial = (double*)p;
+    double* avg = partial + 1024;
+    uint32_t* sel = (uint32_t*)(avg + 2);
+    double* logs = (double*)(p + 1024 * sizeof(double) + 2 * sizeof(double) + 258 * sizeof(uint32_t) + 256);
+    static const int dflt = [] {
+        const char* v = std::getenv("RTG_TM_SEQSUM");
+        return v && *v ? std::atoi(v) : RTG_TM_SEQSUM;
+    }();
+    if (mode < 0) mode = dflt;
+    if (mode > 0) {
+        hipLaunchKernelGGL(k_tm_log, dim3((unsigned)((n + kTmThreads - 1) / kTmThreads)), dim3(kTmThreads), 0, st,
+                           hdr, n, logs);
+        if (mode == 1) hipLaunchKernelGGL(k_tm_seqsum, dim3(1), dim3(64), 0, st, logs, n, avg, sel, idx);
+        else hipLaunchKernelGGL(k_tm_winsum, dim3(1), dim3(kWinThreads), 0, st, logs, n, avg, sel, idx);
+    } else {
+        const int nb = (int)((n + kTmThreads - 1) / kTmThreads < 1024 ? (n + kTmThreads - 1) / kTmThreads : 1024);
+        hipLaunchKernelGGL(k_tm_logsum, dim3(nb), dim3(kTmThreads), 0, st, hdr, n, partial);
+        hipLaunchKernelGGL(k_tm_avg, dim3(1), dim3(kTmThreads), 0, st, partial, nb, n, avg, sel, idx);
+    }
+}
+
+size_t tonemap_avg_offset() { return 1024 * sizeof(double); }
 
 hipError_t launch_tonemap(const float* hdr, int width, int height, float key, float burn, float saturation,
                           float gamma, unsigned char* ldr, void* scratch, hipStream_t st) {
@@ -236,7 +408,6 @@ hipError_t launch_tonemap(const float* hdr, int width, int height, float key, fl
     double* avg = partial + 1024;
     uint32_t* sel = (uint32_t*)(avg + 2);
     uint32_t* hist = sel + 2;
-    double* logs = (double*)(p + 1024 * sizeof(double) + 2 * sizeof(double) + 258 * sizeof(uint32_t) + 256);
     hipError_t e = hipMemsetAsync(hist, 0, 256 * sizeof(uint32_t), st);
     if (e != hipSuccess) return e;
     // burn threshold index exactly as tonemapper.h:104-107 (float * int -> float -> int)
@@ -245,15 +416,7 @@ hipError_t launch_tonemap(const float* hdr, int width, int height, float key, fl
     int idx = (int)(thresholdPerct * lastIdx);
     if (idx > lastIdx) idx = lastIdx;
     if (idx < 0) idx = 0;
-    const int nb = (int)((n + kTmThreads - 1) / kTmThreads < 1024 ? (n + kTmThreads - 1) / kTmThreads : 1024);
-    if (RTG_TM_SEQSUM) {
-        hipLaunchKernelGGL(k_tm_log, dim3((unsigned)((n + kTmThreads - 1) / kTmThreads)), dim3(kTmThreads), 0, st,
-                           hdr, n, logs);
-        hipLaunchKernelGGL(k_tm_seqsum, dim3(1), dim3(64), 0, st, logs, n, avg, sel, (uint32_t)idx);
-    } else {
-        hipLaunchKernelGGL(k_tm_logsum, dim3(nb), dim3(kTmThreads), 0, st, hdr, n, partial);
-        hipLaunchKernelGGL(k_tm_avg, dim3(1), dim3(kTmThreads), 0, st, partial, nb, n, avg, sel, (uint32_t)idx);
-    }
+    launch_log_average(hdr, n, -1, (uint32_t)idx, scratch, st);
     if (burn > 0.01) {
         const long long m = 3 * n;
         const int hb = (int)((m + kTmThreads - 1) / kTmThreads < 2048 ? (m + kTmThreads - 1) / kTmThreads : 2048);

@@ -76,6 +76,7 @@ EXPORTED = [
     "rtg_desc_camera_info", "rtg_desc_counts", "rtg_scene_create", "rtg_scene_destroy",
     "rtg_device_count", "rtg_render", "rtg_render_device", "rtg_resolve_accum",
     "rtg_scene_stats", "rtg_scene_reset_stats", "rtg_scene_timings", "rtg_tonemap_device", "rtg_tonemap",
+    "rtg_tonemap_log_average",
     "rtg_write_png", "rtg_write_hdr",
     "rtg_last_error", "rtg_abi_version",
     "rtg_scene_create_multi", "rtg_scene_num_devices", "rtg_part_runs", "rtg_copy_part_to_host",
@@ -125,6 +126,7 @@ def lib() -> ctypes.CDLL:
     L.rtg_scene_timings.argtypes = [vp, P(ctypes.c_float), P(ctypes.c_char_p), i32, P(i32)]
     L.rtg_tonemap_device.argtypes = [vp, i32, i32, P(TonemapParams), vp, i32, vp]
     L.rtg_tonemap.argtypes = [vp, i32, i32, P(TonemapParams), vp, i32]
+    L.rtg_tonemap_log_average.argtypes = [vp, i32, i32, i32, P(ctypes.c_double), i32]
     L.rtg_write_png.argtypes = [ctypes.c_char_p, i32, i32, vp]
     L.rtg_write_hdr.argtypes = [ctypes.c_char_p, i32, i32, vp]
     L.rtg_scene_create_multi.argtypes = [vp, P(i32), i32, P(vp)]
@@ -329,6 +331,15 @@ def tonemap(hdr: np.ndarray, key=0.18, burn=1.0, saturation=1.0, gamma=2.2, devi
     p = TonemapParams(key, burn, saturation, gamma)
     _check(lib().rtg_tonemap(hdr.ctypes.data, w, h, ctypes.byref(p), ldr.ctypes.data, device))
     return ldr
+
+
+def tonemap_log_average(hdr: np.ndarray, mode: int = -1, device: int = 0) -> float:
+    """Tonemapper::avgLuminance (tonemapper.h:35-48) on the GPU; mode as rtg_tonemap_log_average."""
+    hdr = np.ascontiguousarray(hdr, np.float32)
+    h, w, _ = hdr.shape
+    out = ctypes.c_double()
+    _check(lib().rtg_tonemap_log_average(hdr.ctypes.data, w, h, mode, ctypes.byref(out), device))
+    return out.value
 
 
 def write_png(path: str, ldr: np.ndarray):

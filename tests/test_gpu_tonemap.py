@@ -6,6 +6,7 @@ Exact: the log-average luminance is the reference's sequential double sum in pix
 goldens and the three full-HD cases (tools/diag_tonemap.py).  The device library's double
 log / exp / pow could in principle round differently from glibc's on some input; none of
 these inputs shows it."""
+import math
 import os
 
 import numpy as np
@@ -66,3 +67,40 @@ def test_render_tonemapped_camera(tmp_path):
         assert np.array_equal(band[:8], ob.clamp_ldr(hdr[:8]))
     finally:
         os.chdir(old)
+
+
+def _seq_log_average(hdr):
+    """tonemapper.h:35-48 in Python floats (doubles, math.log = glibc's log, the sum in order)."""
+    x = hdr.reshape(-1, 3).astype(np.float64)
+    lum = 0.2126 * x[:, 0] + 0.7152 * x[:, 1] + 0.0722 * x[:, 2]
+    delta = float(np.float32(0.01))
+    s = 0.0
+    for v in (lum + delta).tolist():
+        s += math.log(v)
+    return math.exp(s / len(lum))
+
+
+def _log_inputs():
+    rng = np.random.default_rng(11)
+    yield "lognormal_1080p", rng.lognormal(0.0, 1.5, size=(1080, 1920, 3)).astype(np.float32)
+    yield "bright", rng.lognormal(3.0, 1.0, size=(480, 640, 3)).astype(np.float32)
+    # luminance around 0.99: log terms around zero, the running sum hovers near 0
+    yield "hover", rng.uniform(0.0, 1.98, size=(480, 640, 3)).astype(np.float32)
+    yield "flat_zero_logs", np.full((300, 500, 3), 0.99, np.float32)
+    yield "black", np.zeros((200, 333, 3), np.float32)
+    yield "ragged_1x1", np.full((1, 1, 3), 2.0, np.float32)
+    yield "ragged_7x150", rng.lognormal(0.0, 2.0, size=(7, 150, 3)).astype(np.float32)
+
+
+@pytest.mark.parametrize("name,hdr", list(_log_inputs()), ids=[n for n, _ in _log_inputs()])
+def test_log_average_sequential(name, hdr):
+    """The windowed sum (mode 2, the default) equals the plain sequential chain (mode 1) bit for
+    bit, and both equal the reference's host sum (glibc log) to the last bit where the device
+    log agrees with glibc's (asserted within 1e-15 relative; exact equality is reported)."""
+    win = rtgpu.tonemap_log_average(hdr, 2)
+    chain = rtgpu.tonemap_log_average(hdr, 1)
+    assert win == chain or (math.isnan(win) and math.isnan(chain)), (name, win.hex(), chain.hex())
+    assert rtgpu.tonemap_log_average(hdr, -1) == win
+    ref = _seq_log_average(hdr)
+    print(name, "window == chain;", "== host reference" if win == ref else f"host {ref!r} vs {win!r}")
+    assert abs(win - ref) <= 1e-15 * abs(ref), (name, win, ref)

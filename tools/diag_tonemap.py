@@ -34,8 +34,10 @@ for params in [(0.18, 1.0, 1.0, 2.2), (0.05, 10.0, 0.7, 2.4), (0.5, 0.0, 1.0, 1.
     ref = ob.tonemap(hdr, *params)
     print("fullhd", params, "differing bytes / max", diff(got, ref), "of", ref.size, flush=True)
 
-for (h, w) in [(1080, 1920), (2160, 3840)]:
-    x = torch.from_numpy(rng.lognormal(1.0, 1.0, size=(h, w, 3)).astype(np.float32)).cuda()
+print("log-sum mode (RTG_TM_SEQSUM):", os.environ.get("RTG_TM_SEQSUM", "library default"))
+for (h, w, kind) in [(1080, 1920, "lognormal"), (2160, 3840, "lognormal"), (1080, 1920, "hover")]:
+    a = rng.lognormal(1.0, 1.0, size=(h, w, 3)) if kind == "lognormal" else rng.uniform(0.0, 1.98, size=(h, w, 3))
+    x = torch.from_numpy(a.astype(np.float32)).cuda()
     y = torch.empty((h, w, 3), dtype=torch.uint8, device="cuda")
     p = rtgpu.TonemapParams(0.18, 1.0, 1.0, 2.2)
     st = torch.cuda.current_stream().cuda_stream
@@ -47,4 +49,4 @@ for (h, w) in [(1080, 1920), (2160, 3840)]:
     for _ in range(5):
         f(ctypes.c_void_p(x.data_ptr()), w, h, ctypes.byref(p), ctypes.c_void_p(y.data_ptr()), 0, ctypes.c_void_p(st))
     torch.cuda.synchronize()
-    print("tonemap", w, "x", h, "ms", round((time.perf_counter() - t) / 5 * 1e3, 3), flush=True)
+    print("tonemap", kind, w, "x", h, "ms", round((time.perf_counter() - t) / 5 * 1e3, 3), flush=True)
