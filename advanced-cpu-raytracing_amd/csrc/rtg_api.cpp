@@ -1323,7 +1323,10 @@ int rtg_scene_reset_stats(rtg_scene* s) {
     for (rtg_scene* r : reps) {
         HIP_TRY(hipSetDevice(r->device));
         HIP_TRY(hipEventSynchronize(r->done));
-        HIP_TRY(hipMemset(r->counters.p, 0, sizeof(rtg::DevCounters)));
+        // on the scene's (non-blocking) stream, complete before return: ordered before the
+        // next render whichever stream that one runs on
+        HIP_TRY(hipMemsetAsync(r->counters.p, 0, sizeof(rtg::DevCounters), r->stream));
+        HIP_TRY(hipStreamSynchronize(r->stream));
     }
     return RTG_OK;
 }

@@ -149,12 +149,17 @@ __global__ __launch_bounds__(64) void k_tm_seqsum(const double* __restrict__ log
 // the window.  s jumps to that term's exact running value, the stopping term is added with
 // one rounded double add (the reference's own step), and the next window starts after it.
 // A window that stops within its first 64 terms (|s| small or near a power of two) is
-// finished with the plain rounded chain, so the worst case is the chain's cost.  The
-// result is the reference's sum bit for bit on any input.
+// finished with the plain rounded chain.  Such a window costs the scan on top of the chain,
+// so an input whose running sum keeps hovering near a binade boundary would run slower than
+// the plain chain; after kWinSlowRun consecutive short windows the kernel therefore runs
+// kWinChainRun windows as the plain chain (no scan) before it tries the shortcut again.
+// The result is the reference's sum bit for bit on any input.
 constexpr int kWinPer = 16;
 constexpr int kWinWaves = 8;
 constexpr int kWinThreads = 64 * kWinWaves;
 constexpr int kWin = kWinThreads * kWinPer;
+constexpr int kWinSlowRun = 4;
+constexpr int kWinChainRun = 16;
 __global__ __launch_bounds__(kWinThreads) void k_tm_winsum(const double* __restrict__ logs, long long n,
                                                            double* __restrict__ avg, uint32_t* __restrict__ sel,
                                                            uint32_t k) {
@@ -174,11 +179,24 @@ __global__ __launch_bounds__(kWinThreads) void k_tm_winsum(const double* __restr
     load(cur, 0);
     double s = 0.0;   // the running sum: the same value in every thread
     long long a = 0;
+    int slow = 0;     // consecutive short windows; >= kWinSlowRun: chain mode
     while (a < n) {
 #pragma unroll
         for (int t = 0; t < kWinPer; ++t) buf[tid * kWinPer + t] = cur[t];
         load(nxt, a + kWin);   // speculative: the next window if this one is consumed whole
         const long long rem = n - a;
+        if (slow >= kWinSlowRun) {         // chain mode: the reference's rounded adds, no scan
+            __syncthreads();
+            const int m = rem < kWin ? (int)rem : kWin;
+#pragma unroll 8
+            for (int j = 0; j < m; ++j) s = s + buf[j];
+            a += kWin;
+#pragma unroll
+            for (int t = 0; t < kWinPer; ++t) cur[t] = nxt[t];
+            if (++slow >= kWinSlowRun + kWinChainRun) slow = 0;
+            __syncthreads();
+            continue;
+        }
         int e = 0;
         const double fr = frexp(s, &e);
         // integers in units of u, held in doubles: every running value of a valid prefix lies in
@@ -249,6 +267,7 @@ __global__ __launch_bounds__(kWinThreads) void k_tm_winsum(const double* __restr
         const double pf = f >= kWin ? M + all : pshare;
         if (f > 0) s = ldexp(pf, e - 53);
         if (f >= kWin) {   // the whole window took the shortcut
+            slow = 0;
             a += kWin;
 #pragma unroll
             for (int t = 0; t < kWinPer; ++t) cur[t] = nxt[t];
@@ -258,6 +277,7 @@ __global__ __launch_bounds__(kWinThreads) void k_tm_winsum(const double* __restr
         if ((long long)f >= rem) break;   // every remaining term took the shortcut
         s = s + buf[f];                    // the stopping term: the reference's rounded add
         if (f < 64) {                      // slow region: finish the window as a chain
+            ++slow;
             const int m = rem < kWin ? (int)rem : kWin;
 #pragma unroll 8
             for (int j = f + 1; j < m; ++j) s = s + buf[j];
@@ -265,6 +285,7 @@ __global__ __launch_bounds__(kWinThreads) void k_tm_winsum(const double* __restr
 #pragma unroll
             for (int t = 0; t < kWinPer; ++t) cur[t] = nxt[t];
         } else {
+            slow = 0;
             a += f + 1;
             load(cur, a);
         }

@@ -18,7 +18,8 @@ and the RNG is keyed by pixel / sample / ray-tree node, never by device):
 * one process per GPU (torch.distributed launch, bench.py): rank r renders part r of N
   with ``DeviceScene.render_device(..., part=(r, N))`` into its own HBM, and
   ``copy_part_to_host`` DMAs its rows into a ``SharedFrame`` -- one page-locked
-  shared-memory framebuffer mapped by every rank on the node.
+  shared-memory framebuffer mapped by every rank on the node; after a barrier
+  ``finish_frame`` tonemaps the gathered frame on rank 0 for a <Tonemap> camera.
 
 ``sample_range`` (sample-parallel split with host accumulation) is kept for
 multi-sample cameras whose frame is too small to cut.
@@ -138,3 +139,20 @@ def render_part(ds, rank: int, world: int, d_hdr: int, d_ldr: int, stream: int, 
     if frame is not None:
         ds.copy_part_to_host(d_hdr if frame.hdr is not None else 0, d_ldr if frame.ldr is not None else 0,
                              frame.hdr_ptr(), frame.ldr_ptr(), stream, camera=camera, part=(rank, world))
+
+
+def finish_frame(host, frame: SharedFrame, camera: int = 0, rank: int = 0, device: int = 0) -> bool:
+    """After every rank's part has landed in ``frame`` (a barrier): a camera with a <Tonemap>
+    needs the whole frame (the log-average and the burn percentile are over all pixels,
+    tonemapper.h:28-60), so rank 0 tonemaps the gathered float image into the frame's LDR,
+    as main.cpp:187-192 does after its threads join.  The parts' own LDR rows hold the
+    un-tonemapped clamp until then.  Returns True when it tonemapped."""
+    params = host.tonemap_params(camera)
+    if params is None or rank != 0:
+        return False
+    if frame.hdr is None or frame.ldr is None:
+        raise ValueError("a tonemapped camera's shared frame needs both the float and the 8-bit image")
+    import rtgpu
+    frame.ldr[...] = rtgpu.tonemap(frame.hdr, *params, device=device)
+    return True
+

@@ -32,6 +32,7 @@ RTG_RENDER_TREE = 16
 RTG_RENDER_EXACT_SHADOW = 32
 RTG_RENDER_ORDERED = 64
 RTG_LOAD_DEVICE_BVH = 1
+RTG_CAMERA_SIZE = 392   # sizeof(rtg_camera), checked against the C compiler by tests/test_abi.py
 
 
 class RTGError(RuntimeError):
@@ -43,6 +44,21 @@ class RTGError(RuntimeError):
 class TonemapParams(ctypes.Structure):
     _fields_ = [("key", ctypes.c_float), ("burn_percent", ctypes.c_float), ("saturation", ctypes.c_float),
                 ("gamma", ctypes.c_float)]
+
+
+class _Camera(ctypes.Structure):
+    """Head of rtg_camera (include/rtgpu.h) up to the tonemapper parameters."""
+    _fields_ = [("f3", ctypes.c_float * 15), ("ext", ctypes.c_float * 5), ("width", ctypes.c_int32),
+                ("height", ctypes.c_int32), ("spp", ctypes.c_int32), ("focus_distance", ctypes.c_float),
+                ("aperture", ctypes.c_float), ("has_tonemapper", ctypes.c_int32), ("tm_key", ctypes.c_float),
+                ("tm_burn", ctypes.c_float), ("tm_saturation", ctypes.c_float), ("tm_gamma", ctypes.c_float)]
+
+
+class _DescHead(ctypes.Structure):
+    """Head of rtg_scene_desc (include/rtgpu.h) up to the camera list."""
+    _fields_ = [("background", ctypes.c_int32 * 3), ("shadow_epsilon", ctypes.c_float),
+                ("max_recursion_depth", ctypes.c_int32), ("bg_texture", ctypes.c_int32),
+                ("ambient_light", ctypes.c_float * 3), ("cameras", ctypes.c_void_p), ("num_cameras", ctypes.c_int32)]
 
 
 class RenderOpts(ctypes.Structure):
@@ -169,6 +185,17 @@ class HostScene:
         _check(lib().rtg_desc_camera_info(self.desc, idx, ctypes.byref(w), ctypes.byref(h),
                                           ctypes.byref(s), ctypes.byref(t)))
         return {"width": w.value, "height": h.value, "spp": s.value, "tonemapped": bool(t.value)}
+
+    def tonemap_params(self, idx: int = 0):
+        """(key, burn %, saturation, gamma) of camera idx's <Tonemap> (tonemapper.h:18-25), or
+        None for a camera without one."""
+        head = _DescHead.from_address(self.desc)
+        if not 0 <= idx < head.num_cameras:
+            raise RTGError(-1, "camera index out of range")
+        cam = _Camera.from_address(head.cameras + idx * RTG_CAMERA_SIZE)
+        if not cam.has_tonemapper:
+            return None
+        return (cam.tm_key, cam.tm_burn, cam.tm_saturation, cam.tm_gamma)
 
     def counts(self) -> dict:
         v = [ctypes.c_int64() for _ in range(4)]

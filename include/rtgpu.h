@@ -316,8 +316,12 @@ typedef struct {
      * RTG_PART_BAND_ROWS rows; band b (counted from row_begin) belongs to part
      * b % part_count.  A render with part_count > 1 computes and writes only the pixels
      * of part part_index; the union of parts 0..part_count-1 is bit-identical to the
-     * whole render (pixels are independent, the RNG is keyed by pixel).  This is how
-     * the frame is dealt to the GPUs of a node (main.cpp:38-39 deals row bands to
+     * whole render (pixels are independent, the RNG is keyed by pixel).  Exception: for
+     * a camera with a <Tonemap>, a part's LDR rows hold clamp((int)c), not the tonemapped
+     * value -- the tonemapper needs the whole frame (tonemapper.h:28-60); a caller that
+     * gathers parts itself runs rtg_tonemap on the gathered float image (multigpu.py
+     * finish_frame), while rtg_render on a multi-replica scene does it internally.  This
+     * is how the frame is dealt to the GPUs of a node (main.cpp:38-39 deals row bands to
      * threads).  part_count <= 0 means 1. */
     int32_t part_index, part_count;
 } rtg_render_opts;

@@ -57,9 +57,9 @@ FIXTURES = {
     "synth_10k": ("generated", 256, 144, "exact", None),
     "ply_quads": ("generated", 160, 120, "exact", None),
     "bump_normal": ("generated", 200, 150, "exact", None),
-    # JPEG textures (stbi_load, nearest / bilinear, replace_kd / blend_kd) and an OpenEXR
-    # background (HDRImage, tinyexr): the image-decoder fixtures of make_images.py in a scene
-    "hdr_jpeg": ("generated", 160, 120, "exact", None),
+    # PNG textures (stbi_load, nearest / bilinear, replace_kd / blend_kd) and a 16-bit PNG
+    # background: the image-decoder fixtures of make_images.py in a scene
+    "image_tex": ("generated", 160, 120, "exact", None),
     # path tracing (raytracer.cpp:135-191): per-pixel mean of AVG_SAMPLES reference samples
     "pt_cornell": ("generated", 64, 64, "stochastic_avg", None),
     "pt_nee": ("generated", 64, 64, "stochastic_avg", None),
@@ -142,10 +142,10 @@ def make_ply_quads():
         f.write(xml)
 
 
-def make_hdr_jpeg():
-    """Two textured quads (4:2:0 baseline and progressive JPEGs) in front of an OpenEXR
+def make_image_tex():
+    """Two textured quads (an RGB and a palette PNG) in front of a 16-bit PNG
     replace_background texture; copies the decoder fixtures to scenes/inputs/."""
-    for f in ("jpg_420.jpg", "jpg_progressive.jpg", "exr_half_zip.exr"):
+    for f in ("png_rgb8.png", "png_pal8.png", "png_rgb16.png"):
         shutil.copyfile(os.path.join(HERE, "images", f), os.path.join(SCENES, "inputs", f))
     xml = """<Scene>
     <MaxRecursionDepth>1</MaxRecursionDepth>
@@ -158,7 +158,7 @@ def make_hdr_jpeg():
             <NearPlane>-1 1 -0.75 0.75</NearPlane>
             <NearDistance>2</NearDistance>
             <ImageResolution>160 120</ImageResolution>
-            <ImageName>hdr_jpeg.png</ImageName>
+            <ImageName>image_tex.png</ImageName>
         </Camera>
     </Cameras>
     <Lights>
@@ -175,9 +175,9 @@ def make_hdr_jpeg():
     </Materials>
     <Textures>
         <Images>
-            <Image id="1">jpg_420.jpg</Image>
-            <Image id="2">jpg_progressive.jpg</Image>
-            <Image id="3">exr_half_zip.exr</Image>
+            <Image id="1">png_rgb8.png</Image>
+            <Image id="2">png_pal8.png</Image>
+            <Image id="3">png_rgb16.png</Image>
         </Images>
         <TextureMap id="1" type="image">
             <ImageId>1</ImageId>
@@ -229,7 +229,7 @@ def make_hdr_jpeg():
     </Objects>
 </Scene>
 """
-    with open(os.path.join(SCENES, "hdr_jpeg.xml"), "w") as f:
+    with open(os.path.join(SCENES, "image_tex.xml"), "w") as f:
         f.write(xml)
 
 
@@ -670,8 +670,8 @@ def prepare(name, src, w, h, edits):
             make_ply_quads()
         elif name == "bump_normal":
             make_bump_normal()
-        elif name == "hdr_jpeg":
-            make_hdr_jpeg()
+        elif name == "image_tex":
+            make_image_tex()
         elif name in PT_SCENES:
             make_pt(name)
         elif name == "c2_cornell":

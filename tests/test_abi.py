@@ -50,13 +50,19 @@ def test_struct_layouts_are_plain_c(tmp_path):
     if not cc:
         pytest.skip("no C compiler")
     src = tmp_path / "sz.c"
-    src.write_text('#include "rtgpu.h"\n#include <stdio.h>\n#include <stddef.h>\nint main(void){printf("%zu %zu %zu\\n", '
-                   'sizeof(rtg_render_opts), sizeof(rtg_stats), offsetof(rtg_render_opts, part_index));return 0;}\n')
+    src.write_text('#include "rtgpu.h"\n#include <stdio.h>\n#include <stddef.h>\nint main(void){printf("%zu %zu %zu %zu %zu %zu %zu\\n", '
+                   'sizeof(rtg_render_opts), sizeof(rtg_stats), offsetof(rtg_render_opts, part_index), '
+                   'sizeof(rtg_camera), offsetof(rtg_camera, tm_gamma), offsetof(rtg_scene_desc, cameras), '
+                   'offsetof(rtg_scene_desc, num_cameras));return 0;}\n')
     exe = tmp_path / "sz"
     subprocess.run([cc, "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
-    opts, stats, part = map(int, subprocess.run([str(exe)], capture_output=True, text=True).stdout.split())
+    opts, stats, part, cam, gamma, cams, ncams = map(
+        int, subprocess.run([str(exe)], capture_output=True, text=True).stdout.split())
     assert (opts, stats) == (ctypes.sizeof(rtgpu.RenderOpts), ctypes.sizeof(rtgpu.Stats))
     assert part == rtgpu.RenderOpts.part_index.offset
+    # the camera / description heads HostScene.tonemap_params reads
+    assert cam == rtgpu.RTG_CAMERA_SIZE and gamma == rtgpu._Camera.tm_gamma.offset
+    assert (cams, ncams) == (rtgpu._DescHead.cameras.offset, rtgpu._DescHead.num_cameras.offset)
 
 
 def test_errors_are_codes_not_crashes(tmp_path):

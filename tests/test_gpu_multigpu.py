@@ -8,7 +8,8 @@ partition must give the single-GPU image bit for bit:
   has one GPU; each replica has its own stream and device buffers, exactly as on N GPUs),
   including a tonemapped camera (tonemap of the gathered frame);
 * one process per "GPU": two / three ranks (gloo) sharing GPU 0, each rendering its part
-  into its own device buffers and DMA-ing its rows into one page-locked /dev/shm frame;
+  into its own device buffers and DMA-ing its rows into one page-locked /dev/shm frame
+  (a tonemapped camera: rank 0 tonemaps the gathered frame, multigpu.finish_frame);
 * the drop-in CLI with --devices.
 """
 import os
@@ -142,7 +143,7 @@ def _rank_main(rank, world, port, shm, scene, out_q):
     try:
         os.chdir(SCENES)
         torch.cuda.set_device(0)
-        hs = R.HostScene(scene + ".xml")
+        hs = R.HostScene(scene)
         ds = R.DeviceScene(hs, 0)
         c = hs.camera(0)
         if rank == 0:
@@ -157,6 +158,7 @@ def _rank_main(rank, world, port, shm, scene, out_q):
         multigpu.render_part(ds, rank, world, d_hdr.data_ptr(), d_ldr.data_ptr(), st, frame)
         torch.cuda.synchronize()
         dist.barrier()
+        multigpu.finish_frame(hs, frame, 0, rank)
         if rank == 0:
             out_q.put((frame.hdr.copy(), frame.ldr.copy()))
         dist.barrier()
@@ -166,10 +168,10 @@ def _rank_main(rank, world, port, shm, scene, out_q):
         dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_process_per_gpu_shared_frame_gather(world):
+@pytest.mark.parametrize("world,tonemapped", [(2, False), (3, False), (2, True)])
+def test_process_per_gpu_shared_frame_gather(world, tonemapped, tmp_path):
     import torch.multiprocessing as mp
-    scene = "synth_10k"
+    scene = _tonemapped_xml(tmp_path) if tonemapped else os.path.join(SCENES, "synth_10k.xml")
     shm = f"rtg_test_{uuid.uuid4().hex[:8]}"
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -185,7 +187,8 @@ def test_process_per_gpu_shared_frame_gather(world):
         if os.path.exists("/dev/shm/" + shm):
             os.unlink("/dev/shm/" + shm)
     assert all(p.exitcode == 0 for p in procs)
-    hs = rtgpu.HostScene(scene + ".xml")
+    hs = rtgpu.HostScene(scene)
+    assert hs.camera(0)["tonemapped"] == tonemapped
     hdr, ldr = rtgpu.DeviceScene(hs, 0).render(0)
     assert _same(ghdr, hdr) and _same(gldr, ldr)
 

@@ -1,12 +1,12 @@
-"""Image decoders of the host loader against the reference's own image classes.
+"""Image decoders of the host loader against the reference's own image class.
 
-Fixtures (tests/golden/make_images.py): small OpenEXR files written by that script's own EXR
-writer (NONE / RLE / ZIPS / ZIP, HALF / FLOAT, RGB / RGBA / one channel / extra channels, a
-decreasing line order, incompressible chunks stored raw) and JPEGs written by PIL (4:4:4, 4:2:2,
-4:2:0, greyscale, restart markers, progressive).  Goldens: the texels HDRImage (tinyexr
-LoadEXR, HDRImage.h:45-72) and LDRImage (stbi_load, LDRImage.h:37-44) read from them, dumped by
-`oracle/_ref/refdriver imgdump` (the reference compiled here).  The loader must reproduce them
-bit for bit, seen through the scene description a parsed <Images> entry produces."""
+Fixtures (tests/golden/make_images.py): small PNGs written by that script's own encoder (grey at
+1/2/4/8/16 bits, grey + alpha, RGB 8/16, RGBA, palette with and without tRNS; every row filter
+type, split IDAT).  Goldens: the texels LDRImage (stbi_load, LDRImage.h:37-44) reads from them,
+dumped by `oracle/_ref/refdriver imgdump` (the reference compiled here).  The loader must
+reproduce them bit for bit, seen through the scene description a parsed <Images> entry
+produces.  JPEG and OpenEXR are outside the loader: refused with
+RTG_ERR_UNSUPPORTED."""
 import ctypes
 import os
 import shutil
@@ -19,8 +19,7 @@ import rtgpu
 
 IMAGES = os.path.join(ob.GOLDEN, "images")
 GOLD = np.load(os.path.join(IMAGES, "decoded.npz"))
-EXR = sorted(f for f in os.listdir(IMAGES) if f.endswith(".exr"))
-JPG = sorted(f for f in os.listdir(IMAGES) if f.endswith(".jpg"))
+PNG = sorted(f for f in os.listdir(IMAGES) if f.endswith(".png"))
 
 SCENE = """<Scene>
     <Cameras><Camera id="1"><Position>0 0 0</Position><Gaze>0 0 -1</Gaze><Up>0 1 0</Up>
@@ -58,7 +57,7 @@ def _texels(hs):
     return info, out
 
 
-@pytest.mark.parametrize("name", EXR + JPG)
+@pytest.mark.parametrize("name", PNG)
 def test_decoder_matches_reference(tmp_path, name):
     base = os.path.splitext(name)[0]
     hs = _load(tmp_path, name)
@@ -69,11 +68,27 @@ def test_decoder_matches_reference(tmp_path, name):
     assert same.all(), (name, int((~same).sum()), np.argwhere(~same)[:5])
 
 
-def test_exr_fixture_semantics():
-    """The goldens themselves carry LoadEXR's conventions: one channel -> grey, a decreasing
-    line order comes out flipped, half specials widen exactly."""
-    g = GOLD["exr_y_float_zip"]
-    assert np.array_equal(g[..., 0], g[..., 1]) and np.array_equal(g[..., 1], g[..., 2])
-    hz = GOLD["exr_half_zips"]
-    assert hz[0, 0, 0] == np.float32(np.float16(6.0e-8)) and np.isinf(hz[0, 5, 0])
-    assert np.signbit(hz[0, 3, 0]) and hz[0, 4, 0] == 65504.0
+@pytest.mark.parametrize("name,data", [("a.jpg", b"\xff\xd8\xff\xe0" + bytes(64)),
+                                       ("a.exr", b"\x76\x2f\x31\x01" + bytes(64))])
+def test_jpeg_exr_refused(tmp_path, name, data):
+    os.makedirs(tmp_path / "inputs", exist_ok=True)
+    (tmp_path / "inputs" / name).write_bytes(data)
+    (tmp_path / "s.xml").write_text(SCENE.replace("IMG", name))
+    old = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        with pytest.raises(rtgpu.RTGError) as e:
+            rtgpu.HostScene(str(tmp_path / "s.xml"))
+    finally:
+        os.chdir(old)
+    assert e.value.code == -6, e.value
+
+
+def test_png_fixture_semantics():
+    """The goldens carry stb's conventions: 16-bit samples keep the high byte, sub-byte grey
+    is scaled to 0..255, a palette with tRNS expands to RGBA."""
+    g16 = GOLD["png_grey16"]
+    assert g16.max() <= 255 and g16.dtype == np.float32
+    g1 = GOLD["png_grey1"]
+    assert set(np.unique(g1)) <= {0.0, 255.0}
+    assert GOLD["png_pal4_trns_info"][2] == 4
