@@ -1907,6 +1907,71 @@ DEV void tile_pixel(const RenderParams& P, int& px, int& py) {
     tile_pixel(P, px, py, crow);
 }
 
+// A wave's 8x8 pixel block (tile_pixel's layout: lane l -> column l & 7, row l >> 3, its
+// rows consecutive image rows) written to the frame in the reference's layout 3 (x + y W)
+// (main.cpp:109-121) as row runs: the colours are staged in LDS and each row's 96 float bytes
+// / 24 LDR bytes go out as 16-B / 4-B stores of consecutive lanes, instead of three scalar
+// stores per lane at a 12-B / 3-B stride (which wrote 2.1x the frame's bytes).  Every lane
+// of the wave must call it; `have` marks the lanes whose pixel is written.
+DEV void store_tile_rgb(float* hdr, unsigned char* out8, int width, int px, int py, bool have, f3 color) {
+    __shared__ float s_tile[4][4 * 64];
+    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+    float* s = s_tile[w];
+    s[3 * l] = color.x;
+    s[3 * l + 1] = color.y;
+    s[3 * l + 2] = color.z;
+    s[192 + l] = have ? 1.0f : 0.0f;
+    const int x0 = __shfl(px, 0), y0 = __shfl(py, 0);   // lane 0: column 0, row 0 of the block
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int r = l / 6, q = l % 6;                      // lanes 0..47: row r, 16-B / 4-B piece q
+    if (hdr) {
+        const bool vec = ((width & 3) == 0) && ((((uintptr_t)hdr) & 15) == 0);
+        if (vec) {
+            if (l < 48) {
+                float* dst = hdr + 3 * ((size_t)(y0 + r) * width + x0) + 4 * q;
+                const int e0 = 4 * q, p0 = r * 8 + e0 / 3, p1 = r * 8 + (e0 + 3) / 3;
+                const float* src = s + 24 * r + e0;
+                if (s[192 + p0] != 0.0f && s[192 + p1] != 0.0f) {
+                    *(float4*)dst = make_float4(src[0], src[1], src[2], src[3]);
+                } else {
+                    for (int k = 0; k < 4; ++k)
+                        if (s[192 + r * 8 + (e0 + k) / 3] != 0.0f) dst[k] = src[k];
+                }
+            }
+        } else {
+            for (int it = 0; it < 3; ++it) {
+                const int j = it * 64 + l, rr = j / 24, e = j % 24, p = rr * 8 + e / 3;
+                if (s[192 + p] != 0.0f) hdr[3 * ((size_t)(y0 + rr) * width + x0) + e] = s[24 * rr + e];
+            }
+        }
+    }
+    if (out8) {
+        const bool vec = ((width & 3) == 0) && ((((uintptr_t)out8) & 3) == 0);
+        if (vec) {
+            if (l < 48) {
+                unsigned char* dst = out8 + 3 * ((size_t)(y0 + r) * width + x0) + 4 * q;
+                const int e0 = 4 * q, p0 = r * 8 + e0 / 3, p1 = r * 8 + (e0 + 3) / 3;
+                const float* src = s + 24 * r + e0;
+                if (s[192 + p0] != 0.0f && s[192 + p1] != 0.0f) {
+                    *(uint32_t*)dst = (uint32_t)ldr(src[0]) | ((uint32_t)ldr(src[1]) << 8) |
+                                      ((uint32_t)ldr(src[2]) << 16) | ((uint32_t)ldr(src[3]) << 24);
+                } else {
+                    for (int k = 0; k < 4; ++k)
+                        if (s[192 + r * 8 + (e0 + k) / 3] != 0.0f) dst[k] = ldr(src[k]);
+                }
+            }
+        } else {
+            for (int it = 0; it < 3; ++it) {
+                const int j = it * 64 + l, rr = j / 24, e = j % 24, p = rr * 8 + e / 3;
+                if (s[192 + p] != 0.0f) out8[3 * ((size_t)(y0 + rr) * width + x0) + e] = ldr(s[24 * rr + e]);
+            }
+        }
+    }
+    __builtin_amdgcn_wave_barrier();   // the block's next use of s_tile comes after every lane read it
+}
+
 template <bool STATS>
 DEV void flush_counters(Cnt<STATS>& cn, DevCounters* counters) {
     if constexpr (STATS) {

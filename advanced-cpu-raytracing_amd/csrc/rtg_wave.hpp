@@ -104,6 +104,18 @@ DEV void finish_pixel(const DevCamera& C, const RenderParams& P, int sample, con
     }
 }
 
+// finish_pixel for every lane of a wave in tile_pixel's layout (uniform call; `have` marks
+// the lanes with a pixel): at 1 spp the wave's 8x8 block goes out as row runs
+// (store_tile_rgb), else per lane.
+DEV void finish_pixel_wave(const DevCamera& C, const RenderParams& P, int sample, const PassOut& O, int pixel, int px,
+                           int py, bool have, f3 color) {
+    if (C.spp <= 1 && !P.accum_only) {
+        store_tile_rgb(O.hdr, O.ldr, C.width, px, py, have, color);
+        return;
+    }
+    if (have) finish_pixel(C, P, sample, O, pixel, color);
+}
+
 // PerformShading's sum for a pixel with at most one light (k_resolve's loop, one slot):
 // ambient + (0 + term if the light is unoccluded) [+ the zero child term].
 DEV f3 resolve_one(f3 base, int flags, bool has_term, f3 term, bool occluded) {
@@ -254,7 +266,7 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
             }
             if (!shadow_occluded<STATS, FEAT, FAST>(S, W, 0, qo, qd, cn)) sum = add(sum, term);
         }
-        if (valid) finish_pixel(C, P, sample, O, pixel, resolve_sum(base, bflags, sum));
+        finish_pixel_wave(C, P, sample, O, pixel, px, py, valid, resolve_sum(base, bflags, sum));
     } else {
     auto push = [&](bool want, f3 target_dir_or_pos, bool directional) {
         // IsInShadow / IsInShadowDirectional shadow-ray set-up (raytracer.cpp:555-584)
@@ -377,12 +389,14 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
         }
     }
     if constexpr (MODE == SH_FUSED) {
+        f3 col = mk(0, 0, 0);
         if (pushed) {
             const bool occluded = shadow_occluded<STATS, FEAT, FAST>(S, W, 0, ro, rd, cn);
-            finish_pixel(C, P, sample, O, pixel, resolve_one(base, bflags, true, term1, occluded));
+            col = resolve_one(base, bflags, true, term1, occluded);
         } else if (valid) {
-            finish_pixel(C, P, sample, O, pixel, resolve_one(base, bflags, has_term, term1, false));
+            col = resolve_one(base, bflags, has_term, term1, false);
         }
+        finish_pixel_wave(C, P, sample, O, pixel, px, py, valid, col);
     }
     if (MODE == SH_ONE && valid && !pushed) finish_pixel(C, P, sample, O, pixel, resolve_one(base, bflags, has_term, term1, false));
     }

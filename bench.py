@@ -215,8 +215,9 @@ def kernel_bytes(st, W, H):
 def pmc_summary(kernel, K, world):
     """Counter-measured bytes per launch of `kernel` for the K-triangle headline scene from
     the newest committed summary (profiles/r*_pmc*.json, tools/pmc_summary.py over separate
-    rocprofv3 --pmc passes of this bench): HBM traffic = 2 x FETCH_SIZE + WRITE_SIZE (gfx950
-    correction, MI355X_MICROARCH.md), L2 hit rate from TCC_HIT / TCC_MISS.  None if absent."""
+    rocprofv3 --pmc passes of this bench, tools/pmc_kernels.py): HBM traffic = 2 x FETCH_SIZE +
+    WRITE_SIZE (gfx950 correction, MI355X_MICROARCH.md), L2 hit rate from TCC_HIT / TCC_MISS,
+    L2 requests, vL1D hit rate, SQ instruction counts and wave-cycle split.  None if absent."""
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc*.json"))):
         rec = json.load(open(f))
@@ -227,32 +228,100 @@ def pmc_summary(kernel, K, world):
         v = rec["kernels"].get(kernel + "<false>") or rec["kernels"].get(kernel)
         if v and "traffic_bytes" in v:
             best = dict(v, source=os.path.basename(f))
+            best.setdefault("l2_request_bytes", 128 * v["l2_requests"] if "l2_requests" in v else None)
+            if best["l2_request_bytes"] is None:
+                del best["l2_request_bytes"]
     return best
 
 
+CLOCK_GHZ = 2.4            # MI355X engine clock (MI355X_MICROARCH.md)
+SIMDS, CUS = 1024, 256     # 256 CUs x 4 SIMDs
+VALU_CYC = 2.0             # one wave64 VALU instruction per 2 cycles per SIMD ("v_fma_f32 (wave64)")
+
+
+def limiter(pmc, kernel_ms):
+    """Which unit limits the kernel, from its counters (profiles/r*_pmc_K*.json, one rocprofv3
+    --pmc pass per counter group) and its live duration: the busy fraction of each unit
+    = work / (units x cycles of the launch).  VALU: SQ_INSTS_VALU x 2 cycles over the 1024
+    SIMDs; SALU: SQ_INSTS_SALU over the 256 CUs' scalar units; L2: TCC_REQ x 128 B against the
+    34.5 TB/s aggregate; HBM: the corrected FETCH + WRITE bytes against 8 TB/s.  A unit at 70 %
+    or more is the bound; when none is and the waves spend 30 % or more of their cycles parked
+    on s_waitcnt (SQ_WAIT_ANY), the kernel is latency-bound: dependent node fetches with too few
+    waves to cover them, the busiest unit listed beside it."""
+    if not pmc or "valu_insts" not in pmc:
+        return None
+    cyc = kernel_ms * 1e-3 * CLOCK_GHZ * 1e9
+    secs = kernel_ms * 1e-3
+    busy = {"valu": pmc["valu_insts"] * VALU_CYC / (SIMDS * cyc),
+            "salu": pmc.get("salu_insts", 0) / (CUS * cyc)}
+    if "l2_request_bytes" in pmc:
+        busy["l2"] = pmc["l2_request_bytes"] / secs / 1e9 / L2_PEAK_GBS
+    if "traffic_bytes" in pmc:
+        busy["hbm"] = pmc["traffic_bytes"] / secs / 1e9 / HBM_PEAK_GBS
+    top = max(busy, key=busy.get)
+    wait = pmc.get("wait_any_frac")
+    bound = top if busy[top] >= 0.7 else ("latency" if wait is not None and wait >= 0.3 else top)
+    return {"bound": bound, "busy": {k: round(v, 4) for k, v in busy.items()},
+            "wave_cycles": {"wait_any": wait, "wait_inst_any": pmc.get("wait_inst_any_frac"),
+                            "active": pmc.get("active_frac")},
+            "l1_hit_rate": pmc.get("l1_hit_rate"), "l2_hit_rate": pmc.get("l2_hit_rate"),
+            "l2_request_bytes": pmc.get("l2_request_bytes"),
+            "per_wave": {k: round(pmc[k + "_insts"] / max(1, pmc.get("waves", 1)), 1)
+                         for k in ("valu", "salu", "vmem_rd", "vmem_wr", "lds", "branch") if k + "_insts" in pmc},
+            "source": pmc.get("source")}
+
+
 def roofline(kernel, algo_bytes, kernel_ms, pmc):
-    """Dominant kernel's roofline.  `achieved` = algorithmic bytes / its average launch time.
-    The peak is that of the level serving those bytes: HBM when the counter-measured HBM
-    traffic is at least half the algorithmic bytes, else L2 (the scene's nodes and
-    triangles are re-read from the caches: the 10 MB headline scene sits in L2 / Infinity
-    Cache and the measured HBM bytes are a few % of the algorithmic ones)."""
+    """Dominant kernel's roofline.  `bound` is measured (limiter(): the busiest unit from the
+    kernel's counters, or "latency" when no unit is half busy and the waves mostly wait on
+    memory).  `achieved` = algorithmic bytes / average launch time, priced against the peak of
+    the level that serves those bytes -- HBM when the counter-measured HBM traffic is at
+    least half the algorithmic bytes, else the L2 aggregate (the scene's nodes and triangles
+    are re-read from the caches); that fraction is a secondary figure (`frac_basis`)."""
     secs = kernel_ms * 1e-3
     achieved = algo_bytes / secs / 1e9
-    traffic = pmc["traffic_bytes"] if pmc else None
+    traffic = pmc["traffic_bytes"] if pmc and "traffic_bytes" in pmc else None
     hbm_gbs = traffic / secs / 1e9 if traffic is not None else None
     serves_hbm = traffic is not None and traffic >= 0.5 * algo_bytes
     peak = HBM_PEAK_GBS if serves_hbm else L2_PEAK_GBS
-    r = {"bound": "hbm" if serves_hbm else "l2", "achieved": round(achieved, 1), "peak": peak, "unit": "GB/s",
-         "frac": round(achieved / peak, 4), "traffic": traffic, "kernel": kernel, "kernel_ms": round(kernel_ms, 4),
+    lim = limiter(pmc, kernel_ms)
+    r = {"bound": lim["bound"] if lim else ("hbm" if serves_hbm else "l2"), "achieved": round(achieved, 1),
+         "peak": peak, "unit": "GB/s", "frac": round(achieved / peak, 4),
+         "frac_basis": ("algorithmic bytes (SURVEY 8d) / " + ("HBM" if serves_hbm else "L2 aggregate") +
+                        " peak -- secondary; the measured limiter is `bound` / `limiter`"),
+         "traffic": traffic, "kernel": kernel, "kernel_ms": round(kernel_ms, 4),
          "algo_bytes_per_launch": int(algo_bytes),
          "hbm_gbs_measured": round(hbm_gbs, 1) if hbm_gbs is not None else None,
          "hbm_frac_measured": round(hbm_gbs / HBM_PEAK_GBS, 4) if hbm_gbs is not None else None,
          "l2_frac": round(achieved / L2_PEAK_GBS, 4)}
+    if lim:
+        r["limiter"] = lim
     if pmc:
         r["traffic_source"] = pmc["source"]
         if "l2_hit_rate" in pmc:
             r["l2_hit_rate"] = pmc["l2_hit_rate"]
     return r
+
+
+def part_scaling(ds, torch, hdr, ldr, sptr, seed, steps, value, frame_s, counts=(2, 4, 8)):
+    """The N-GPU frame on one GPU: every part r of N (the 16-row bands b % N == r,
+    multigpu.py) rendered alone and timed as a step is.  With one GPU per part the N-GPU
+    frame takes the slowest part, so the predicted strong-scaling efficiency is
+    frame / (N x max part) -- launch latency, the tail of a small grid and band imbalance
+    all show up in it (main.cpp:38-39 deals row bands to threads the same way)."""
+    out = {}
+    for n in counts:
+        ms = []
+        for r in range(n):
+            e, _ = measure(lambda: ds.render_device(hdr.data_ptr(), ldr.data_ptr(), sptr, seed=seed, part=(r, n)),
+                           torch, steps, 1, lambda: None)
+            ms.append(e / steps * 1e3)
+        worst = max(ms)
+        out[str(n)] = {"part_ms": [round(x, 4) for x in ms], "max_part_ms": round(worst, 4),
+                       "predicted_efficiency": round(frame_s * 1e3 / (n * worst), 4),
+                       "predicted_mrays_s": round(value * frame_s * 1e3 / worst, 1)}
+        log(f"parts x{n}: max part {worst:.4f} ms, predicted efficiency {out[str(n)]['predicted_efficiency']}")
+    return out
 
 
 def frame_stats(ds, torch, render_counting, reduce_sum):
@@ -448,6 +517,8 @@ def main():
                 pl.close()
                 if ph:
                     ph.close()
+            if world == 1:
+                result["parts"] = part_scaling(ds, torch, hdr, ldr, sptr, seed, args.steps, value, elapsed / args.steps)
             if world == 1:
                 # opt-in ordered closest hit (RTG_RENDER_ORDERED): same frame, its agreement with
                 # the reference-order walk measured here (pixels whose float bits differ)
