@@ -13,6 +13,7 @@
 
 #include "host_assets.hpp"
 #include "host_scene.hpp"
+#include "rtg_ahb.hpp"
 #include "rtg_device.hpp"
 #include "rtg_kernels.hpp"
 #include "rtgpu.h"
@@ -105,7 +106,8 @@ struct rtg_scene {
     DevBuf<rtg::DevSpotLight> spot_lights;
     DevBuf<rtg::DevCounters> counters;
     DevBuf<rtg::WNode> wnodes;
-    DevBuf<rtg::CWNode> cwnodes;
+    DevBuf<rtg::WNode> anodes;
+    DevBuf<float4> ahtris;
     DevBuf<int2> node_up;
     DevBuf<int> face_leaf;
     DevBuf<int> guard;                // RTG_GUARD builds: index-violation bits
@@ -277,6 +279,130 @@ static int build_bvh_on_device(rtg_scene* sc, const rtg_scene_desc* d, bool anyU
     return RTG_OK;
 }
 
+// The reference's BVH (mesh.cpp:23-156, as the description carries it) re-laid in pre-order
+// with skip links (rtg_device.hpp): a stackless walk "hit -> i+1, miss or leaf done -> skip"
+// visits boxes and faces in the order of BVH::IntersectBVH's recursion (bvh.cpp:5-30).
+static int reference_preorder(const rtg_scene_desc* d, std::vector<float4>& nodes, std::vector<int2>& next,
+                              std::vector<int>& meshBegin, std::vector<int>& meshEnd, bool& bigleaf) {
+    nodes.reserve(2 * d->num_nodes); next.reserve(d->num_nodes);
+    for (int m = 0; m < d->num_meshes; ++m) {
+        const rtg_mesh& M = d->meshes[m];
+        const rtg_bvh_node* N = d->nodes + M.node_offset;
+        const int base = (int)(nodes.size() / 2);
+        meshBegin[m] = base;
+        // pre-order, recording each node's subtree end for the skip link
+        std::vector<int> order;
+        order.reserve(M.node_count);
+        std::vector<int> stack{0};
+        while (!stack.empty()) {
+            int k = stack.back();
+            stack.pop_back();
+            if (k < 0 || k >= M.node_count) return set_err(RTG_ERR_INVALID, "mesh %d: corrupt BVH", m);
+            order.push_back(k);
+            if (N[k].left >= 0) { stack.push_back(N[k].left + 1); stack.push_back(N[k].left); }
+        }
+        std::vector<int> pos(M.node_count, -1);
+        for (size_t i = 0; i < order.size(); ++i) pos[order[i]] = (int)i;
+        std::vector<int> size(M.node_count, 1);
+        for (int i = (int)order.size() - 1; i >= 0; --i) {
+            int k = order[i];
+            if (N[k].left >= 0) size[k] = 1 + size[N[k].left] + size[N[k].left + 1];
+        }
+        for (int k : order) {
+            const rtg_bvh_node& n = N[k];
+            int skip = base + pos[k] + size[k];
+            const int first = M.face_offset + n.first;
+            int leaf = -1;
+            if (n.left < 0) leaf = (first < (1 << 23) && n.count < 255) ? (first << 8) | n.count : rtg::LEAF_EXT;
+            if (n.left < 0 && n.count > rtg::kBigLeaf) bigleaf = true;
+            float4 a, b;
+            a.x = n.bmin[0]; a.y = n.bmin[1]; a.z = n.bmin[2]; a.w = n.bmax[0];
+            b.x = n.bmax[1]; b.y = n.bmax[2];
+            std::memcpy(&b.z, &skip, 4);
+            std::memcpy(&b.w, &leaf, 4);
+            nodes.push_back(a); nodes.push_back(b);
+            next.push_back(make_int2(n.left < 0 ? first : -1, n.left < 0 ? n.count : 0));
+        }
+        meshEnd[m] = (int)(nodes.size() / 2);
+    }
+
+    return RTG_OK;
+}
+
+// Any-hit trees of every mesh (rtg_ahb.cpp).  `reach` bounds |A - o| in the mesh's local space
+// for every shadow ray: origins are surface points and ends light points (a directional
+// light's ray matters only inside the scene), so the world box of every object and light,
+// mapped into each object's local space, bounds both.  False (and no trees) when a leaf
+// entry range does not fit its encoding: shadow rays then take the reference walk.
+static bool anyhit_trees(const rtg_scene_desc* d, const std::vector<float4>& nd, const std::vector<int2>& nx,
+                         const std::vector<int>& meshBegin, const std::vector<int>& meshEnd, const float4* htp, int mode,
+                         std::vector<rtg::WNode>& anodes, std::vector<float4>& ahtris, std::vector<int>& aroot,
+                         rtg::AhbStats& ast) {
+    double wlo[3] = {INFINITY, INFINITY, INFINITY}, whi[3] = {-INFINITY, -INFINITY, -INFINITY};
+    auto addp = [&](double x, double y, double z) {
+        const double p[3] = {x, y, z};
+        for (int k = 0; k < 3; ++k) { wlo[k] = std::min(wlo[k], p[k]); whi[k] = std::max(whi[k], p[k]); }
+    };
+    auto xf = [](const double* m, const double* p, double* o) {
+        for (int r = 0; r < 3; ++r) o[r] = m[4 * r] * p[0] + m[4 * r + 1] * p[1] + m[4 * r + 2] * p[2] + m[4 * r + 3];
+    };
+    for (int i = 0; i < d->num_objects; ++i) {
+        const rtg_object& o = d->objects[i];
+        double lo[3], hi[3];
+        if (o.kind == RTG_OBJ_SPHERE) {
+            for (int k = 0; k < 3; ++k) {
+                lo[k] = (&o.center.x)[k] - std::fabs((double)o.radius);
+                hi[k] = (&o.center.x)[k] + std::fabs((double)o.radius);
+            }
+        } else {
+            for (int k = 0; k < 3; ++k) { lo[k] = o.bbox_min[k]; hi[k] = o.bbox_max[k]; }
+        }
+        for (int c = 0; c < 8; ++c) {
+            const double p[3] = {(c & 1) ? hi[0] : lo[0], (c & 2) ? hi[1] : lo[1], (c & 4) ? hi[2] : lo[2]};
+            if (o.kind == RTG_OBJ_INSTANCE) { addp(p[0], p[1], p[2]); continue; }   // world box already
+            double w[3];
+            xf(o.transform, p, w);
+            addp(w[0], w[1], w[2]);
+        }
+    }
+    for (int i = 0; i < d->num_point_lights; ++i)
+        addp(d->point_lights[i].position.x, d->point_lights[i].position.y, d->point_lights[i].position.z);
+    for (int i = 0; i < d->num_spot_lights; ++i)
+        addp(d->spot_lights[i].position.x, d->spot_lights[i].position.y, d->spot_lights[i].position.z);
+    for (int i = 0; i < d->num_area_lights; ++i) {
+        const rtg_area_light& L = d->area_lights[i];
+        for (int c = 0; c < 4; ++c) {
+            const double su = (c & 1) ? 0.5 : -0.5, sv = (c & 2) ? 0.5 : -0.5;
+            addp(L.position.x + (L.u.x * su + L.v.x * sv) * L.extent, L.position.y + (L.u.y * su + L.v.y * sv) * L.extent,
+                 L.position.z + (L.u.z * su + L.v.z * sv) * L.extent);
+        }
+    }
+    std::vector<double> reach(d->num_meshes, 0.0);
+    for (int i = 0; i < d->num_objects; ++i) {
+        const rtg_object& o = d->objects[i];
+        if (o.kind == RTG_OBJ_SPHERE) continue;
+        double mx = 0;
+        for (int k = 0; k < 3; ++k) mx = std::max({mx, std::fabs((double)o.bbox_min[k]), std::fabs((double)o.bbox_max[k])});
+        for (int c = 0; c < 8 && std::isfinite(wlo[0]); ++c) {
+            const double p[3] = {(c & 1) ? whi[0] : wlo[0], (c & 2) ? whi[1] : wlo[1], (c & 4) ? whi[2] : wlo[2]};
+            double l[3];
+            xf(o.inv_transform, p, l);
+            for (int k = 0; k < 3; ++k) mx = std::max(mx, std::fabs(l[k]));
+        }
+        reach[o.mesh] = std::max(reach[o.mesh], 2.0 * std::sqrt(3.0) * mx);
+    }
+    aroot.assign(d->num_meshes, -1);
+    bool ahbOk = true;
+    for (int m = 0; m < d->num_meshes && ahbOk; ++m) {
+        if (meshEnd[m] <= meshBegin[m]) continue;
+        aroot[m] = rtg::build_ahb(nd, nx, meshBegin[m], meshEnd[m], htp, reach[m], (rtg::AhbMode)mode, anodes,
+                                  ahtris, &ast);
+        if (aroot[m] == -2) ahbOk = false;      // leaf encoding exceeded: shadow rays take the reference walk
+    }
+    if (!ahbOk) { anodes.clear(); ahtris.clear(); aroot.assign(d->num_meshes, -1); }
+    return ahbOk;
+}
+
 // Any-hit wide BVH (rtg_device.hpp WNode, rtg_common.hpp trace_any_wide): each mesh's
 // reference BVH (pre-order records with skip links, as uploaded) collapsed to 4-wide nodes.
 // A wide node's children are found by opening, from {left, right}, the inner child of largest
@@ -339,69 +465,6 @@ static int build_wide(const std::vector<float4>& nodes, int root, std::vector<rt
     return rootIdx;
 }
 
-// Compressed copy of a wide node (rtg_device.hpp CWNode).  Per axis, a grid of spacing 2^e
-// over the children's extent with one spare cell on each side (251 cells for the extent):
-// each child's lo / hi plane goes to the grid line at least one cell beyond it, so the
-// dequantised box contains the child box with a cell to spare -- the margin the device's
-// rounding needs (walk_cwide_any).  Checked in exact double arithmetic; a grid too coarse
-// for that (cannot happen for float inputs) doubles the spacing.
-static rtg::CWNode compress_wide(const rtg::WNode& W) {
-    rtg::CWNode C;
-    std::memset(&C, 0, sizeof(C));
-    const float* lo[3] = {&W.lox.x, &W.loy.x, &W.loz.x};
-    const float* hi[3] = {&W.hix.x, &W.hiy.x, &W.hiz.x};
-    const int* ch = &W.child.x;
-    float* org = &C.org.x;
-    unsigned qlo[3] = {0, 0, 0}, qhi[3] = {0, 0, 0};
-    int ebits = 0;
-    for (int a = 0; a < 3; ++a) {
-        double plo = INFINITY, phi = -INFINITY;
-        for (int k = 0; k < 4; ++k)
-            if (ch[k] != rtg::WCHILD_EMPTY) { plo = std::min(plo, (double)lo[a][k]); phi = std::max(phi, (double)hi[a][k]); }
-        if (!(plo <= phi)) plo = phi = 0.0;
-        const double ext = phi - plo;
-        int e;
-        if (ext > 0) e = (int)std::ceil(std::log2(ext / 251.0));
-        else e = (plo != 0.0 ? std::ilogb(plo) : -40) - 16;
-        e = std::max(-100, std::min(100, e));
-        for (;; ++e) {
-            const double sc = std::ldexp(1.0, e);
-            double ov = plo - 2.0 * sc;
-            float of = (float)ov;
-            if ((double)of > ov) of = std::nextafter(of, -INFINITY);
-            bool ok = true;
-            unsigned ql = 0, qh = 0;
-            for (int k = 0; k < 4; ++k) {
-                unsigned l = 255, h = 0;                 // empty slot: an inverted box
-                if (ch[k] != rtg::WCHILD_EMPTY) {
-                    const double fl = std::floor(((double)lo[a][k] - of) / sc) - 1.0;
-                    const double fh = std::ceil(((double)hi[a][k] - of) / sc) + 1.0;
-                    if (fl < 0.0 || fh > 255.0 || !((double)of + fl * sc <= (double)lo[a][k] - sc) ||
-                        !((double)of + fh * sc >= (double)hi[a][k] + sc)) {
-                        ok = false;
-                        break;
-                    }
-                    l = (unsigned)fl;
-                    h = (unsigned)fh;
-                }
-                ql |= l << (8 * k);
-                qh |= h << (8 * k);
-            }
-            if (ok || e >= 100) {
-                org[a] = of;
-                qlo[a] = ql;
-                qhi[a] = qh;
-                ebits |= (e + 128) << (8 * a);
-                break;
-            }
-        }
-    }
-    std::memcpy(&C.org.w, &ebits, 4);
-    C.qxy = make_uint4(qlo[0], qhi[0], qlo[1], qhi[1]);
-    C.qz = make_uint4(qlo[2], qhi[2], 0u, 0u);
-    C.child = W.child;
-    return C;
-}
 
 int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     if (!d || !out) return set_err(RTG_ERR_INVALID, "null argument");
@@ -460,47 +523,10 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     std::vector<float4> nodes;
     std::vector<int2> next;
     bool bigleaf = false;
-    nodes.reserve(2 * d->num_nodes); next.reserve(d->num_nodes);
     std::vector<int> meshBegin(d->num_meshes), meshEnd(d->num_meshes);
-    for (int m = 0; m < d->num_meshes && !gpuBuild; ++m) {
-        const rtg_mesh& M = d->meshes[m];
-        const rtg_bvh_node* N = d->nodes + M.node_offset;
-        const int base = (int)(nodes.size() / 2);
-        meshBegin[m] = base;
-        // pre-order, recording each node's subtree end for the skip link
-        std::vector<int> order;
-        order.reserve(M.node_count);
-        std::vector<int> stack{0};
-        while (!stack.empty()) {
-            int k = stack.back();
-            stack.pop_back();
-            if (k < 0 || k >= M.node_count) return set_err(RTG_ERR_INVALID, "mesh %d: corrupt BVH", m);
-            order.push_back(k);
-            if (N[k].left >= 0) { stack.push_back(N[k].left + 1); stack.push_back(N[k].left); }
-        }
-        std::vector<int> pos(M.node_count, -1);
-        for (size_t i = 0; i < order.size(); ++i) pos[order[i]] = (int)i;
-        std::vector<int> size(M.node_count, 1);
-        for (int i = (int)order.size() - 1; i >= 0; --i) {
-            int k = order[i];
-            if (N[k].left >= 0) size[k] = 1 + size[N[k].left] + size[N[k].left + 1];
-        }
-        for (int k : order) {
-            const rtg_bvh_node& n = N[k];
-            int skip = base + pos[k] + size[k];
-            const int first = M.face_offset + n.first;
-            int leaf = -1;
-            if (n.left < 0) leaf = (first < (1 << 23) && n.count < 255) ? (first << 8) | n.count : rtg::LEAF_EXT;
-            if (n.left < 0 && n.count > rtg::kBigLeaf) bigleaf = true;
-            float4 a, b;
-            a.x = n.bmin[0]; a.y = n.bmin[1]; a.z = n.bmin[2]; a.w = n.bmax[0];
-            b.x = n.bmax[1]; b.y = n.bmax[2];
-            std::memcpy(&b.z, &skip, 4);
-            std::memcpy(&b.w, &leaf, 4);
-            nodes.push_back(a); nodes.push_back(b);
-            next.push_back(make_int2(n.left < 0 ? first : -1, n.left < 0 ? n.count : 0));
-        }
-        meshEnd[m] = (int)(nodes.size() / 2);
+    if (!gpuBuild) {
+        const int rc = reference_preorder(d, nodes, next, meshBegin, meshEnd, bigleaf);
+        if (rc) return rc;
     }
 
     nodes.push_back(make_float4(0.f, 0.f, 0.f, 0.f));     // pad node: walk_bvh prefetches i+1
@@ -573,10 +599,12 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     // shadow-ray acceleration (rtg_common.hpp): parent links + face -> leaf for the walk from
     // the origin's leaf (trace_any_up), and the any-hit wide BVH (trace_any_wide, A/B builds).
     // RTG_NO_FAST_SHADOW=1: shadow rays walk the reference BVH top-down.
-    std::vector<rtg::WNode> wide;
+    std::vector<rtg::WNode> wide, anodes;
+    std::vector<float4> ahtris;
+    int ahbMode = rtg::AHB_SPLIT;
     std::vector<int2> nodeUp;
     std::vector<int> faceLeaf;
-    for (int i = 0; i < d->num_objects; ++i) objs[i].wroot = -1;
+    for (int i = 0; i < d->num_objects; ++i) objs[i].wroot = objs[i].aroot = -1;
     if (!std::getenv("RTG_NO_FAST_SHADOW") && d->num_meshes > 0 && RTG_SHADOW_MODE >= 2) {
         std::vector<float4> dn;
         std::vector<int2> dx;
@@ -611,6 +639,27 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
         }
         for (int i = 0; i < d->num_objects; ++i)
             objs[i].wroot = d->objects[i].kind != RTG_OBJ_SPHERE ? wroot[d->objects[i].mesh] : -1;
+
+        // any-hit tree per mesh (anyhit_trees, rtg_ahb.cpp)
+        std::vector<float4> ht;
+        const float4* htp = tris.data();
+        if (gpuBuild) {
+            ht.resize(3 * (size_t)d->num_faces);
+            HIP_TRY(hipMemcpy(ht.data(), sc->tris.p, ht.size() * sizeof(float4), hipMemcpyDeviceToHost));
+            htp = ht.data();
+        }
+        const char* am = std::getenv("RTG_AHB");
+        ahbMode = !am ? rtg::AHB_SPLIT : (std::strcmp(am, "ref") == 0 ? rtg::AHB_REF
+                                          : std::strcmp(am, "exact") == 0 ? rtg::AHB_EXACT : rtg::AHB_SPLIT);
+        rtg::AhbStats ast;
+        std::vector<int> aroot;
+        anyhit_trees(d, nd, nx, meshBegin, meshEnd, htp, ahbMode, anodes, ahtris, aroot, ast);
+        for (int i = 0; i < d->num_objects; ++i)
+            objs[i].aroot = d->objects[i].kind != RTG_OBJ_SPHERE ? aroot[d->objects[i].mesh] : -1;
+        if (std::getenv("RTG_AHB_VERBOSE"))
+            std::fprintf(stderr, "rtgpu any-hit tree (mode %d): %lld nodes, %lld entries, depth %d, %lld leaf prims, "
+                                 "%lld face prims (%lld on their leaf box)\n",
+                         ahbMode, ast.nodes, ast.entries, ast.max_depth, ast.leaf_prims, ast.face_prims, ast.exact_faces);
     }
     // instance groups: runs of consecutive instances without motion blur, chunked by ~sqrt of
     // the run length, with the exact (min/max) union of the members' world boxes
@@ -794,11 +843,8 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     HIP_TRY(sc->spot_lights.upload(sls)); HIP_TRY(sc->env_images.upload(envs));
     HIP_TRY(sc->mesh_lights.upload(mls)); HIP_TRY(sc->light_faces.upload(lfs));
     HIP_TRY(sc->wnodes.upload(wide));
-    if (RTG_SHADOW_MODE == 4) {
-        std::vector<rtg::CWNode> cw(wide.size());
-        for (size_t i = 0; i < wide.size(); ++i) cw[i] = compress_wide(wide[i]);
-        HIP_TRY(sc->cwnodes.upload(cw));
-    }
+    HIP_TRY(sc->anodes.upload(anodes));
+    HIP_TRY(sc->ahtris.upload(ahtris));
     HIP_TRY(sc->node_up.upload(nodeUp));
     HIP_TRY(sc->face_leaf.upload(faceLeaf));
     std::vector<rtg::DevCounters> zero(1);
@@ -833,7 +879,9 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     for (int k = 0; k < 3; ++k) S.background[k] = d->background[k];
     S.coop = (sc->feat & rtg::FEAT_BIGLEAF) ? 1 : 0;
     S.wnodes = wide.empty() ? nullptr : sc->wnodes.p;
-    S.cwnodes = wide.empty() || RTG_SHADOW_MODE != 4 ? nullptr : sc->cwnodes.p;
+    S.anodes = anodes.empty() ? nullptr : sc->anodes.p;
+    S.ahtris = ahtris.empty() ? nullptr : sc->ahtris.p;
+    S.ahb_split = ahbMode == rtg::AHB_SPLIT && !anodes.empty();
     S.num_faces = (int)d->num_faces;
     S.num_textures = d->num_textures;
     S.num_images = d->num_images;
@@ -1370,3 +1418,39 @@ int rtg_write_hdr(const char* path, int32_t w, int32_t h, const float* rgb) {
 }
 
 }  // extern "C"
+
+extern "C" int rtg_desc_anyhit_check(const rtg_scene_desc* d, int32_t mode, int64_t* out, int32_t n_out) {
+    if (!d || !out || n_out < 8 || mode < 0 || mode > 2) return set_err(RTG_ERR_INVALID, "bad argument");
+    if (d->num_faces > 0 && d->num_nodes == 0) return set_err(RTG_ERR_INVALID, "description without a BVH");
+    try {
+        std::vector<float4> nodes;
+        std::vector<int2> next;
+        std::vector<int> meshBegin(d->num_meshes), meshEnd(d->num_meshes);
+        bool bigleaf = false;
+        int rc = reference_preorder(d, nodes, next, meshBegin, meshEnd, bigleaf);
+        if (rc) return rc;
+        nodes.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
+        nodes.push_back(make_float4(0.f, 0.f, 0.f, 0.f));
+        std::vector<float4> tris(3 * (size_t)d->num_faces);
+        for (int64_t f = 0; f < d->num_faces; ++f) {
+            const rtg_face& F = d->faces[f];
+            tris[3 * f] = make_float4(F.v0.x, F.v0.y, F.v0.z, 0.f);
+            tris[3 * f + 1] = make_float4(F.v0.x - F.v1.x, F.v0.y - F.v1.y, F.v0.z - F.v1.z, 0.f);
+            tris[3 * f + 2] = make_float4(F.v0.x - F.v2.x, F.v0.y - F.v2.y, F.v0.z - F.v2.z, 0.f);
+        }
+        std::vector<rtg::WNode> anodes;
+        std::vector<float4> ahtris;
+        std::vector<int> aroot;
+        rtg::AhbStats ast;
+        const bool ok = anyhit_trees(d, nodes, next, meshBegin, meshEnd, tris.data(), mode, anodes, ahtris, aroot, ast);
+        long long bad = 0;
+        for (int m = 0; m < d->num_meshes && ok; ++m)
+            bad += rtg::ahb_validate(anodes, ahtris, aroot[m], nodes, next, meshBegin[m], meshEnd[m], tris.data());
+        const int64_t v[8] = {ast.nodes, ast.entries, ast.max_depth, ast.leaf_prims, ast.face_prims, ast.exact_faces,
+                              bad, ok ? 1 : 0};
+        for (int k = 0; k < 8; ++k) out[k] = v[k];
+    } catch (const std::bad_alloc&) {
+        return set_err(RTG_ERR_NOMEM, "out of memory");
+    }
+    return RTG_OK;
+}

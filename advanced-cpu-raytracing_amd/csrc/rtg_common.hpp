@@ -256,6 +256,22 @@ DEV bool tri_test(const DevScene& S, int f, const Ray& r, float minT, float& tou
     return t > 0.0f && t < minT;
 }
 
+// Mesh::IntersectFace on a face record (any-hit tree entries: a copy of S.tris[3f..3f+2]).
+DEV bool tri_test_rec(const float4* R, const Ray& r, float minT, float& tout) {
+    const float4 A = R[0], E1 = R[1], E2 = R[2];
+    const float dx = r.d.x, dy = r.d.y, dz = r.d.z;
+    float detA = det3(E1.x, E2.x, dx, E1.y, E2.y, dy, E1.z, E2.z, dz);
+    if (detA == 0) return false;
+    const float sx = A.x - r.o.x, sy = A.y - r.o.y, sz = A.z - r.o.z;
+    float beta = det3(sx, E2.x, dx, sy, E2.y, dy, sz, E2.z, dz) / detA;
+    if (beta < 0) return false;
+    float gama = det3(E1.x, sx, dx, E1.y, sy, dy, E1.z, sz, dz) / detA;
+    if (gama < 0 || gama + beta > 1) return false;
+    float t = det3(E1.x, E2.x, sx, E1.y, E2.y, sy, E1.z, E2.z, sz) / detA;
+    tout = t;
+    return t > 0.0f && t < minT;
+}
+
 // tri_test for traversal: beta and gamma from one reciprocal of detA, with the decisions
 // beta<0, gamma<0 (exact signs unless a quotient underflows) and beta+gamma>1 (taken
 // only when clear of 1 by 4x the error bound) identical to the division form; t itself
@@ -290,6 +306,38 @@ DEV bool tri_test_fast(const DevScene& S, int f, const Ray& r, float minT, float
         }
     }
     return tri_test(S, f, r, minT, tout);
+}
+// The same on a face record (any-hit tree entries).
+DEV bool tri_test_fast_rec(const float4* R, const Ray& r, float minT, float& tout) {
+    const float4 A = R[0], E1 = R[1], E2 = R[2];
+    const float dx = r.d.x, dy = r.d.y, dz = r.d.z;
+    const float detA = det3(E1.x, E2.x, dx, E1.y, E2.y, dy, E1.z, E2.z, dz);
+    if (detA == 0) return false;
+    const float ad = fabsf(detA);
+    if (ad >= 0x1p-100f && ad <= 0x1p100f) {
+        const float rd = __builtin_amdgcn_rcpf(detA);
+        const float sx = A.x - r.o.x, sy = A.y - r.o.y, sz = A.z - r.o.z;
+        const float nb = det3(sx, E2.x, dx, sy, E2.y, dy, sz, E2.z, dz);
+        const float beta = nb * rd;
+        const bool bsure = nb == 0.0f || fabsf(beta) > 1e-30f;
+        if (bsure) {
+            if (beta < 0) return false;
+            const float ng = det3(E1.x, sx, dx, E1.y, sy, dy, E1.z, sz, dz);
+            const float gama = ng * rd;
+            const bool gsure = ng == 0.0f || fabsf(gama) > 1e-30f;
+            if (gsure) {
+                if (gama < 0) return false;
+                const float sum = gama + beta;
+                if (fabsf(sum - 1.0f) > 0x1p-19f * sum + 0x1p-22f) {
+                    if (sum > 1) return false;
+                    float t = det3(E1.x, E2.x, sx, E1.y, E2.y, sy, E1.z, E2.z, sz) / detA;
+                    tout = t;
+                    return t > 0.0f && t < minT;
+                }
+            }
+        }
+    }
+    return tri_test_rec(R, r, minT, tout);
 }
 
 // 64-bit lexicographic (t, face) key of a candidate hit; t > 0, so the float bits order
@@ -781,10 +829,12 @@ DEV bool slab_cons(float lx, float ly, float lz, float hx, float hy, float hz, c
     return (tmax > -1e-30f) & (tmax >= tmin * (1.0f - 0x1p-21f) - 1e-30f) & (tmin < minTc);
 }
 
-// One mesh's wide BVH (local ray lr).  inst_conf: the instance's world box passes at limit
-// (true for plain meshes).  Returns 1 / 0 / -1 as above.  A node's leaf children are tested
-// in place (all lanes stay in step: a separate iteration per leaf measured 2x slower), then
-// the nearest hit inner child is the next node and the others go onto the stack.
+// One mesh's any-hit tree (rtg_ahb.cpp; local ray lr).  inst_conf: the instance's world box
+// passes at limit (true for plain meshes).  Returns 1 / 0 / -1 as above.  A node's leaf
+// children are tested in place (all lanes stay in step: a separate iteration per leaf measured
+// 2x slower), then the nearest hit inner child is the next node and the others go onto the
+// stack.  A leaf is a range of entries, each a face record with its reference leaf node in
+// the first record's w: the exact decisions use that leaf's own box.
 template <bool STATS>
 DEV int walk_wide_any(const DevScene& S, int node, const Ray& lr, float minT0, float limit, bool inst_conf,
                       Cnt<STATS>& c) {
@@ -797,7 +847,7 @@ DEV int walk_wide_any(const DevScene& S, int node, const Ray& lr, float minT0, f
     int sp = 0;
     bool undecided = false;
     while (true) {
-        const WNode* N = S.wnodes + node;
+        const WNode* N = S.anodes + node;
         const float4 lox = N->lox, hix = N->hix, loy = N->loy, hiy = N->hiy, loz = N->loz, hiz = N->hiz;
         const int4 ch = N->child, lf = N->leaf;
         c.wnode();
@@ -828,124 +878,15 @@ DEV int walk_wide_any(const DevScene& S, int node, const Ray& lr, float minT0, f
                 }
                 continue;
             }
-            const int ref = -2 - cr;
-            int first = lidx[k] >> 8, cnt = lidx[k] & 255;
-            if (lidx[k] == LEAF_EXT) {
-                const int2 e = S.node_ext[ref];
-                first = e.x;
-                cnt = e.y;
-            }
-            for (int f = first; f < first + cnt; ++f) {
+            const int first = lidx[k] >> 8, cnt = lidx[k] & 255;
+            for (int e = first; e < first + cnt; ++e) {
                 c.template tri<true>();
                 float t;
-                if (!tri_test_fast(S, f, lr, limit, t)) continue;
-                // exact decisions on the leaf's own (reference) box
+                if (!tri_test_fast_rec(S.ahtris + 3 * (size_t)e, lr, limit, t)) continue;
+                // exact decisions on the face's reference leaf box
+                const int ref = __float_as_int(S.ahtris[3 * (size_t)e].w);
                 const float4 a = S.nodes[2 * ref], b = S.nodes[2 * ref + 1];
-                if (!box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, minT0)) break;   // leaf unreachable
-                if (inst_conf && box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, limit)) return 1;
-                undecided = true;
-            }
-        }
-        if (next >= 0) {
-            node = next;
-            continue;
-        }
-        if (sp == 0) break;
-        node = stack[--sp][tid];
-    }
-    return undecided ? -1 : 0;
-}
-
-// The same walk on the compressed nodes (CWNode).  Per node and axis the grid spacing and the
-// origin become a = 2^e / d and b = (org - o) / d, and each child plane is t = fma(q, a, b)
-// for its 8-bit index q (the near / far plane rows picked once per node by the direction's
-// sign).  Conservative: the dequantised box contains the child box with one grid cell to
-// spare on every side (host side, compress_wide); the computed t of a plane differs from
-// (plane - o) / d by at most ~2^-23 (|b| + |q a|) + 2^-23 |t| (the rcp, two roundings in b,
-// one in the fma), and |b| <= |t| + 255 |a|, so everything but the |t|-relative part is far
-// inside the spare cell, and the |t|-relative part is covered by 2^-19 margins below.
-// Leaf slots carry the reference node, whose record gives the face range (one load per
-// leaf reached); the exact leaf decisions are those of walk_wide_any.
-template <bool STATS>
-DEV int walk_cwide_any(const DevScene& S, int node, const Ray& lr, float minT0, float limit, bool inst_conf,
-                       Cnt<STATS>& c) {
-    __shared__ int stack[RTG_WIDE_STACK][256];
-    const RayRcp q = ray_rcp(lr);
-    if (!q.fast) return -1;                          // zero / tiny direction component: reference walk
-    const float minTc = minT0 * (1.0f + 0x1p-19f);
-    const bool nx = q.ix < 0.f, ny = q.iy < 0.f, nz = q.iz < 0.f;
-    const int tid = threadIdx.x;
-    int sp = 0;
-    bool undecided = false;
-    while (true) {
-        const CWNode* N = S.cwnodes + node;
-        const float4 org = N->org;
-        const uint4 qxy = N->qxy;
-        const uint2 qz = *(const uint2*)&N->qz;
-        const int4 ch = N->child;
-        c.wnode();
-        const int eb = __float_as_int(org.w);
-        const float ax = __builtin_ldexpf(q.ix, (eb & 255) - 128);
-        const float ay = __builtin_ldexpf(q.iy, ((eb >> 8) & 255) - 128);
-        const float az = __builtin_ldexpf(q.iz, ((eb >> 16) & 255) - 128);
-        const float bx = (org.x - lr.o.x) * q.ix, by = (org.y - lr.o.y) * q.iy, bz = (org.z - lr.o.z) * q.iz;
-        // near / far plane rows by the sign of the direction
-        const unsigned nX = nx ? qxy.y : qxy.x, fX = nx ? qxy.x : qxy.y;
-        const unsigned nY = ny ? qxy.w : qxy.z, fY = ny ? qxy.z : qxy.w;
-        const unsigned nZ = nz ? qz.y : qz.x, fZ = nz ? qz.x : qz.y;
-        float tn[4];
-        bool h[4];
-        const int cidx[4] = {ch.x, ch.y, ch.z, ch.w};
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int sh = 8 * k;
-            const float tnx = __builtin_fmaf((float)((nX >> sh) & 255u), ax, bx);
-            const float tfx = __builtin_fmaf((float)((fX >> sh) & 255u), ax, bx);
-            const float tny = __builtin_fmaf((float)((nY >> sh) & 255u), ay, by);
-            const float tfy = __builtin_fmaf((float)((fY >> sh) & 255u), ay, by);
-            const float tnz = __builtin_fmaf((float)((nZ >> sh) & 255u), az, bz);
-            const float tfz = __builtin_fmaf((float)((fZ >> sh) & 255u), az, bz);
-            const float tmin = fmaxf(fmaxf(tnx, tny), tnz);
-            const float tmax = fminf(fminf(tfx, tfy), tfz);
-            tn[k] = tmin;
-            h[k] = (tmax > -1e-30f) & (tmax >= tmin * (1.0f - 0x1p-19f) - 1e-30f) & (tmin < minTc) &
-                   (cidx[k] != WCHILD_EMPTY);
-        }
-        int next = -1;
-        float nextT = INFINITY;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (!h[k]) continue;
-            const int cr = cidx[k];
-            if (cr >= 0) {
-                int spill = cr;
-                if (tn[k] < nextT) {
-                    spill = next;
-                    next = cr;
-                    nextT = tn[k];
-                }
-                if (spill >= 0) {
-                    if (sp < RTG_WIDE_STACK) stack[sp++][tid] = spill;
-                    else undecided = true;
-                }
-                continue;
-            }
-            const int ref = -2 - cr;
-            const float4 b = S.nodes[2 * ref + 1];
-            const int lf = __float_as_int(b.w);
-            int first = lf >> 8, cnt = lf & 255;
-            if (lf == LEAF_EXT) {
-                const int2 e = S.node_ext[ref];
-                first = e.x;
-                cnt = e.y;
-            }
-            for (int f = first; f < first + cnt; ++f) {
-                c.template tri<true>();
-                float t;
-                if (!tri_test_fast(S, f, lr, limit, t)) continue;
-                // exact decisions on the leaf's own (reference) box
-                const float4 a = S.nodes[2 * ref];
-                if (!box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, minT0)) break;   // leaf unreachable
+                if (!box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, minT0)) continue;   // leaf unreachable
                 if (inst_conf && box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, limit)) return 1;
                 undecided = true;
             }
@@ -963,7 +904,7 @@ DEV int walk_cwide_any(const DevScene& S, int node, const Ray& lr, float minT0, 
 // CastShadowRay on the wide BVH: objects in any order (the answer is a boolean), spheres
 // exactly (a sphere hit with t < limit is accepted at any minT_cur >= limit, one with
 // t >= limit never decides).  Returns 1 / 0 / -1 (undecided: run trace<true>).
-template <bool STATS, int FEAT, bool CW = false>
+template <bool STATS, int FEAT>
 DEV int trace_any_wide(const DevScene& S, const Ray& r, float minT0, float limit, Cnt<STATS>& c) {
     const RayRcp rq = (FEAT & FEAT_INSTANCE) ? ray_rcp(r) : RayRcp{};
     if ((FEAT & FEAT_INSTANCE) && !rq.fast) return -1;
@@ -993,8 +934,8 @@ DEV int trace_any_wide(const DevScene& S, const Ray& r, float minT0, float limit
             conf = box_hit_fast(ob.bmin[0], ob.bmin[1], ob.bmin[2], ob.bmax[0], ob.bmax[1], ob.bmax[2], r, rq, limit);
         }
         const Ray lr = (FEAT & FEAT_XFORM) ? trav_ray(ob, r, 0.f) : r;
-        const int res = CW ? walk_cwide_any<STATS>(S, ob.wroot, lr, minT0, limit, conf, c)
-                           : walk_wide_any<STATS>(S, ob.wroot, lr, minT0, limit, conf, c);
+        if (ob.aroot < 0) return -1;                 // no any-hit tree for this mesh: reference walk
+        const int res = walk_wide_any<STATS>(S, ob.aroot, lr, minT0, limit, conf, c);
         if (res > 0) return 1;
         undecided |= res < 0;
     }
@@ -1907,71 +1848,6 @@ DEV void tile_pixel(const RenderParams& P, int& px, int& py) {
     tile_pixel(P, px, py, crow);
 }
 
-// A wave's 8x8 pixel block (tile_pixel's layout: lane l -> column l & 7, row l >> 3, its
-// rows consecutive image rows) written to the frame in the reference's layout 3 (x + y W)
-// (main.cpp:109-121) as row runs: the colours are staged in LDS and each row's 96 float bytes
-// / 24 LDR bytes go out as 16-B / 4-B stores of consecutive lanes, instead of three scalar
-// stores per lane at a 12-B / 3-B stride (which wrote 2.1x the frame's bytes).  Every lane
-// of the wave must call it; `have` marks the lanes whose pixel is written.
-DEV void store_tile_rgb(float* hdr, unsigned char* out8, int width, int px, int py, bool have, f3 color) {
-    __shared__ float s_tile[4][4 * 64];
-    const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
-    float* s = s_tile[w];
-    s[3 * l] = color.x;
-    s[3 * l + 1] = color.y;
-    s[3 * l + 2] = color.z;
-    s[192 + l] = have ? 1.0f : 0.0f;
-    const int x0 = __shfl(px, 0), y0 = __shfl(py, 0);   // lane 0: column 0, row 0 of the block
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int r = l / 6, q = l % 6;                      // lanes 0..47: row r, 16-B / 4-B piece q
-    if (hdr) {
-        const bool vec = ((width & 3) == 0) && ((((uintptr_t)hdr) & 15) == 0);
-        if (vec) {
-            if (l < 48) {
-                float* dst = hdr + 3 * ((size_t)(y0 + r) * width + x0) + 4 * q;
-                const int e0 = 4 * q, p0 = r * 8 + e0 / 3, p1 = r * 8 + (e0 + 3) / 3;
-                const float* src = s + 24 * r + e0;
-                if (s[192 + p0] != 0.0f && s[192 + p1] != 0.0f) {
-                    *(float4*)dst = make_float4(src[0], src[1], src[2], src[3]);
-                } else {
-                    for (int k = 0; k < 4; ++k)
-                        if (s[192 + r * 8 + (e0 + k) / 3] != 0.0f) dst[k] = src[k];
-                }
-            }
-        } else {
-            for (int it = 0; it < 3; ++it) {
-                const int j = it * 64 + l, rr = j / 24, e = j % 24, p = rr * 8 + e / 3;
-                if (s[192 + p] != 0.0f) hdr[3 * ((size_t)(y0 + rr) * width + x0) + e] = s[24 * rr + e];
-            }
-        }
-    }
-    if (out8) {
-        const bool vec = ((width & 3) == 0) && ((((uintptr_t)out8) & 3) == 0);
-        if (vec) {
-            if (l < 48) {
-                unsigned char* dst = out8 + 3 * ((size_t)(y0 + r) * width + x0) + 4 * q;
-                const int e0 = 4 * q, p0 = r * 8 + e0 / 3, p1 = r * 8 + (e0 + 3) / 3;
-                const float* src = s + 24 * r + e0;
-                if (s[192 + p0] != 0.0f && s[192 + p1] != 0.0f) {
-                    *(uint32_t*)dst = (uint32_t)ldr(src[0]) | ((uint32_t)ldr(src[1]) << 8) |
-                                      ((uint32_t)ldr(src[2]) << 16) | ((uint32_t)ldr(src[3]) << 24);
-                } else {
-                    for (int k = 0; k < 4; ++k)
-                        if (s[192 + r * 8 + (e0 + k) / 3] != 0.0f) dst[k] = ldr(src[k]);
-                }
-            }
-        } else {
-            for (int it = 0; it < 3; ++it) {
-                const int j = it * 64 + l, rr = j / 24, e = j % 24, p = rr * 8 + e / 3;
-                if (s[192 + p] != 0.0f) out8[3 * ((size_t)(y0 + rr) * width + x0) + e] = ldr(s[24 * rr + e]);
-            }
-        }
-    }
-    __builtin_amdgcn_wave_barrier();   // the block's next use of s_tile comes after every lane read it
-}
-
 template <bool STATS>
 DEV void flush_counters(Cnt<STATS>& cn, DevCounters* counters) {
     if constexpr (STATS) {
@@ -2012,8 +1888,6 @@ DEV bool shadow_occluded(const DevScene& S, const WaveBufs& W, size_t q, float4 
         res = trace_any_up<STATS, FEAT>(S, r, o.w, d.w, sobj, sface, cn);
 #elif RTG_SHADOW_MODE == 3
         res = trace_any_wide<STATS, FEAT>(S, r, o.w, d.w, cn);
-#elif RTG_SHADOW_MODE == 4
-        res = trace_any_wide<STATS, FEAT, true>(S, r, o.w, d.w, cn);
 #else
         Hit h;
         res = trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;

@@ -40,37 +40,30 @@ struct DevObject {
     double baseInvT[12];            // base mesh's inverseTransposeTransform
     int id;                         // Shape::id (XML id; spheres: never a light's id)
     int group_end;                  // first object of an instance group: one past its last member
-    int wroot;                      // (base) mesh's root in the any-hit wide BVH (WNode), -1: none
-    int pad4;
+    int wroot;                      // (base) mesh's root in the collapsed reference BVH (WNode; ordered walk), -1: none
+    int aroot;                      // (base) mesh's root in the any-hit tree (anodes; shadow rays), -1: none
 };
 
-// Any-hit acceleration for shadow rays (CastShadowRay, raytracer.cpp:585-623, is a boolean:
-// order-free).  A 4-wide BVH collapsed from the reference's own BVH: every child slot is a
-// reference node -- its box copied exactly -- and the leaves are the reference's leaves, so
-// each child box contains (exactly: unions of face boxes) every leaf box below it.  128 B,
-// one cache line pair: the four child boxes as SoA float4 rows, then the child references.
+// 4-wide BVH node, 128 B (one cache line pair): the four child boxes as SoA float4 rows, then
+// the child references.  Two trees use it:
+//   * wnodes: the reference's own BVH collapsed to 4 wide -- every child slot a reference node
+//     with its box copied exactly, leaf slots the reference's leaves (child <= -2: reference
+//     node -2 - child, leaf = its (first << 8) | count or LEAF_EXT) -- for the opt-in ordered
+//     closest-hit walk (trace_ordered);
+//   * anodes: the any-hit tree of shadow rays (rtg_ahb.cpp: binned SAH over the reference's
+//     small leaves and the faces of its large ones); leaf slots (child <= -2) hold a range of
+//     ahtris entries, leaf = (first << 8) | count, count <= 255.
 struct WNode {
     float4 lox, hix, loy, hiy, loz, hiz;
-    int4 child;                     // >= 0: wide node; WCHILD_EMPTY; <= -2: leaf, reference node -2 - child
-    int4 leaf;                      // leaf slots: (first << 8) | count, or LEAF_EXT (node_ext of the reference node)
+    int4 child;                     // >= 0: wide node; WCHILD_EMPTY; <= -2: leaf
+    int4 leaf;                      // leaf slots: see above
 };
 enum : int { WCHILD_EMPTY = -1 };
-// The same node compressed to 64 B (two per cache line; RTG_SHADOW_MODE 4, an A/B build): each child box on
-// a per-node grid -- origin org.xyz, spacing 2^e per axis -- as 8-bit plane indices padded one
-// cell outward (so the dequantised box contains the child box with a cell to spare, which
-// covers the rounding of the device's fma(q, 2^e / d, (org - o) / d)), child j in byte j.
-// Leaf slots carry only the reference node (-2 - ref); its record gives the face range.
-struct CWNode {
-    float4 org;                     // w: int bits (e_x + 128) | (e_y + 128) << 8 | (e_z + 128) << 16
-    uint4 qxy;                      // lo.x, hi.x, lo.y, hi.y
-    uint4 qz;                       // lo.z, hi.z, 0, 0
-    int4 child;                     // as WNode
-};
 // Shadow-ray walk of the wavefront pipeline's k_shadow (rtg_common.hpp): 3 = any-hit on the
-// 4-wide BVH (trace_any_wide; undecided rays take the reference walk: default), 4 = the same on
-// the compressed 64-B nodes (measured slower: 0.311 vs 0.273 ms), 0 = the
+// any-hit tree (trace_any_wide; undecided rays take the reference walk: default), 0 = the
 // reference walk per lane, 1 = the same walks as a wave packet (walk_bvh_packet), 2 = any-hit
-// climb from the ray's origin leaf (trace_any_up).  The ray-tree pipeline's k_shadow always
+// climb from the ray's origin leaf (trace_any_up).  (Round 2's mode 4, the collapsed tree on
+// compressed 64-B nodes, measured slower -- 0.311 vs 0.273 ms -- and was removed.)  The ray-tree pipeline's k_shadow always
 // uses the per-lane reference walk (its secondary rays are incoherent: modes 1-3 measured
 // slower on C5).  Camera rays: RTG_PRIMARY_PACKET (0: per lane, default).  DESIGN.md §5.
 #ifndef RTG_SHADOW_MODE
@@ -175,11 +168,13 @@ struct DevScene {
     float ambient[3];
     int background[3];
     int coop;                        // the scene has large leaves (FEAT_BIGLEAF)
-    const WNode* __restrict__ wnodes;  // any-hit wide BVH (null: shadow rays take the reference walk)
-    const CWNode* __restrict__ cwnodes; // the same, compressed (same node indices)
+    const WNode* __restrict__ wnodes;  // collapsed reference BVH (ordered walk; null: none)
+    const WNode* __restrict__ anodes;  // any-hit tree (null: shadow rays take the reference walk)
+    const float4* __restrict__ ahtris; // its leaf entries: face record, reference leaf node in [0].w
     const int2* __restrict__ node_up;  // per node: (parent, parent's skip); null: no up-walk
     const int* __restrict__ face_leaf; // per face: its leaf node
     int exact_shadow;                  // RTG_RENDER_EXACT_SHADOW: shadow rays take the reference walk
+    int ahb_split;                     // the any-hit tree splits large leaves (AHB_SPLIT)
     int ordered;                       // RTG_RENDER_ORDERED (plain mesh scenes with a wide BVH)
     // RTG_GUARD builds (fault hunting): table sizes and a violation bit mask (rtg_common.hpp GIDX)
     int* guard;

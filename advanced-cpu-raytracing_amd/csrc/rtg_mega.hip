@@ -404,10 +404,9 @@ __global__ __launch_bounds__(256, RTG_MEGA_WAVES) void k_render(DevScene S, DevC
     int px, py;
     tile_pixel(P, px, py);
     Cnt<STATS> cn;
-    f3 color = mk(0, 0, 0);
-    const bool valid = px < C.width && py < P.row_end;
-    if (valid) {
+    if (px < C.width && py < P.row_end) {
         const int pixel = px + py * C.width;
+        f3 color;
         if (C.spp <= 1 && !P.accum_only) {
             color = render_sample<MAXD, STATS, PT>(S, C, px, py, root_key(P.seed, pixel, 0), cn);
         } else {
@@ -432,9 +431,12 @@ __global__ __launch_bounds__(256, RTG_MEGA_WAVES) void k_render(DevScene S, DevC
                 color = mk(acc.x / sumW, acc.y / sumW, acc.z / sumW);
             }
         }
+        if (!P.accum_only) {
+            const size_t idx = 3 * (size_t)pixel;
+            if (hdr) { hdr[idx] = color.x; hdr[idx + 1] = color.y; hdr[idx + 2] = color.z; }
+            if (ldrOut) { ldrOut[idx] = ldr(color.x); ldrOut[idx + 1] = ldr(color.y); ldrOut[idx + 2] = ldr(color.z); }
+        }
     }
-    // the wave's 8x8 block as row runs (store_tile_rgb)
-    if (!P.accum_only) store_tile_rgb(hdr, ldrOut, C.width, px, py, valid, color);
     flush_counters<STATS>(cn, counters);
 }
 

@@ -104,18 +104,6 @@ DEV void finish_pixel(const DevCamera& C, const RenderParams& P, int sample, con
     }
 }
 
-// finish_pixel for every lane of a wave in tile_pixel's layout (uniform call; `have` marks
-// the lanes with a pixel): at 1 spp the wave's 8x8 block goes out as row runs
-// (store_tile_rgb), else per lane.
-DEV void finish_pixel_wave(const DevCamera& C, const RenderParams& P, int sample, const PassOut& O, int pixel, int px,
-                           int py, bool have, f3 color) {
-    if (C.spp <= 1 && !P.accum_only) {
-        store_tile_rgb(O.hdr, O.ldr, C.width, px, py, have, color);
-        return;
-    }
-    if (have) finish_pixel(C, P, sample, O, pixel, color);
-}
-
 // PerformShading's sum for a pixel with at most one light (k_resolve's loop, one slot):
 // ambient + (0 + term if the light is unoccluded) [+ the zero child term].
 DEV f3 resolve_one(f3 base, int flags, bool has_term, f3 term, bool occluded) {
@@ -266,7 +254,7 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
             }
             if (!shadow_occluded<STATS, FEAT, FAST>(S, W, 0, qo, qd, cn)) sum = add(sum, term);
         }
-        finish_pixel_wave(C, P, sample, O, pixel, px, py, valid, resolve_sum(base, bflags, sum));
+        if (valid) finish_pixel(C, P, sample, O, pixel, resolve_sum(base, bflags, sum));
     } else {
     auto push = [&](bool want, f3 target_dir_or_pos, bool directional) {
         // IsInShadow / IsInShadowDirectional shadow-ray set-up (raytracer.cpp:555-584)
@@ -389,14 +377,12 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
         }
     }
     if constexpr (MODE == SH_FUSED) {
-        f3 col = mk(0, 0, 0);
         if (pushed) {
             const bool occluded = shadow_occluded<STATS, FEAT, FAST>(S, W, 0, ro, rd, cn);
-            col = resolve_one(base, bflags, true, term1, occluded);
+            finish_pixel(C, P, sample, O, pixel, resolve_one(base, bflags, true, term1, occluded));
         } else if (valid) {
-            col = resolve_one(base, bflags, has_term, term1, false);
+            finish_pixel(C, P, sample, O, pixel, resolve_one(base, bflags, has_term, term1, false));
         }
-        finish_pixel_wave(C, P, sample, O, pixel, px, py, valid, col);
     }
     if (MODE == SH_ONE && valid && !pushed) finish_pixel(C, P, sample, O, pixel, resolve_one(base, bflags, has_term, term1, false));
     }
@@ -446,10 +432,11 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
     if (!one) sk = SK_ALL;
     // fast any-hit walk (RTG_SHADOW_MODE) unless RTG_RENDER_EXACT_SHADOW asks for the
     // reference walk
-    const bool fast = (RTG_SHADOW_MODE == 4 ? S.cwnodes != nullptr
-                       : RTG_SHADOW_MODE == 3 ? S.wnodes != nullptr
+    // (large-leaf scenes: the split any-hit tree cuts their pole fans into small leaves; with
+    // RTG_AHB=ref / exact they keep the cooperative reference walk unless RTG_WIDE_BIGLEAF)
+    const bool fast = (RTG_SHADOW_MODE == 3 ? S.anodes != nullptr
                                             : RTG_SHADOW_MODE == 2 ? S.node_up != nullptr : S.nodes != nullptr) &&
-                      (!(FEAT & FEAT_BIGLEAF) || wide_bigleaf()) && !S.exact_shadow;
+                      (!(FEAT & FEAT_BIGLEAF) || S.ahb_split || wide_bigleaf()) && !S.exact_shadow;
     // shading fused with the shadow ray: plain shading, the fast any-hit walk (RTG_NO_FUSED_SHADE=1
     // keeps the queue: experiments)
     const bool fused = scene_sk == 0 && fast && !(FEAT & FEAT_BIGLEAF) && nshadow > 0 && !no_fused_shade();

@@ -89,7 +89,7 @@ class Stats(ctypes.Structure):
 EXPORTED = [
     "rtg_host_scene_load_xml", "rtg_host_scene_load_xml_ex", "rtg_host_scene_desc", "rtg_host_scene_free",
     "rtg_scene_export_bvh",
-    "rtg_desc_camera_info", "rtg_desc_counts", "rtg_scene_create", "rtg_scene_destroy",
+    "rtg_desc_camera_info", "rtg_desc_counts", "rtg_desc_anyhit_check", "rtg_scene_create", "rtg_scene_destroy",
     "rtg_device_count", "rtg_render", "rtg_render_device", "rtg_resolve_accum",
     "rtg_scene_stats", "rtg_scene_reset_stats", "rtg_scene_timings", "rtg_tonemap_device", "rtg_tonemap",
     "rtg_tonemap_log_average",
@@ -130,6 +130,7 @@ def lib() -> ctypes.CDLL:
     L.rtg_host_scene_free.restype = None
     L.rtg_desc_camera_info.argtypes = [vp, ctypes.c_int, P(i32), P(i32), P(i32), P(i32)]
     L.rtg_desc_counts.argtypes = [vp] + [P(ctypes.c_int64)] * 4
+    L.rtg_desc_anyhit_check.argtypes = [vp, i32, P(ctypes.c_int64), i32]
     L.rtg_scene_create.argtypes = [vp, ctypes.c_int, P(vp)]
     L.rtg_scene_destroy.argtypes = [vp]
     L.rtg_scene_destroy.restype = None
@@ -201,6 +202,14 @@ class HostScene:
         v = [ctypes.c_int64() for _ in range(4)]
         _check(lib().rtg_desc_counts(self.desc, *[ctypes.byref(x) for x in v]))
         return dict(zip(("objects", "faces", "nodes", "lights"), (x.value for x in v)))
+
+    def anyhit_check(self, mode: int = 2) -> dict:
+        """Host-only build + structural check of the shadow rays' any-hit trees
+        (rtg_desc_anyhit_check; mode 0 reference collapse, 1 SAH over leaves, 2 split)."""
+        out = (ctypes.c_int64 * 8)()
+        _check(lib().rtg_desc_anyhit_check(self.desc, mode, out, 8))
+        keys = ("nodes", "entries", "depth", "leaf_prims", "face_prims", "exact_faces", "violations", "built")
+        return dict(zip(keys, (int(x) for x in out)))
 
     def num_cameras(self) -> int:
         n = 0

@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 4
+#define RTG_ABI_VERSION 5
 
 enum rtg_status {
     RTG_OK = 0,
@@ -252,6 +252,13 @@ int rtg_desc_camera_info(const rtg_scene_desc* desc, int camera, int32_t* width,
                          int32_t* height, int32_t* spp, int32_t* has_tonemapper);
 int rtg_desc_counts(const rtg_scene_desc* desc, int64_t* num_objects, int64_t* num_faces,
                     int64_t* num_nodes, int64_t* num_lights);
+/* Diagnostic (ABI 5, host only, no device): builds the shadow rays' any-hit trees of a
+ * description with a BVH as rtg_scene_create does (mode 0 = the reference's BVH collapsed,
+ * 1 = binned SAH over its leaves, 2 = the default: large leaves split into faces) and checks
+ * them -- every face reached once, box nesting, triangle containment.  out[0..7] = wide
+ * nodes, leaf entries, depth, whole-leaf primitives, split faces, split faces kept on their
+ * leaf box, violations, built (1) or not (0: leaf encoding exceeded). */
+int rtg_desc_anyhit_check(const rtg_scene_desc* desc, int32_t mode, int64_t* out, int32_t n_out);
 
 /* ------------------------------------------------------------------------- */
 /* Device scene + render                                                      */

@@ -1,10 +1,13 @@
 """k_shadow's walk against the per-lane reference-order walk (RTG_RENDER_EXACT_SHADOW).
 The shipped wavefront walk (RTG_SHADOW_MODE 3, rtg_common.hpp trace_any_wide) decides
-CastShadowRay (raytracer.cpp:585-623, a boolean) on a 4-wide BVH collapsed from the
-reference's, by exact sufficient / necessary conditions with a reference-walk fallback
-(k_shadow_fallback); the A/B builds' walks (1: wave packets of the per-lane walk, 2: climbing
-from the ray's origin leaf) pass the same tests.  Every image must be bit-identical -- on every golden scene, through
-the wavefront, ray-tree and fused pipelines, and at the headline's full size."""
+CastShadowRay (raytracer.cpp:585-623, a boolean) on the any-hit tree (rtg_ahb.cpp: binned
+SAH over the reference's small leaves and the faces of its large ones), by exact sufficient /
+necessary conditions on each face's reference leaf box with a reference-walk fallback; the
+A/B trees (RTG_AHB=exact: SAH over the reference's leaves only, RTG_AHB=ref: the reference's
+BVH collapsed) and the A/B builds' walks (1: wave packets of the per-lane walk, 2: climbing
+from the ray's origin leaf) pass the same tests.  Every image must be bit-identical -- on
+every golden scene, through the wavefront, ray-tree and fused pipelines, at the headline's
+full size and on C2-C5 at full size."""
 import os
 
 import numpy as np
@@ -38,6 +41,17 @@ def test_wide_shadow_equals_reference_walk(name, flags):
     ds = rtgpu.DeviceScene(hs, 0)
     hdr, ldr = ds.render(0, flags=flags)
     ehdr, eldr = ds.render(0, flags=flags | rtgpu.RTG_RENDER_EXACT_SHADOW)
+    assert _same(hdr, ehdr) and _same(ldr, eldr)
+
+
+@pytest.mark.parametrize("mode", ["exact", "ref"])
+@pytest.mark.parametrize("name", NAMES)
+def test_anyhit_tree_modes(name, mode, monkeypatch):
+    monkeypatch.setenv("RTG_AHB", mode)
+    hs = rtgpu.HostScene(name + ".xml")
+    ds = rtgpu.DeviceScene(hs, 0)
+    hdr, ldr = ds.render(0)
+    ehdr, eldr = ds.render(0, flags=rtgpu.RTG_RENDER_EXACT_SHADOW)
     assert _same(hdr, ehdr) and _same(ldr, eldr)
 
 
@@ -95,3 +109,34 @@ def test_wide_shadow_configs(tmp_path, cfg):
     finally:
         os.chdir(old)
     assert root
+
+
+@pytest.mark.parametrize("cfg", ["c3", "c3ton", "c4", "c5"])
+def test_wide_shadow_configs_full_size(tmp_path, cfg):
+    """C3 (70k blob, area light, 4 spp), C3 on ton_Roosendaal, C4 (instances, 16 spp) and C5
+    (870k, 4K, 64 spp) at their BASELINE sizes: the shipped render against the reference
+    walk, every pixel; the large-leaf scenes (C3, C3-ton, C4) now take the any-hit tree."""
+    import scenes
+    if cfg == "c3":
+        xml = scenes.config_c3(str(tmp_path))
+    elif cfg == "c3ton":
+        xml = scenes.config_c3_ton(str(tmp_path), os.path.join(SCENES, "ton_Roosendaal_smooth_ply"))
+    elif cfg == "c4":
+        xml = scenes.config_c4(str(tmp_path))
+    else:
+        xml = scenes.config_c5(str(tmp_path))
+    old = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        hs = rtgpu.HostScene(xml)
+        ds = rtgpu.DeviceScene(hs, 0)
+        hdr, ldr = ds.render(0)
+        ehdr, eldr = ds.render(0, flags=rtgpu.RTG_RENDER_EXACT_SHADOW)
+        diff = int((hdr.view(np.uint32) != ehdr.view(np.uint32)).any(axis=2).sum())
+        print(cfg, "differing pixels", diff)
+        assert diff == 0 and _same(ldr, eldr)
+        st = _stats(ds, 0)
+        print(cfg, {k: st[k] for k in ("shadow_rays", "shadow_wide_visits", "shadow_tri_tests", "shadow_fallbacks")})
+    finally:
+        os.chdir(old)
+
