@@ -35,17 +35,21 @@ namespace {
 constexpr int kSplitLeaf = 8;          // reference leaves above this many faces are split into faces
 constexpr int kMaxLeafFaces = 8;
 constexpr int kBins = 32;
-constexpr double kKappaMax = 64.0;
 // Leaf shape: a range of at most `leaf_faces` faces is a leaf outright; up to kMaxLeafFaces
 // the SAH decides, with a face test costing `isect_cost` box tests (RTG_AHB_LEAF /
 // RTG_AHB_CI: A/B experiments).
-int leaf_faces() {
-    static const int v = std::getenv("RTG_AHB_LEAF") ? std::atoi(std::getenv("RTG_AHB_LEAF")) : 2;
-    return v;
+int env_int(const char* name, int dflt) {
+    const char* v = std::getenv(name);
+    return v ? std::atoi(v) : dflt;
 }
+int leaf_faces() { return env_int("RTG_AHB_LEAF", 2); }
+// pad of a split face = 2^pad_exp kappa reach (RTG_AHB_PADEXP: A/B experiments)
+int pad_exp() { return env_int("RTG_AHB_PADEXP", -16); }
+// split faces with kappa above this keep their leaf box (RTG_AHB_KAPPA: A/B experiments)
+double kappa_max() { return env_int("RTG_AHB_KAPPA", 64); }
 double isect_cost() {
-    static const double v = std::getenv("RTG_AHB_CI") ? std::atof(std::getenv("RTG_AHB_CI")) : 2.0;
-    return v;
+    const char* v = std::getenv("RTG_AHB_CI");
+    return v ? std::atof(v) : 2.0;
 }
 
 struct Prim {
@@ -235,7 +239,8 @@ int build_ahb(const std::vector<float4>& nodes, const std::vector<int2>& ext, in
     if (node_end <= node_begin) return -1;
     std::vector<Prim> P;
     std::vector<int> chunks(nodes.size() / 2, 0);   // AHB_REF: prims per reference leaf
-    const double u = std::ldexp(1.0, -12);
+    const double u = std::ldexp(1.0, pad_exp());
+    const double kmax = kappa_max();
     for (int i = node_begin; i < node_end; ++i) {
         if (leaf_of(nodes, i) < 0) continue;
         int first, count;
@@ -267,7 +272,7 @@ int build_ahb(const std::vector<float4>& nodes, const std::vector<int2>& ext, in
             const double n2 = std::sqrt(e2[0] * e2[0] + e2[1] * e2[1] + e2[2] * e2[2]);
             const double nc = std::sqrt(cx * cx + cy * cy + cz * cz);
             const double kappa = nc > 0 ? n1 * n2 / nc : INFINITY;
-            if (!(kappa <= kKappaMax)) {
+            if (!(kappa <= kmax)) {
                 if (st) ++st->exact_faces;           // a sliver: its leaf box
             } else {
                 double mag = 0;

@@ -8,11 +8,15 @@
 
 namespace rtg {
 
-// Topology of the any-hit tree (RTG_AHB environment variable, A/B experiments):
-//   AHB_SPLIT (default) binned-SAH 4-wide tree over the reference's small leaves (exact leaf
-//             boxes) and the single faces of its large leaves (padded triangle boxes);
-//   AHB_EXACT binned SAH over the reference's leaves only (every cull box a reference leaf box);
-//   AHB_REF   the reference's own BVH collapsed to 4 wide (round 2's tree).
+// Topology of the any-hit tree (RTG_AHB environment variable):
+//   AHB_EXACT (default) binned-SAH 4-wide tree over the reference's leaves: every cull box a
+//             reference leaf box, so culling is exact; large-leaf scenes keep the cooperative
+//             reference walk for their shadow rays (a lane alone in a 255-face pole fan stalls
+//             its wave);
+//   AHB_SPLIT (opt-in) the same, the faces of large leaves split into their own primitives
+//             with padded triangle boxes (exact for rays more than ~1 degree off a face's
+//             plane; rtg_ahb.cpp), and large-leaf scenes take the tree;
+//   AHB_REF   the reference's own BVH collapsed to 4 wide (round 2's tree, A/B).
 enum AhbMode { AHB_REF = 0, AHB_EXACT = 1, AHB_SPLIT = 2 };
 
 struct AhbStats {

@@ -377,19 +377,23 @@ static bool anyhit_trees(const rtg_scene_desc* d, const std::vector<float4>& nd,
                  L.position.z + (L.u.z * su + L.v.z * sv) * L.extent);
         }
     }
+    // reach = the diagonal of the local-space box holding the mesh and every world point (the
+    // distance |A - o| between a face and a shadow ray's origin is below it)
     std::vector<double> reach(d->num_meshes, 0.0);
     for (int i = 0; i < d->num_objects; ++i) {
         const rtg_object& o = d->objects[i];
         if (o.kind == RTG_OBJ_SPHERE) continue;
-        double mx = 0;
-        for (int k = 0; k < 3; ++k) mx = std::max({mx, std::fabs((double)o.bbox_min[k]), std::fabs((double)o.bbox_max[k])});
+        double lo[3], hi[3];
+        for (int k = 0; k < 3; ++k) { lo[k] = o.bbox_min[k]; hi[k] = o.bbox_max[k]; }
         for (int c = 0; c < 8 && std::isfinite(wlo[0]); ++c) {
             const double p[3] = {(c & 1) ? whi[0] : wlo[0], (c & 2) ? whi[1] : wlo[1], (c & 4) ? whi[2] : wlo[2]};
             double l[3];
             xf(o.inv_transform, p, l);
-            for (int k = 0; k < 3; ++k) mx = std::max(mx, std::fabs(l[k]));
+            for (int k = 0; k < 3; ++k) { lo[k] = std::min(lo[k], l[k]); hi[k] = std::max(hi[k], l[k]); }
         }
-        reach[o.mesh] = std::max(reach[o.mesh], 2.0 * std::sqrt(3.0) * mx);
+        const double diag = std::sqrt((hi[0] - lo[0]) * (hi[0] - lo[0]) + (hi[1] - lo[1]) * (hi[1] - lo[1]) +
+                                      (hi[2] - lo[2]) * (hi[2] - lo[2]));
+        reach[o.mesh] = std::max(reach[o.mesh], diag);
     }
     aroot.assign(d->num_meshes, -1);
     bool ahbOk = true;
@@ -601,7 +605,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     // RTG_NO_FAST_SHADOW=1: shadow rays walk the reference BVH top-down.
     std::vector<rtg::WNode> wide, anodes;
     std::vector<float4> ahtris;
-    int ahbMode = rtg::AHB_SPLIT;
+    int ahbMode = rtg::AHB_EXACT;
     std::vector<int2> nodeUp;
     std::vector<int> faceLeaf;
     for (int i = 0; i < d->num_objects; ++i) objs[i].wroot = objs[i].aroot = -1;
@@ -649,8 +653,8 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
             htp = ht.data();
         }
         const char* am = std::getenv("RTG_AHB");
-        ahbMode = !am ? rtg::AHB_SPLIT : (std::strcmp(am, "ref") == 0 ? rtg::AHB_REF
-                                          : std::strcmp(am, "exact") == 0 ? rtg::AHB_EXACT : rtg::AHB_SPLIT);
+        ahbMode = !am ? rtg::AHB_EXACT : (std::strcmp(am, "ref") == 0 ? rtg::AHB_REF
+                                          : std::strcmp(am, "split") == 0 ? rtg::AHB_SPLIT : rtg::AHB_EXACT);
         rtg::AhbStats ast;
         std::vector<int> aroot;
         anyhit_trees(d, nd, nx, meshBegin, meshEnd, htp, ahbMode, anodes, ahtris, aroot, ast);

@@ -28,10 +28,7 @@ __global__ __launch_bounds__(256) void k_resolve(const DevCamera C, const Render
 
 // RTG_WIDE_BIGLEAF=1: shadow rays of large-leaf scenes also take the any-hit wide walk
 // (experiment; by default they take the cooperative reference walk)
-bool wide_bigleaf() {
-    static const bool v = std::getenv("RTG_WIDE_BIGLEAF") != nullptr;
-    return v;
-}
+bool wide_bigleaf() { return std::getenv("RTG_WIDE_BIGLEAF") != nullptr; }
 
 bool no_fused_shade() {
     static const bool v = std::getenv("RTG_NO_FUSED_SHADE") != nullptr;

@@ -205,7 +205,7 @@ class HostScene:
 
     def anyhit_check(self, mode: int = 2) -> dict:
         """Host-only build + structural check of the shadow rays' any-hit trees
-        (rtg_desc_anyhit_check; mode 0 reference collapse, 1 SAH over leaves, 2 split)."""
+        (rtg_desc_anyhit_check; mode 0 reference collapse, 1 SAH over leaves (default), 2 split)."""
         out = (ctypes.c_int64 * 8)()
         _check(lib().rtg_desc_anyhit_check(self.desc, mode, out, 8))
         keys = ("nodes", "entries", "depth", "leaf_prims", "face_prims", "exact_faces", "violations", "built")

@@ -254,7 +254,7 @@ int rtg_desc_counts(const rtg_scene_desc* desc, int64_t* num_objects, int64_t* n
                     int64_t* num_nodes, int64_t* num_lights);
 /* Diagnostic (ABI 5, host only, no device): builds the shadow rays' any-hit trees of a
  * description with a BVH as rtg_scene_create does (mode 0 = the reference's BVH collapsed,
- * 1 = binned SAH over its leaves, 2 = the default: large leaves split into faces) and checks
+ * 1 = binned SAH over its leaves, the default, 2 = large leaves split into faces) and checks
  * them -- every face reached once, box nesting, triangle containment.  out[0..7] = wide
  * nodes, leaf entries, depth, whole-leaf primitives, split faces, split faces kept on their
  * leaf box, violations, built (1) or not (0: leaf encoding exceeded). */

@@ -1,6 +1,6 @@
 """The shadow rays' any-hit trees (rtg_ahb.cpp), built on the host exactly as rtg_scene_create
 builds them, checked structurally on every fixture scene in the three modes (0: the reference's
-BVH collapsed, 1: binned SAH over its leaves, 2: the default, large leaves split into single
+BVH collapsed, 1: the default, binned SAH over its leaves, 2: opt-in, large leaves split into single
 faces): every face of a mesh reached by exactly one leaf entry naming its reference leaf, child
 boxes nested in their parent slot's box, every entry's triangle inside its leaf slot's box
 (rtg_desc_anyhit_check).  The traversal answer against the reference walk is the GPU test

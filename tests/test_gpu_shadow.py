@@ -1,10 +1,10 @@
 """k_shadow's walk against the per-lane reference-order walk (RTG_RENDER_EXACT_SHADOW).
 The shipped wavefront walk (RTG_SHADOW_MODE 3, rtg_common.hpp trace_any_wide) decides
 CastShadowRay (raytracer.cpp:585-623, a boolean) on the any-hit tree (rtg_ahb.cpp: binned
-SAH over the reference's small leaves and the faces of its large ones), by exact sufficient /
-necessary conditions on each face's reference leaf box with a reference-walk fallback; the
-A/B trees (RTG_AHB=exact: SAH over the reference's leaves only, RTG_AHB=ref: the reference's
-BVH collapsed) and the A/B builds' walks (1: wave packets of the per-lane walk, 2: climbing
+SAH over the reference's leaves), by exact sufficient / necessary conditions on each face's
+reference leaf box with a reference-walk fallback; the A/B trees (RTG_AHB=split: large leaves
+split into faces with padded boxes, RTG_AHB=ref: the reference's BVH collapsed) and the A/B
+builds' walks (1: wave packets of the per-lane walk, 2: climbing
 from the ray's origin leaf) pass the same tests.  Every image must be bit-identical -- on
 every golden scene, through the wavefront, ray-tree and fused pipelines, at the headline's
 full size and on C2-C5 at full size."""
@@ -44,7 +44,7 @@ def test_wide_shadow_equals_reference_walk(name, flags):
     assert _same(hdr, ehdr) and _same(ldr, eldr)
 
 
-@pytest.mark.parametrize("mode", ["exact", "ref"])
+@pytest.mark.parametrize("mode", ["split", "ref"])
 @pytest.mark.parametrize("name", NAMES)
 def test_anyhit_tree_modes(name, mode, monkeypatch):
     monkeypatch.setenv("RTG_AHB", mode)
@@ -112,11 +112,14 @@ def test_wide_shadow_configs(tmp_path, cfg):
 
 
 @pytest.mark.parametrize("cfg", ["c3", "c3ton", "c4", "c5"])
-def test_wide_shadow_configs_full_size(tmp_path, cfg):
+@pytest.mark.parametrize("mode", ["exact", "split"])
+def test_wide_shadow_configs_full_size(tmp_path, cfg, mode, monkeypatch):
     """C3 (70k blob, area light, 4 spp), C3 on ton_Roosendaal, C4 (instances, 16 spp) and C5
     (870k, 4K, 64 spp) at their BASELINE sizes: the shipped render against the reference
-    walk, every pixel; the large-leaf scenes (C3, C3-ton, C4) now take the any-hit tree."""
+    walk, every pixel, with the default tree and with large leaves split (RTG_AHB=split,
+    which large-leaf scenes C3, C3-ton and C4 then take)."""
     import scenes
+    monkeypatch.setenv("RTG_AHB", mode)
     if cfg == "c3":
         xml = scenes.config_c3(str(tmp_path))
     elif cfg == "c3ton":
