@@ -8,10 +8,14 @@ host beside it.
         --master-port P bench.py --gpus N --steps K --warmup W
 
 A step = one full 1920x1080 frame (one sample pass) traced and shaded, inputs (scene, BVH)
-resident in HBM.  With N ranks the frame is partitioned (multigpu.py): rank r renders the
-16-row bands b with b % N == r into its own HBM -- strong scaling of one frame, no collective
-on the data path (the barriers around the timed region and the max-over-ranks of the elapsed
-time are the only collectives).  `value` = rays of the frame x steps / max-over-ranks time.
+resident in HBM.  With N ranks every frame is partitioned (multigpu.py): rank r renders the
+16-row bands b with b % N == r into its own HBM -- no collective on the data path (the
+barriers around the timed region and the max-over-ranks of the elapsed time are the only
+collectives).  The steps rotate over 8 scene replicas, each on its own stream ("frames in
+flight"), so a frame's kernels overlap the next frames' -- a part of 1/N of one frame alone
+is too small a grid to keep a GPU busy; `config.serial` times the same steps
+on one stream, one frame after the other.  `value` = rays of the frames x steps /
+max-over-ranks time.
 The host framebuffer gather (every rank DMA-ing its rows into one page-locked shared frame)
 is timed separately ("gather"); the one-process host-buffer path of the CLI ("host_frame")
 too -- neither is `value` (the PCIe-inclusive rates).
@@ -25,6 +29,14 @@ import subprocess
 import sys
 import tempfile
 import time
+
+# Frames in flight: every step renders one frame, and the steps rotate over FRAMES_IN_FLIGHT
+# scene replicas, each on its own stream, so one frame's kernels overlap the next frames' (a
+# part of 1/N of a frame is too small a grid to fill the GPU on its own: DESIGN.md §6).  Each
+# stream needs its own hardware queue (HIP's default is 4 per process); set before the HIP
+# runtime starts.
+if "--help" not in sys.argv and "-h" not in sys.argv:
+    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "advanced-cpu-raytracing_amd")
@@ -50,6 +62,9 @@ def parse():
     p.add_argument("--no-extras", action="store_true", help="skip gather / host-frame timings")
     p.add_argument("--config", default="headline", choices=["headline", "c2", "c3", "c3ton", "c4", "c5"],
                    help="BASELINE.json configuration (c2-c5: one frame = all camera samples)")
+    p.add_argument("--inflight", type=int, default=0,
+                   help="frames in flight (scene replicas / streams the steps rotate over); 0 = 8 for the "
+                        "headline, 1 for c2-c5")
     return p.parse_args()
 
 
@@ -158,14 +173,20 @@ def cpu_baseline(xml_dir, xml, rays_per_frame, reps):
 
 
 # ----------------------------------------------------------------------------- timing
-def measure(render, torch, steps, warmup, barrier):
+def measure(render, torch, steps, warmup, barrier, serial=None):
     """Wall time of exactly `steps` frames between barrier + synchronize on both sides (no
-    event records inside the timed loop: they cost ~0.01 ms per frame, tools/diag_streams.py),
-    and, from a separate untimed pass with an event pair around each frame, the mean GPU time
-    per frame."""
-    stream = torch.cuda.current_stream()
+    event records inside the timed loop: they cost ~0.01 ms per frame, tools/diag_streams.py);
+    `render(k)` issues step k (with frames in flight, on the stream of replica k % F -- the
+    device-wide synchronize waits for all of them).  From a separate untimed pass of
+    `serial()` (one replica, one stream) with an event pair around each frame: the mean GPU
+    time of one frame alone."""
+    import inspect
+    if len(inspect.signature(render).parameters) == 0:
+        r0 = render
+        render = lambda k: r0()  # noqa: E731
+    serial = serial or (lambda: render(0))
     for k in range(warmup):
-        render()
+        render(k)
         torch.cuda.synchronize()
         log(f"warmup {k + 1}/{warmup}")
     torch.cuda.synchronize()
@@ -173,15 +194,16 @@ def measure(render, torch, steps, warmup, barrier):
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(steps):
-        render()
+        render(k)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
+    stream = torch.cuda.current_stream()
     starts = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
     ends = [torch.cuda.Event(enable_timing=True) for _ in range(steps)]
     for k in range(steps):
         starts[k].record(stream)
-        render()
+        serial()
         ends[k].record(stream)
     torch.cuda.synchronize()
     kern_ms = sum(s.elapsed_time(e) for s, e in zip(starts, ends)) / steps
@@ -303,18 +325,24 @@ def roofline(kernel, algo_bytes, kernel_ms, pmc):
     return r
 
 
-def part_scaling(ds, torch, hdr, ldr, sptr, seed, steps, value, frame_s, counts=(2, 4, 8)):
+def part_scaling(reps, torch, seed, steps, value, frame_s, counts=(2, 4, 8)):
     """The N-GPU frame on one GPU: every part r of N (the 16-row bands b % N == r,
-    multigpu.py) rendered alone and timed as a step is.  With one GPU per part the N-GPU
-    frame takes the slowest part, so the predicted strong-scaling efficiency is
-    frame / (N x max part) -- launch latency, the tail of a small grid and band imbalance
-    all show up in it (main.cpp:38-39 deals row bands to threads the same way)."""
+    multigpu.py) rendered alone, with the same frames in flight as the headline steps
+    (`reps`: the replicas the steps rotate over).  With one GPU per part the N-GPU node takes
+    the slowest part's time per frame, so the predicted strong-scaling efficiency is
+    frame / (N x max part) -- band imbalance, launch latency and the tail of a small grid all
+    show up in it (main.cpp:38-39 deals row bands to threads the same way)."""
     out = {}
+    F = len(reps)
     for n in counts:
         ms = []
         for r in range(n):
-            e, _ = measure(lambda: ds.render_device(hdr.data_ptr(), ldr.data_ptr(), sptr, seed=seed, part=(r, n)),
-                           torch, steps, 1, lambda: None)
+            def step(k, r=r, n=n):
+                ds_, h, l, sp = reps[k % F]
+                ds_.render_device(h.data_ptr(), l.data_ptr(), sp, seed=seed, part=(r, n))
+            # warm-up: every replica renders this part once (its tile map for the part's rows is
+            # built on first use)
+            e, _ = measure(step, torch, steps, F, lambda: None, serial=lambda: None)
             ms.append(e / steps * 1e3)
         worst = max(ms)
         out[str(n)] = {"part_ms": [round(x, 4) for x in ms], "max_part_ms": round(worst, 4),
@@ -354,7 +382,8 @@ def sweep_point(args, torch, rtgpu, local, K, hdr, ldr):
         ds.close()
         hs.close()
         return {"mrays_s": round(rays * steps / e / 1e6, 1), "ms_per_frame": round(e / steps * 1e3, 4),
-                "rays": int(rays), "kernels_ms": {k: round(v, 4) for k, v in kt.items()}, "roofline": rl}
+                "rays": int(rays), "kernels_ms": {k: round(v, 4) for k, v in kt.items()}, "roofline": rl,
+                "mode": "serial (one stream, one frame at a time)"}
     finally:
         os.chdir(old)
         shutil.rmtree(sub, ignore_errors=True)
@@ -423,18 +452,40 @@ def main():
         def render(flags=0):
             ds.render_device(hdr.data_ptr(), ldr.data_ptr(), sptr, seed=seed, flags=flags, part=part)
 
+        # frames in flight: replicas 1..F-1 of the scene, each with its own frame buffers and
+        # stream; step k renders frame k on replica k % F (replica 0 = ds on the current stream)
+        F = args.inflight or (8 if args.config == "headline" else 1)
+        reps = [(ds, hdr, ldr, sptr)]
+        streams = []
+        for _ in range(F - 1):
+            s = torch.cuda.Stream()
+            streams.append(s)
+            reps.append((rtgpu.DeviceScene(hs, local), torch.empty_like(hdr), torch.empty_like(ldr), s.cuda_stream))
+
+        def render_step(k):
+            r, h, l, sp = reps[k % F]
+            r.render_device(h.data_ptr(), l.data_ptr(), sp, seed=seed, part=part)
+
+        # set-up: one render per replica (each allocates its work buffers on its first render)
+        for k in range(F):
+            render_step(k)
+        torch.cuda.synchronize()
+
         # untimed counting pass: rays / BVH nodes / triangle tests of the whole frame
         log(f"scene ready: {hs.counts()}, part {rank}/{world}, counting pass")
         part_st, part_rays = frame_stats(ds, torch, lambda: render(rtgpu.RTG_RENDER_COUNT_STATS), lambda s: s)
         st = reduce_sum(part_st)
         rays = st["camera_rays"] + st["secondary_rays"] + st["shadow_rays"]
 
-        log(f"rays/frame {rays} (this part {part_rays}); timing {args.steps} steps")
-        elapsed, kern_ms = measure(render, torch, args.steps, args.warmup, barrier)
+        log(f"rays/frame {rays} (this part {part_rays}); timing {args.steps} steps, {F} frames in flight")
+        elapsed, kern_ms = measure(render_step, torch, args.steps, args.warmup, barrier, serial=lambda: render())
         log(f"timed: {elapsed / args.steps * 1e3:.3f} ms/step")
         elapsed = reduce_max(elapsed)
         kern_ms = reduce_max(kern_ms)
         value = rays * args.steps / elapsed / 1e6
+        # the same frames one after another on one stream (no overlap): the single-frame rate
+        s_el, _ = measure(lambda: render(), torch, args.steps, 1, barrier)
+        s_el = reduce_max(s_el)
 
         ktimes = kernel_times(ds, torch, lambda: render(rtgpu.RTG_RENDER_TIMING), args.steps)
         # the library times the kernels of the last sample pass: bytes of this rank's pass
@@ -473,6 +524,10 @@ def main():
                 "shadow_tri_tests_per_ray": round(st["shadow_tri_tests"] / max(st["shadow_rays"], 1), 2),
                 "parallelism": f"image partition x{world}: 16-row bands dealt round-robin, rank r renders bands "
                                f"b % {world} == r (one frame per step)",
+                "frames_in_flight": F,
+                "serial": {"ms_per_step": round(s_el / args.steps * 1e3, 4),
+                           "mrays_s": round(rays * args.steps / s_el / 1e6, 2),
+                           "what": "the same steps issued on one stream, each frame after the previous one"},
             },
             "roofline": rl,
             "cpu_baseline": None,
@@ -518,7 +573,7 @@ def main():
                 if ph:
                     ph.close()
             if world == 1:
-                result["parts"] = part_scaling(ds, torch, hdr, ldr, sptr, seed, args.steps, value, elapsed / args.steps)
+                result["parts"] = part_scaling(reps, torch, seed, args.steps, value, elapsed / args.steps)
             if world == 1:
                 # opt-in ordered closest hit (RTG_RENDER_ORDERED): same frame, its agreement with
                 # the reference-order walk measured here (pixels whose float bits differ)
@@ -547,9 +602,11 @@ def main():
             sweep = {}
             for Ks in SWEEP_K:
                 if Ks == args.K:
-                    sweep[str(Ks)] = {"mrays_s": round(value, 1), "ms_per_frame": result["ms_per_step"],
+                    ser = result["config"]["serial"]
+                    sweep[str(Ks)] = {"mrays_s": ser["mrays_s"], "ms_per_frame": ser["ms_per_step"],
                                       "rays": int(rays), "kernels_ms": rl["kernels_ms"],
-                                      "roofline": {k: rl[k] for k in rl if k not in ("kernels_ms",)}}
+                                      "roofline": {k: rl[k] for k in rl if k not in ("kernels_ms",)},
+                                      "mode": "serial (one stream, one frame at a time)"}
                     continue
                 log(f"sweep K={Ks}")
                 sweep[str(Ks)] = sweep_point(args, torch, rtgpu, local, Ks, hdr, ldr)

@@ -11,6 +11,11 @@ import sys
 import tempfile
 import time
 
+# RTG_DIAG_QUEUES: hardware queues per process (HIP's default is 4): more streams than queues
+# share them and serialise
+if os.environ.get("RTG_DIAG_QUEUES"):
+    os.environ["GPU_MAX_HW_QUEUES"] = os.environ["RTG_DIAG_QUEUES"]
+
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "advanced-cpu-raytracing_amd"))
 import torch  # noqa: E402
@@ -23,7 +28,8 @@ d = tempfile.mkdtemp()
 xml = scenes.synthetic_heightfield(d)
 os.chdir(d)
 hs = rtgpu.HostScene(xml)
-FMAX = 8
+FS = [int(x) for x in os.environ.get("RTG_DIAG_F", "1,2,4,8").split(",")]
+FMAX = max(FS)
 reps = [rtgpu.DeviceScene(hs, 0) for _ in range(FMAX)]
 c = hs.camera(0)
 H, W = c["height"], c["width"]
@@ -54,11 +60,11 @@ for n in (1, 2, 4, 8):
                               flags=rtgpu.RTG_RENDER_TIMING, part=(0, n))
         for k, v in reps[0].timings().items():
             kt[k] = kt.get(k, 0.0) + v / 5
-    for f in (1, 2, 4, 8):
+    for f in FS:
         ms = run(n, 0, f, steps)
         # f frames' part 0 per ms; an N-GPU node renders f whole frames in this time
         eff = base * f / (n * ms)
-        print(json.dumps({"N": n, "frames_in_flight": f, "ms_per_step": round(ms, 4),
+        print(json.dumps({"N": n, "frames_in_flight": f, "hw_queues": os.environ.get("GPU_MAX_HW_QUEUES", "default"), "ms_per_step": round(ms, 4),
                           "kernels_ms_one_part": {k: round(v, 4) for k, v in kt.items()},
                           "predicted_efficiency": round(eff, 4),
                           "predicted_mrays_s": round(4147193 * f * n / (n * ms * 1e-3) / 1e6, 1)}), flush=True)

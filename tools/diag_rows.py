@@ -1,5 +1,6 @@
 """Where a configuration's traversal time goes: k_primary / k_shadow time and traversal
-counts per 32-row band of one sample pass.  python tools/diag_rows.py [config]"""
+counts per 32-row band (RTG_DIAG_BAND) of one sample pass.  python tools/diag_rows.py [config|headline]
+(headline: the shadow column is k_shade_shadow, shading included; svisits = wide nodes)"""
 import os
 import sys
 import tempfile
@@ -14,21 +15,22 @@ import scenes  # noqa: E402
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c3"
 d = tempfile.mkdtemp()
 os.chdir(d)
-xml = getattr(scenes, "config_" + cfg)(d, spp=1)
+xml = scenes.synthetic_heightfield(d) if cfg == "headline" else getattr(scenes, "config_" + cfg)(d, spp=1)
 hs = rtgpu.HostScene(xml)
 ds = rtgpu.DeviceScene(hs, 0)
 H = hs.camera(0)["height"]
 rows = []
-for r0 in range(0, H, 32):
-    band = (r0, min(H, r0 + 32))
+BAND = int(os.environ.get("RTG_DIAG_BAND", "32"))
+for r0 in range(0, H, BAND):
+    band = (r0, min(H, r0 + BAND))
     for _ in range(2):
         ds.render(0, rows=band, flags=rtgpu.RTG_RENDER_TIMING)
         t = ds.timings()
     ds.reset_stats()
     ds.render(0, rows=band, flags=rtgpu.RTG_RENDER_COUNT_STATS)
     st = ds.stats()
-    rows.append((band, t.get("k_primary", 0), t.get("k_shadow", 0), st["node_visits"], st["tri_tests"],
-                 st["shadow_node_visits"], st["shadow_tri_tests"]))
+    rows.append((band, t.get("k_primary", 0), t.get("k_shadow", 0) + t.get("k_shade_shadow", 0), st["node_visits"],
+                 st["tri_tests"], st["shadow_node_visits"] + st.get("shadow_wide_visits", 0), st["shadow_tri_tests"]))
 tot = sum(r[1] + r[2] for r in rows)
 print(f"{cfg}: sum of band times {tot:.3f} ms")
 for r in rows:
