@@ -4,7 +4,9 @@ image, within the parity tolerance of test_gpu_parity (north_star: 1e-4 per chan
 
 The reduced-size copies of these scenes are pinned to the reference itself by the goldens
 (tests/golden, refdriver); here the full-size frames -- up to 1080x1920 -- are checked
-against the oracle, which is bit-exact to the reference on those goldens.  Fixture edits:
+against the oracle, whole image, and against the reference at native resolution
+(tests/golden/native, make_native.py: its whole 8-bit frame, its float frame at a pixel
+sample, its per-row sums).  Fixture edits:
 cornell_dielectric's camera is reset to look into the box, the akif_uslu scenes lose the
 empty <TexCoordData /> the reference's parser crashes on (parser.cpp:279-291), car_smooth's
 second camera is its own fixture (car_smooth_front)."""
@@ -53,3 +55,8 @@ def test_shipped_scene_native_resolution(tmp_path, name):
     print(name, (w, h), r)
     assert r["rel_pass"] == 1.0, r
     assert np.mean(ldr == oldr) >= 0.9999
+    # the reference itself at native resolution (tests/golden/native, refdriver): every 8-bit
+    # value, the float frame at 8192 sampled pixels, every row's float sum
+    g = ob.compare_native(hdr, ldr, ob.load_native(name), REL)
+    print(name, "vs reference", g)
+    assert g["ldr_equal"] >= 0.9999 and g["sample_pass"] == 1.0 and g["rows_pass"] == 1.0, g
