@@ -241,7 +241,8 @@ struct TreeLevel {
     float4* value;                      // node value (rgb), ray hit something (int bits)
     float4* term;                       // per light slot: Shade term
     unsigned char* occ;                 // per light slot: 1 = in shadow
-    int n;
+    int n;                              // rays (host-driven levels) or the capacity the grids cover
+    const int* nd;                      // device-driven levels: the level's ray count on the device
 };
 // Per-block output segments of k_tree_shade: shadow rays (256 x slots per block, the
 // k_shadow layout) and child rays (512 per block).

@@ -21,12 +21,18 @@
 //
 // Every value is computed by the same expressions in the same order as the recursion
 // (rtg_mega.hip / the reference), so the result is bit-identical to the fused kernel.
+#include <algorithm>
+#include <cstdlib>
 #include <vector>
 
 #include "rtg_common.hpp"
 #include "rtg_kernels.hpp"
 
 namespace rtg {
+
+// the level's ray count: the device's (device-driven levels, written by the previous level's
+// k_tree_scan) or the host's
+DEV int level_n(const TreeLevel& L) { return L.nd ? *L.nd : L.n; }
 
 enum : int { TK_FINAL = 0, TK_LEAF = 1, TK_ADDZERO = 2, TK_MIRROR = 3, TK_CONDUCTOR = 4, TK_TIR = 5, TK_DIEL = 6 };
 enum : int { TK_LIT = 16 };
@@ -51,7 +57,7 @@ __global__ __launch_bounds__(256, RTG_TRACE_WAVES(FEAT)) void k_tree_trace(const
                                                     DevCounters* counters) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     Cnt<STATS> cn;
-    if (i < L.n) {
+    if (i < level_n(L)) {
         const float4 o = L.o[i], d = L.d[i];
         Ray r;
         r.o = mk(o.x, o.y, o.z);
@@ -87,7 +93,7 @@ __global__ __launch_bounds__(256, RTG_TREE_SHADE_WAVES) void k_tree_shade(const 
     if (threadIdx.x == 0) { nShadow = 0; nChild = 0; }
     __syncthreads();
     const int i = blockIdx.x * 256 + threadIdx.x;
-    const bool valid = i < L.n;
+    const bool valid = i < level_n(L);
     Cnt<STATS> cn;
     ShadeCtx c;
     bool lit = false;
@@ -301,8 +307,11 @@ __global__ __launch_bounds__(256, RTG_TREE_SHADE_WAVES) void k_tree_shade(const 
     flush_counters<STATS>(cn, counters);
 }
 
-// exclusive prefix over the per-block child counts (one block); total -> offs[nb]
-__global__ __launch_bounds__(1024) void k_tree_scan(const int* __restrict__ cnt, int nb, int* __restrict__ offs) {
+// exclusive prefix over the per-block child counts (one block); total -> offs[nb] and, for
+// device-driven levels, min(total, cap) -> *next_n (the next level's count) with *overflow
+// set when the planned capacity (0 past the planned levels) is exceeded
+__global__ __launch_bounds__(1024) void k_tree_scan(const int* __restrict__ cnt, int nb, int* __restrict__ offs,
+                                                    int* __restrict__ next_n, int cap, int* __restrict__ overflow) {
     __shared__ int part[1024];
     const int t = threadIdx.x;
     const int per = (nb + 1023) / 1024;
@@ -322,16 +331,23 @@ __global__ __launch_bounds__(1024) void k_tree_scan(const int* __restrict__ cnt,
         offs[b] = run;
         run += cnt[b];
     }
-    if (t == 1023) offs[nb] = part[1023];
+    if (t == 1023) {
+        offs[nb] = part[1023];
+        if (next_n) {
+            *next_n = part[1023] < cap ? part[1023] : cap;
+            if (part[1023] > cap) *overflow = 1;
+        }
+    }
 }
 
 __global__ __launch_bounds__(256) void k_tree_compact(const TreeSegs G, const int* __restrict__ offs,
-                                                      const TreeLevel cur, const TreeLevel nxt) {
+                                                      const TreeLevel cur, const TreeLevel nxt, const int cap) {
     const int b = blockIdx.x;
     const int n = G.c_count[b], base = offs[b];
     for (int k = threadIdx.x; k < n; k += 256) {
         const size_t q = (size_t)b * 512 + k;
         const int dst = base + k;
+        if (dst >= cap) break;                       // over the planned capacity (k_tree_scan flagged it)
         nxt.o[dst] = G.c_o[q];
         nxt.d[dst] = G.c_d[q];
         nxt.key[dst] = G.c_key[q];
@@ -350,7 +366,7 @@ __global__ __launch_bounds__(256) void k_tree_resolve(const DevScene S, const De
                                                       float* __restrict__ hdr, unsigned char* __restrict__ ldrOut,
                                                       float4* __restrict__ accum) {
     const int i = blockIdx.x * 256 + threadIdx.x;
-    if (i >= L.n) return;
+    if (i >= level_n(L)) return;
     const float4 b = L.base[i];
     const int kb = __float_as_int(b.w);
     const int kind = kb & 15;
@@ -381,6 +397,15 @@ __global__ __launch_bounds__(256) void k_tree_resolve(const DevScene S, const De
             const DevMaterial& pm = S.materials[__float_as_int(ex.y)];
             auto child = [&](int slot, f3& v, bool& vHit, float& vT, float& vMed) {
                 const int ci = __float_as_int(slot == 0 ? ex.z : ex.w);
+                if (ci < 0) {
+                    // a child dropped by a device-driven level over its planned capacity: the
+                    // overflow flag is set and the render is redone host-driven
+                    v = mk(0, 0, 0);
+                    vHit = false;
+                    vT = 0.f;
+                    vMed = 1.f;
+                    return;
+                }
                 const float4 cv = Lc.value[ci];
                 v = mk(cv.x, cv.y, cv.z);
                 vHit = __float_as_int(cv.w) != 0;
@@ -467,7 +492,13 @@ struct TreeState {
     TreeSegs G{};
     size_t c_qo = 0, c_qd = 0, c_qs = 0, c_qc = 0, c_o = 0, c_d = 0, c_k = 0, c_m = 0, c_p = 0, c_cc = 0, c_off = 0;
     int* offs = nullptr;
-    int* h_total = nullptr;     // pinned host word
+    int* h_total = nullptr;     // pinned host words: [0] a level's size, [1] the overflow flag
+    // device-driven levels: per level the ray count (written by the previous level's scan) and
+    // the overflow flag; the plan = capacities per level learned from a host-driven pass of
+    // the same frame part (plan_key)
+    int* d_counts = nullptr;    // kMaxLevels + 1 ints, [kMaxLevels] = overflow
+    std::vector<size_t> plan;
+    std::vector<long long> plan_key;
     ~TreeState() {
         auto f = [](void* p) { if (p) (void)hipFree(p); };
         for (auto& lv : levels) {
@@ -476,10 +507,11 @@ struct TreeState {
             f(L.value); f(L.term); f(L.occ);
         }
         f(G.q_o); f(G.q_d); f(G.q_slot); f(G.q_count); f(G.c_o); f(G.c_d); f(G.c_key); f(G.c_miss); f(G.c_parent);
-        f(G.c_count); f(offs);
+        f(G.c_count); f(offs); f(d_counts);
         if (h_total) (void)hipHostFree(h_total);
     }
 };
+constexpr int kMaxLevels = 64;
 
 static hipError_t ensure_level(TreeState::Level& lv, size_t n, int ns) {
     TreeLevel& L = lv.L;
@@ -490,6 +522,7 @@ static hipError_t ensure_level(TreeState::Level& lv, size_t n, int ns) {
     G_(L.term, cte, n * (size_t)(ns > 0 ? ns : 1)); G_(L.occ, coc, n * (size_t)(ns > 0 ? ns : 1));
 #undef G_
     L.n = (int)n;
+    L.nd = nullptr;
     return hipSuccess;
 }
 
@@ -508,15 +541,40 @@ static hipError_t ensure_segs(TreeState& T, size_t blocks, int ns) {
 
 void tree_destroy(TreeState* t) { delete t; }
 
+// One level's trace / shade / shadow / scan launches (rays: L's count, on the host or device).
 template <bool STATS, int FEAT>
-static hipError_t tree_pass(TreeState& T, const DevScene& S, const DevCamera& C, const RenderParams& P, int s,
-                            bool first, bool last, float* hdr, unsigned char* l, float4* accum, DevCounters* cnt,
-                            hipStream_t st, hipEvent_t* ev) {
+static void level_launches(TreeState& T, const DevScene& S, const DevCamera& C, const RenderParams& P, int s,
+                           int level, TreeLevel& L, int blocks, int ns, int* next_n, int cap_next, DevCounters* cnt,
+                           hipStream_t st) {
+    if (level == 0) hipLaunchKernelGGL(k_tree_gen, dim3(blocks), dim3(256), 0, st, C, P, s, L);
+    hipLaunchKernelGGL((k_tree_trace<STATS, FEAT>), dim3(blocks), dim3(256), 0, st, S, L, level, cnt);
+    hipLaunchKernelGGL((k_tree_shade<STATS>), dim3(blocks), dim3(256), 0, st, S, C, L, level, P, T.G, cnt);
+    if (ns > 0) {
+        WaveBufs W{};
+        W.q_o = T.G.q_o; W.q_d = T.G.q_d; W.q_slot = T.G.q_slot; W.q_count = T.G.q_count;
+        W.occ = L.occ;
+        W.num_slots = ns;
+        W.hit_obj = L.obj;              // the hits the shadow rays leave (their origin leaf)
+        W.hit_face = L.face;
+        hipLaunchKernelGGL((k_shadow<STATS, FEAT, false>), dim3(blocks, ns), dim3(256), 0, st, S, W, cnt);
+    }
+    hipLaunchKernelGGL(k_tree_scan, dim3(1), dim3(1024), 0, st, T.G.c_count, blocks, T.offs, next_n, cap_next,
+                       T.d_counts ? T.d_counts + kMaxLevels : nullptr);
+}
+
+// Host-driven sample pass: after each level the next level's size comes back to the host
+// (one stream synchronisation per level), the arrays grow to it.  `sizes` receives the
+// level sizes (the plan of device-driven passes).
+template <bool STATS, int FEAT>
+static hipError_t tree_pass_sync(TreeState& T, const DevScene& S, const DevCamera& C, const RenderParams& P, int s,
+                                 bool first, bool last, float* hdr, unsigned char* l, float4* accum, DevCounters* cnt,
+                                 hipStream_t st, hipEvent_t* ev, std::vector<size_t>& sizes) {
     const int ns = S.num_point + S.num_area + S.num_env + S.num_dir + S.num_spot + S.num_mesh;
     const int npix = P.part_rows * C.width;
     hipError_t e;
     size_t n = (size_t)npix;
     int level = 0;
+    sizes.assign(1, n);
     if (ev) (void)hipEventRecord(ev[0], st);
     for (;; ++level) {
         if ((int)T.levels.size() <= level) T.levels.emplace_back();
@@ -524,28 +582,18 @@ static hipError_t tree_pass(TreeState& T, const DevScene& S, const DevCamera& C,
         TreeLevel& L = T.levels[level].L;
         const int blocks = (int)((n + 255) / 256);
         if ((e = ensure_segs(T, (size_t)blocks, ns)) != hipSuccess) return e;
-        if (level == 0) hipLaunchKernelGGL(k_tree_gen, dim3(blocks), dim3(256), 0, st, C, P, s, L);
-        hipLaunchKernelGGL((k_tree_trace<STATS, FEAT>), dim3(blocks), dim3(256), 0, st, S, L, level, cnt);
-        hipLaunchKernelGGL((k_tree_shade<STATS>), dim3(blocks), dim3(256), 0, st, S, C, L, level, P, T.G, cnt);
-        if (ns > 0) {
-            WaveBufs W{};
-            W.q_o = T.G.q_o; W.q_d = T.G.q_d; W.q_slot = T.G.q_slot; W.q_count = T.G.q_count;
-            W.occ = L.occ;
-            W.num_slots = ns;
-            W.hit_obj = L.obj;              // the hits the shadow rays leave (their origin leaf)
-            W.hit_face = L.face;
-            hipLaunchKernelGGL((k_shadow<STATS, FEAT, false>), dim3(blocks, ns), dim3(256), 0, st, S, W, cnt);
-        }
-        hipLaunchKernelGGL(k_tree_scan, dim3(1), dim3(1024), 0, st, T.G.c_count, blocks, T.offs);
+        level_launches<STATS, FEAT>(T, S, C, P, s, level, L, blocks, ns, nullptr, 0, cnt, st);
         if ((e = hipMemcpyAsync(T.h_total, T.offs + blocks, sizeof(int), hipMemcpyDeviceToHost, st)) != hipSuccess)
             return e;
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
         const size_t nn = (size_t)*T.h_total;
         if (nn == 0) break;
+        if (level + 1 >= kMaxLevels) return hipErrorInvalidValue;
+        sizes.push_back(nn);
         if ((int)T.levels.size() <= level + 1) T.levels.emplace_back();
         if ((e = ensure_level(T.levels[level + 1], nn, ns)) != hipSuccess) return e;
         hipLaunchKernelGGL(k_tree_compact, dim3(blocks), dim3(256), 0, st, T.G, T.offs, T.levels[level].L,
-                           T.levels[level + 1].L);
+                           T.levels[level + 1].L, (int)nn);
         n = nn;
     }
     if (ev) (void)hipEventRecord(ev[1], st);
@@ -560,17 +608,120 @@ static hipError_t tree_pass(TreeState& T, const DevScene& S, const DevCamera& C,
     return hipGetLastError();
 }
 
+// Device-driven sample pass: no host synchronisation.  The levels follow the plan (capacity
+// per level); each level's grids cover its capacity and its kernels read the level's ray count
+// on the device (written by the previous level's scan), blocks past it exit at once.  A level
+// that outgrows its capacity, or children past the planned depth, set the overflow flag; the
+// caller checks it once per render and redoes the render host-driven.
+template <bool STATS, int FEAT>
+static hipError_t tree_pass_async(TreeState& T, const DevScene& S, const DevCamera& C, const RenderParams& P, int s,
+                                  bool first, bool last, float* hdr, unsigned char* l, float4* accum,
+                                  DevCounters* cnt, hipStream_t st, hipEvent_t* ev) {
+    const int ns = S.num_point + S.num_area + S.num_env + S.num_dir + S.num_spot + S.num_mesh;
+    const int D = (int)T.plan.size();
+    if (ev) (void)hipEventRecord(ev[0], st);
+    for (int level = 0; level < D; ++level) {
+        TreeLevel& L = T.levels[level].L;
+        L.n = (int)T.plan[level];
+        L.nd = level == 0 ? nullptr : T.d_counts + level;
+        const int blocks = (int)((T.plan[level] + 255) / 256);
+        const bool more = level + 1 < D;
+        level_launches<STATS, FEAT>(T, S, C, P, s, level, L, blocks, ns, T.d_counts + level + 1,
+                                    more ? (int)T.plan[level + 1] : 0, cnt, st);
+        if (more) {
+            TreeLevel& Ln = T.levels[level + 1].L;
+            Ln.n = (int)T.plan[level + 1];
+            Ln.nd = T.d_counts + level + 1;
+            hipLaunchKernelGGL(k_tree_compact, dim3(blocks), dim3(256), 0, st, T.G, T.offs, L, Ln,
+                               (int)T.plan[level + 1]);
+        }
+    }
+    if (ev) (void)hipEventRecord(ev[1], st);
+    for (int lv = D - 1; lv >= 0; --lv) {
+        const TreeLevel& L = T.levels[lv].L;
+        const TreeLevel& Lc = lv + 1 < D ? T.levels[lv + 1].L : L;
+        const int blocks = (int)((T.plan[lv] + 255) / 256);
+        hipLaunchKernelGGL(k_tree_resolve, dim3(blocks), dim3(256), 0, st, S, C, P, s, (int)first, (int)last, L,
+                           Lc, lv, ns, hdr, l, accum);
+    }
+    if (ev) (void)hipEventRecord(ev[2], st);
+    return hipGetLastError();
+}
+
+// RTG_TREE_SYNC=1: every pass host-driven (one synchronisation per level; A/B)
+static bool tree_sync_only() { return std::getenv("RTG_TREE_SYNC") != nullptr; }
+
 template <bool STATS, int FEAT>
 static hipError_t tree_run(TreeState& T, const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr,
                            unsigned char* l, float4* accum, DevCounters* cnt, hipStream_t st, hipEvent_t* ev) {
+    hipError_t e;
     if (!T.h_total) {
-        hipError_t e = hipHostMalloc(&T.h_total, sizeof(int));
-        if (e != hipSuccess) return e;
+        if ((e = hipHostMalloc(&T.h_total, 2 * sizeof(int))) != hipSuccess) return e;
+        if ((e = hipMalloc(&T.d_counts, (kMaxLevels + 1) * sizeof(int))) != hipSuccess) return e;
     }
-    for (int s = P.sample_begin; s < P.sample_begin + P.sample_count; ++s) {
-        const bool first = s == P.sample_begin, last = s == P.sample_begin + P.sample_count - 1;
-        hipError_t e = tree_pass<STATS, FEAT>(T, S, C, P, s, first, last, hdr, l, accum, cnt, st, last ? ev : nullptr);
-        if (e != hipSuccess) return e;
+    const int ns = S.num_point + S.num_area + S.num_env + S.num_dir + S.num_spot + S.num_mesh;
+    const std::vector<long long> key = {P.row_begin, P.row_end, P.part_index, P.part_count, C.width, C.height,
+                                        (long long)(size_t)S.objects, S.max_depth};
+    auto prepare = [&]() -> hipError_t {
+        // capacities and block segments of the plan; the overflow flag cleared
+        hipError_t r;
+        for (size_t lv = 0; lv < T.plan.size(); ++lv) {
+            if (T.levels.size() <= lv) T.levels.emplace_back();
+            if ((r = ensure_level(T.levels[lv], T.plan[lv], ns)) != hipSuccess) return r;
+        }
+        if ((r = ensure_segs(T, (*std::max_element(T.plan.begin(), T.plan.end()) + 255) / 256, ns)) != hipSuccess)
+            return r;
+        return hipMemsetAsync(T.d_counts + kMaxLevels, 0, sizeof(int), st);
+    };
+    auto make_plan = [&](const std::vector<size_t>& seen) {
+        // the level sizes seen, with a margin for sampled (stochastic) trees
+        // (RTG_TREE_PLAN_TIGHT=1, tests: one ray short of the sizes seen, so every planned
+        // render overflows and is redone host-driven)
+        const bool tight = std::getenv("RTG_TREE_PLAN_TIGHT") != nullptr;
+        T.plan.clear();
+        for (size_t k = 0; k < seen.size(); ++k)
+            T.plan.push_back(k == 0 ? seen[k] : tight ? (seen[k] > 1 ? seen[k] - 1 : seen[k]) : seen[k] + seen[k] / 4 + 1024);
+        T.plan_key = key;
+    };
+    for (int attempt = 0; attempt < 2; ++attempt) {
+        // attempt 0: planned passes when this frame part has a plan, else the first pass
+        // host-driven and the rest planned from it; attempt 1 (a level outgrew the plan):
+        // every pass host-driven, re-planning
+        const bool adapt = attempt == 0 && !tree_sync_only();
+        bool planned = adapt && T.plan_key == key && !T.plan.empty();
+        bool any_async = false;
+        if (planned && (e = prepare()) != hipSuccess) return e;
+        std::vector<size_t> seen;
+        for (int s = P.sample_begin; s < P.sample_begin + P.sample_count; ++s) {
+            const bool first = s == P.sample_begin, last = s == P.sample_begin + P.sample_count - 1;
+            hipEvent_t* pev = last ? ev : nullptr;
+            if (planned) {
+                e = tree_pass_async<STATS, FEAT>(T, S, C, P, s, first, last, hdr, l, accum, cnt, st, pev);
+                any_async = true;
+            } else {
+                std::vector<size_t> sizes;
+                e = tree_pass_sync<STATS, FEAT>(T, S, C, P, s, first, last, hdr, l, accum, cnt, st, pev, sizes);
+                if (sizes.size() > seen.size()) seen.resize(sizes.size(), 0);
+                for (size_t k = 0; k < sizes.size(); ++k) seen[k] = std::max(seen[k], sizes[k]);
+                if (e == hipSuccess && adapt) {
+                    make_plan(seen);
+                    planned = true;
+                    e = prepare();
+                }
+            }
+            if (e != hipSuccess) return e;
+        }
+        if (!any_async) {
+            if (!seen.empty()) make_plan(seen);
+            return hipSuccess;
+        }
+        // one synchronisation per render: did a level outgrow the plan?
+        if ((e = hipMemcpyAsync(T.h_total + 1, T.d_counts + kMaxLevels, sizeof(int), hipMemcpyDeviceToHost, st)) !=
+            hipSuccess)
+            return e;
+        if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
+        if (T.h_total[1] == 0) return hipSuccess;
+        T.plan.clear();
     }
     return hipSuccess;
 }
