@@ -116,6 +116,8 @@ struct rtg_scene {
     bool wave_ok = false;             // scene renders on the wavefront pipeline
     bool tree_ok = false;             // scene may render on the wavefront ray-tree pipeline
     rtg::TreeState* tree = nullptr;   // its buffers
+    bool path_ok = false;             // path-tracing cameras may render on the wavefront path tracer
+    rtg::PathState* path = nullptr;   // its buffers
     int feat = rtg::FEAT_ALL;         // scene feature bits (traversal specialisation)
     int num_slots = 0;                // lights per pixel (wavefront light slots)
     int shade_sk = rtg::SK_ALL;       // shading features (k_shade variant, rtg_common.hpp SK_*)
@@ -149,6 +151,7 @@ struct rtg_scene {
                 std::fprintf(stderr, "rtgpu guard: index violations, bits 0x%x\n", bits);
         }
         if (tree) rtg::tree_destroy(tree);
+        if (path) rtg::path_destroy(path);
         if (done) (void)hipEventDestroy(done);
         if (stream) (void)hipStreamDestroy(stream);
         for (auto& e : ev)
@@ -708,6 +711,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     if (std::getenv("RTG_NO_COOP")) sc->feat &= ~rtg::FEAT_BIGLEAF;
     sc->tree_ok = !blur && d->max_recursion_depth > 0 && branching;
     sc->wave_ok = !blur && (d->max_recursion_depth <= 0 || !branching);
+    sc->path_ok = !blur;
     sc->num_slots = d->num_point_lights + d->num_area_lights + d->num_env_lights + d->num_dir_lights +
                     d->num_spot_lights + d->num_mesh_lights;
     // shading features: textures / maps (incl. a background texture), BRDFs, env / spot / mesh
@@ -1091,7 +1095,25 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
     // ray trees: the wavefront tree pipeline for large frames (it synchronises once per tree
     // level), the fused kernel otherwise; RTG_RENDER_TREE / RTG_RENDER_FUSED force either
     const long long work = (long long)P.part_rows * C.width * P.sample_count;
-    // path tracing runs in the fused kernel only (its GI chains live on the per-thread stack)
+    // path tracing: the fused kernel; the wavefront path tracer (rtg_path.hip, same image bit
+    // for bit) with RTG_RENDER_TREE -- measured slower than the fused kernel on the path-tracing
+    // fixtures, so it is opt-in
+    if (C.path_tracing && s->path_ok && !(o->flags & RTG_RENDER_FUSED) && (o->flags & RTG_RENDER_TREE)) {
+        float4* acc = (float4*)d_accum;
+        if (!P.accum_only && C.spp > 1) {   // internal accumulator indexed by absolute pixel
+            int rc = ensure_wave(s, (size_t)C.width * C.height, s->num_slots, (size_t)P.num_tiles);
+            if (rc) return rc;
+            acc = s->wave.accum;
+        }
+        const hipError_t pe = rtg::launch_path(s->path, ds, C, P, d_hdr, d_ldr, acc, s->counters.p, stats, s->feat,
+                                               s->shade_sk, stream, ev);
+        if (pe == hipSuccess) {
+            if (ev) s->timed_layout = rtg::LAYOUT_PATH;
+            return RTG_OK;
+        }
+        if (pe != hipErrorNotSupported) HIP_TRY(pe);
+        (void)hipGetLastError();
+    }
     const bool fused_only = (o->flags & RTG_RENDER_FUSED) || C.path_tracing;
     const bool use_tree = s->tree_ok && !fused_only &&
                           ((o->flags & RTG_RENDER_TREE) || work >= (1ll << 21));
@@ -1385,12 +1407,13 @@ int rtg_scene_reset_stats(rtg_scene* s) {
 
 int rtg_scene_timings(rtg_scene* s, float* ms, const char** names, int32_t cap, int32_t* count) {
     // stage names per layout (rtg_kernels.hpp LAYOUT_*)
-    static const char* kNames[5][rtg::MAX_STAGES] = {{"k_primary", "k_shade", "k_shadow", "k_resolve"},
+    static const char* kNames[6][rtg::MAX_STAGES] = {{"k_primary", "k_shade", "k_shadow", "k_resolve"},
                                                      {"k_primary", "k_shade", "k_shadow"},
                                                      {"k_primary", "k_shade_shadow"},
                                                      {"tree_levels", "tree_resolve"},
-                                                     {"k_render"}};
-    static const int kCount[5] = {rtg::WAVE_STAGES, 3, 2, rtg::TREE_STAGES, rtg::MEGA_STAGES};
+                                                     {"k_render"},
+                                                     {"path_iterations"}};
+    static const int kCount[6] = {rtg::WAVE_STAGES, 3, 2, rtg::TREE_STAGES, rtg::MEGA_STAGES, rtg::PATH_STAGES};
     if (!s || !count) return set_err(RTG_ERR_INVALID, "null argument");
     if (s->timed_layout < 0) return set_err(RTG_ERR_INVALID, "no render was issued with RTG_RENDER_TIMING");
     HIP_TRY(hipSetDevice(s->device));

@@ -1631,6 +1631,8 @@ struct LightSample {
     Ray sr;
     float minT, limit;
 };
+// SK without SK_XLIGHT: the scene has no env / spot / mesh lights (their code is left out).
+template <int SK = SK_ALL>
 DEV LightSample light_sample(const DevScene& S, int slot, f3 p, f3 n, uint64_t key, int skipId = -1) {
     LightSample ls;
     ls.shadow = true;
@@ -1639,6 +1641,7 @@ DEV LightSample light_sample(const DevScene& S, int slot, f3 p, f3 n, uint64_t k
     f3 lpos = mk(0, 0, 0);
     bool positional = true;
     int i = slot;
+    constexpr bool XL = (SK & SK_XLIGHT) != 0;
     if (i < S.num_point) {
         const f3 lp = ld3(S.point_lights[i].pos);
         lpos = lp;
@@ -1659,12 +1662,13 @@ DEV LightSample light_sample(const DevScene& S, int slot, f3 p, f3 n, uint64_t k
         if (lc < 0) lc = dot(ld3(L.normal), w_i);
         ls.w_i = w_i;
         ls.E = muls(ld3(L.radiance), L.area * lc / dSqr);
-    } else if ((i -= S.num_area) < S.num_env) {                           // no shadow ray (:741-755)
+    } else if (XL && (i -= S.num_area) < S.num_env) {                     // no shadow ray (:741-755)
         f3 sd = env_direction(n, key, i);
         ls.E = env_sample(S, i, sd);
         ls.w_i = n;
         ls.shadow = false;
-    } else if ((i -= S.num_env) < S.num_dir) {
+    } else if (!XL || (i -= S.num_env) < S.num_dir) {
+        if (!XL) i -= S.num_area;
         const f3 ldir = ld3(S.dir_lights[i].dir);
         ls.w_i = neg(ldir);
         ls.E = ld3(S.dir_lights[i].radiance);
@@ -1720,21 +1724,22 @@ DEV LightSample light_sample(const DevScene& S, int slot, f3 p, f3 n, uint64_t k
 // traversal are inlined once).
 // TP / skipId: path tracing -- throughput update per Shade, and the mesh light the node's
 // GI ray hit is not sampled (raytracer.cpp:92,784).
-template <bool STATS, bool TP = false>
+// SK / FEAT: shading and traversal features the scene may use (the path tracer's variants).
+template <bool STATS, bool TP = false, int SK = SK_ALL, int FEAT = FEAT_ALL>
 DEV f3 direct(const DevScene& S, const ShadeCtx& c, f3 w_o, float mbTime, uint64_t key, Cnt<STATS>& cn,
               int skipId = -1, f3* tp = nullptr) {
     f3 color = mk(0, 0, 0);
     const f3 p = c.s.p, n = c.s.n;
     const int nslots = S.num_point + S.num_area + S.num_env + S.num_dir + S.num_spot + S.num_mesh;
     for (int l = 0; l < nslots; ++l) {
-        LightSample ls = light_sample(S, l, p, n, key, skipId);
+        LightSample ls = light_sample<SK>(S, l, p, n, key, skipId);
         if (ls.skip) continue;
         if (ls.shadow) {
             Hit h;
             cn.shd();
-            if (trace<true, STATS>(S, ls.sr, mbTime, ls.minT, ls.limit, h, cn)) continue;
+            if (trace<true, STATS, FEAT>(S, ls.sr, mbTime, ls.minT, ls.limit, h, cn)) continue;
         }
-        color = add(color, shade<TP>(S, c, ls.w_i, w_o, ls.E, tp));
+        color = add(color, shade<TP, SK>(S, c, ls.w_i, w_o, ls.E, tp));
     }
     return color;
 }

@@ -23,6 +23,14 @@ void tree_destroy(TreeState* tree);
 hipError_t launch_tree(TreeState*& tree, const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr,
                        unsigned char* ldr, float4* accum, DevCounters* counters, bool stats, int feat,
                        hipStream_t stream, hipEvent_t* ev);
+// wavefront path tracing (rtg_path.hip): path-tracing cameras without motion blur; path
+// queues and frame stacks kept in `path`.  hipErrorNotSupported: a pass needed more than
+// its iteration bound (the caller renders with the fused kernel instead)
+struct PathState;
+void path_destroy(PathState* path);
+hipError_t launch_path(PathState*& path, const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr,
+                       unsigned char* ldr, float4* accum, DevCounters* counters, bool stats, int feat, int sk,
+                       hipStream_t stream, hipEvent_t* ev);
 // photographic tonemapper (rtg_tonemap.hip); scratch of tonemap_scratch_bytes()
 size_t tonemap_scratch_bytes(long long pixels);
 size_t tonemap_avg_offset();   // byte offset of the log-average luminance (double) in the scratch
@@ -37,11 +45,12 @@ hipError_t build_mesh_bvh(const rtg_face* d_faces, int n, const float root_mn[3]
                           int faceOff, int nodeBase, float4* d_nodes, int2* d_ext, float4* d_tris, float4* d_fn,
                           float2* d_fuv, float4* d_v12, int* d_perm, int* nodeCount, bool* bigleaf,
                           hipStream_t st);
-enum { WAVE_STAGES = 4, MEGA_STAGES = 1, TREE_STAGES = 2, MAX_STAGES = 4 };
+enum { WAVE_STAGES = 4, MEGA_STAGES = 1, TREE_STAGES = 2, PATH_STAGES = 1, MAX_STAGES = 4 };
 // Timed stage layouts (RTG_RENDER_TIMING): which kernels ran between the recorded events.
 enum { LAYOUT_WAVE = 0,          // k_primary, k_shade, k_shadow, k_resolve
        LAYOUT_WAVE_ONE = 1,      // k_primary, k_shade, k_shadow (k_shadow_one finishes pixels)
        LAYOUT_WAVE_FUSED = 2,    // k_primary, k_shade_shadow
-       LAYOUT_TREE = 3, LAYOUT_MEGA = 4 };
+       LAYOUT_TREE = 3, LAYOUT_MEGA = 4,
+       LAYOUT_PATH = 5 };          // the last sample pass of the wavefront path tracer
 
 }  // namespace rtg

@@ -300,8 +300,11 @@ enum rtg_render_flags {
                                      render (last sample pass); see rtg_scene_timings */
     RTG_RENDER_TREE = 16,         /* force the wavefront ray-tree pipeline for scenes with
                                      mirror / conductor / dielectric materials (default:
-                                     frames of >= 2^21 pixel-samples; it synchronises the
-                                     stream once per tree level)                       */
+                                     frames of >= 2^21 pixel-samples; one stream
+                                     synchronisation per render once its level sizes are
+                                     planned).  ABI 5: for path-tracing cameras, the
+                                     wavefront path tracer (opt-in; same image as the
+                                     fused kernel bit for bit)                         */
     RTG_RENDER_EXACT_SHADOW = 32, /* shadow rays walk the reference BVH instead of the
                                      any-hit wide BVH (same answers; for cross-checks)  */
     RTG_RENDER_ORDERED = 64       /* opt-in (ABI 4): camera rays of plain mesh scenes walk

@@ -110,3 +110,61 @@ def test_path_tracing_deterministic_across_row_bands(tmp_path):
         band, _ = ds.render(0, rows=(t * 8, t * 8 + 8), seed=17)
         out[t * 8:t * 8 + 8] = band[t * 8:t * 8 + 8]
     assert np.array_equal(out.view(np.uint32), full.view(np.uint32))
+
+
+PT_ONLY = ["pt_cornell", "pt_nee", "pt_rr", "pt_meshlight"]
+
+
+def _bits(a):
+    return a.view(np.uint32)
+
+
+@pytest.mark.parametrize("name", PT_ONLY)
+@pytest.mark.parametrize("spp", [1, 4])
+def test_path_wavefront_equals_fused(name, spp, tmp_path):
+    """The wavefront path tracer (rtg_path.hip, forced with RTG_RENDER_TREE) gives the fused
+    kernel's image bit for bit: the same node steps (rtg_node.hpp) on the same RNG keys.  The
+    first render plans its later passes from its first; the second runs planned throughout."""
+    hs = _scene(tmp_path, name, spp)
+    ds = rtgpu.DeviceScene(hs, 0)
+    b, lb = ds.render(0, seed=11, flags=rtgpu.RTG_RENDER_FUSED)
+    for _ in range(2):
+        a, la = ds.render(0, seed=11, flags=rtgpu.RTG_RENDER_TREE)
+        assert np.array_equal(_bits(a), _bits(b)), ob.compare(a, b)
+        assert np.array_equal(la, lb)
+    ds.render(0, seed=11, flags=rtgpu.RTG_RENDER_TREE | rtgpu.RTG_RENDER_TIMING)
+    assert "path_iterations" in ds.timings()
+
+
+@pytest.mark.parametrize("env", ["RTG_PATH_SYNC", "RTG_PATH_PLAN_TIGHT"])
+def test_path_wavefront_host_driven_and_overflow(env, tmp_path, monkeypatch):
+    """Every pass host-driven (RTG_PATH_SYNC), and plans one iteration short
+    (RTG_PATH_PLAN_TIGHT: every planned pass leaves paths, the render is redone host-driven):
+    the same image as the fused kernel."""
+    monkeypatch.setenv(env, "1")
+    hs = _scene(tmp_path, "pt_nee", 4)
+    ds = rtgpu.DeviceScene(hs, 0)
+    b, _ = ds.render(0, seed=5, flags=rtgpu.RTG_RENDER_FUSED)
+    for _ in range(2):
+        a, _ = ds.render(0, seed=5, flags=rtgpu.RTG_RENDER_TREE)
+        assert np.array_equal(_bits(a), _bits(b)), ob.compare(a, b)
+
+
+def test_path_wavefront_stats_and_bands(tmp_path):
+    """Ray counts of the wavefront path tracer equal the fused kernel's; row bands rendered
+    separately give the whole frame (part_pixel mapping of the path queues)."""
+    hs = _scene(tmp_path, "pt_cornell", 2)
+    ds = rtgpu.DeviceScene(hs, 0)
+    ds.reset_stats()
+    ds.render(0, seed=17, flags=rtgpu.RTG_RENDER_FUSED | rtgpu.RTG_RENDER_COUNT_STATS)
+    sf = ds.stats()
+    ds.reset_stats()
+    full, _ = ds.render(0, seed=17, flags=rtgpu.RTG_RENDER_TREE | rtgpu.RTG_RENDER_COUNT_STATS)
+    sw = ds.stats()
+    for k in ("camera_rays", "secondary_rays", "shadow_rays"):
+        assert sw[k] == sf[k], (k, sw[k], sf[k])
+    out = np.zeros_like(full)
+    for t in range(4):
+        band, _ = ds.render(0, rows=(t * 16, t * 16 + 16), seed=17, flags=rtgpu.RTG_RENDER_TREE)
+        out[t * 16:t * 16 + 16] = band[t * 16:t * 16 + 16]
+    assert np.array_equal(_bits(out), _bits(full))
