@@ -933,6 +933,14 @@ void rtg_scene_destroy(rtg_scene* s) {
     delete s;
 }
 
+// Band k of part `part` of `parts` (rtgpu.h RTG_PART_BAND_ROWS; part_row in rtg_common.hpp):
+// round-robin, rotated by one slot per round of `parts` bands.  Increasing in k.
+static int part_band(int part, int parts, int k) {
+    int slot = (part - k) % parts;
+    if (slot < 0) slot += parts;
+    return k * parts + slot;
+}
+
 int rtg_part_runs(int32_t row_begin, int32_t row_end, int32_t part, int32_t parts, int32_t* runs, int32_t cap,
                   int32_t* count) {
     if (!count) return set_err(RTG_ERR_INVALID, "null argument");
@@ -940,7 +948,8 @@ int rtg_part_runs(int32_t row_begin, int32_t row_end, int32_t part, int32_t part
     if (part < 0 || part >= parts || row_begin < 0 || row_end < row_begin)
         return set_err(RTG_ERR_INVALID, "bad partition (part %d of %d, rows [%d, %d))", part, parts, row_begin, row_end);
     int n = 0, r0 = -1, r1 = -1;
-    for (int b = part; row_begin + b * RTG_PART_BAND_ROWS < row_end; b += parts) {
+    for (int k = 0, b = part_band(part, parts, 0); row_begin + b * RTG_PART_BAND_ROWS < row_end;
+         b = part_band(part, parts, ++k)) {
         const int a = row_begin + b * RTG_PART_BAND_ROWS, e = std::min(a + RTG_PART_BAND_ROWS, (int)row_end);
         if (a == r1) { r1 = e; continue; }
         if (r0 >= 0) { if (runs && n < cap) { runs[2 * n] = r0; runs[2 * n + 1] = r1; } ++n; }
@@ -1031,17 +1040,20 @@ static int prepare(rtg_scene* s, const rtg_render_opts* o, rtg::DevCamera& C, rt
     P.part_index = o->part_index;
     if (P.part_index < 0 || P.part_index >= P.part_count)
         return set_err(RTG_ERR_INVALID, "part %d of %d", P.part_index, P.part_count);
-    // this part's bands of RTG_PART_BAND_ROWS (= the tile height) rows and its row count
+    // this part's bands of RTG_PART_BAND_ROWS rows (part_row in rtg_common.hpp) and its row
+    // count; tiles of 16 compact rows (two bands; a wave's 8 rows are one band)
+    static_assert(RTG_PART_BAND_ROWS == 8, "part_row's band shift");
     const int bands = (P.row_end - P.row_begin + RTG_PART_BAND_ROWS - 1) / RTG_PART_BAND_ROWS;
-    const int own = bands > P.part_index ? (bands - P.part_index + P.part_count - 1) / P.part_count : 0;
+    int own = 0;
+    while (part_band(P.part_index, P.part_count, own) < bands) ++own;
     P.part_rows = 0;
     if (own > 0) {
-        const int lastBand = P.part_index + (own - 1) * P.part_count;
+        const int lastBand = part_band(P.part_index, P.part_count, own - 1);
         P.part_rows = (own - 1) * RTG_PART_BAND_ROWS +
                       std::min(RTG_PART_BAND_ROWS, P.row_end - P.row_begin - lastBand * RTG_PART_BAND_ROWS);
     }
     P.tiles_x = (c.width + 15) / 16;
-    P.tiles_y = own;
+    P.tiles_y = (P.part_rows + 15) / 16;
     P.num_tiles = P.tiles_x * P.tiles_y;
     if (P.num_tiles == 0) return RTG_OK;   // nothing of this part in the row range
     P.seed = o->seed;

@@ -1831,10 +1831,15 @@ DEV unsigned char ldr(float c) {
 
 // 16x16-pixel tile per 256-thread block, 8x8 per wave; tiles dealt so that consecutive
 // tiles share an XCD (blocks b and b+8 share one under round-robin dispatch).
-// Image row of compact row `crow` of this render's part (RenderParams): band crow/16 of
-// the part is band (crow/16) * part_count + part_index of the row range.
+// Image row of compact row `crow` of this render's part (RenderParams): compact rows are
+// the part's 8-row bands in order.
+// Band kb of part p of N is band kb * N + ((p - kb) mod N) of the row range (rtgpu.h
+// RTG_PART_BAND_ROWS: round-robin, rotated by one slot per round).
 DEV int part_row(const RenderParams& P, int crow) {
-    return P.row_begin + (((crow >> 4) * P.part_count + P.part_index) << 4) + (crow & 15);
+    const int kb = crow >> 3;
+    int slot = (P.part_index - kb) % P.part_count;
+    if (slot < 0) slot += P.part_count;
+    return P.row_begin + ((kb * P.part_count + slot) << 3) + (crow & 7);
 }
 // Image pixel of compact pixel index i (= crow * width + x).
 DEV int part_pixel(const RenderParams& P, int width, int i) {

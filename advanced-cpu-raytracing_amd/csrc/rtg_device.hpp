@@ -197,7 +197,7 @@ struct RenderParams {
     int row_begin, row_end;
     int sample_begin, sample_count;
     int accum_only;
-    int tiles_x, tiles_y, num_tiles;    // tiles_y: this part's bands
+    int tiles_x, tiles_y, num_tiles;    // tiles of 16 x 16 compact pixels (16 compact rows = 2 bands)
     int part_index, part_count, part_rows;
     unsigned long long seed;
     const int* __restrict__ tile_map;   // block -> 16x16 tile of this part (host-built, XCD-aware)

@@ -2,8 +2,10 @@
 
 The reference's only parallelism is row bands over std::threads (src/main.cpp:38-39,
 164-185: thread t renders rows [t*H/8, (t+1)*H/8)).  Here the frame is dealt to GPUs in
-16-row bands (RTG_PART_BAND_ROWS, the tile height of every kernel): band b belongs to part
-b % N.  Interleaving the bands balances the image's cost gradient over the parts (a
+8-row bands (RTG_PART_BAND_ROWS, the rows of one wave's 8x8 pixel block), dealt round-robin
+with the order rotated by one slot per round: the k-th band of part p is band
+k * N + ((p - k) mod N).  Interleaving the bands balances the image's cost gradient over the
+parts, and the rotation its gradient within a round of N bands (a
 contiguous band per GPU would not -- the CPU shows 1->8 threads giving only 2.5x on
 ton_Roosendaal), and every band is a contiguous run of the row-major
 framebuffer (layout 3*(x + y*W), main.cpp:109), so the gather is one DMA per run straight
@@ -32,7 +34,7 @@ import os
 
 import numpy as np
 
-BAND_ROWS = 16   # RTG_PART_BAND_ROWS (include/rtgpu.h)
+BAND_ROWS = 8    # RTG_PART_BAND_ROWS (include/rtgpu.h)
 
 
 def part_runs(row_begin: int, row_end: int, part: int, parts: int):
@@ -50,16 +52,19 @@ def part_runs(row_begin: int, row_end: int, part: int, parts: int):
 def part_runs_py(row_begin: int, row_end: int, part: int, parts: int):
     """Pure-Python statement of the same partition (cross-check of rtg_part_runs)."""
     runs = []
-    b = part
-    while row_begin + b * BAND_ROWS < row_end:
+    parts = max(parts, 1)
+    k = 0
+    while True:
+        b = k * parts + (part - k) % parts       # round-robin, rotated one slot per round
         a = row_begin + b * BAND_ROWS
+        if a >= row_end:
+            return runs
         e = min(a + BAND_ROWS, row_end)
         if runs and runs[-1][1] == a:
             runs[-1] = (runs[-1][0], e)
         else:
             runs.append((a, e))
-        b += max(parts, 1)
-    return runs
+        k += 1
 
 
 def sample_range(rank: int, world: int, spp: int):

@@ -9,7 +9,7 @@ host beside it.
 
 A step = one full 1920x1080 frame (one sample pass) traced and shaded, inputs (scene, BVH)
 resident in HBM.  With N ranks every frame is partitioned (multigpu.py): rank r renders the
-16-row bands b with b % N == r into its own HBM -- no collective on the data path (the
+8-row bands dealt round-robin (rotated one slot per round) into its own HBM -- no collective on the data path (the
 barriers around the timed region and the max-over-ranks of the elapsed time are the only
 collectives).  The steps rotate over 8 scene replicas, each on its own stream ("frames in
 flight"), so a frame's kernels overlap the next frames' -- a part of 1/N of one frame alone
@@ -33,10 +33,15 @@ import time
 # Frames in flight: every step renders one frame, and the steps rotate over FRAMES_IN_FLIGHT
 # scene replicas, each on its own stream, so one frame's kernels overlap the next frames' (a
 # part of 1/N of a frame is too small a grid to fill the GPU on its own: DESIGN.md §6).  Each
-# stream needs its own hardware queue (HIP's default is 4 per process); set before the HIP
-# runtime starts.
+# stream needs its own hardware queue (HIP's default is 4 per process, and streams beyond the
+# queues share them and serialise: part (0, 8) 0.14 ms with 4 queues, 0.070 with 9;
+# profiles/r03o_parts_queues.txt); raised to 9 -- the replicas' 8 streams + torch's own; 9
+# measured faster than 12 or 16 -- before the HIP runtime starts.
+HW_QUEUES = int(os.environ.get("RTG_BENCH_HW_QUEUES", "9"))
 if "--help" not in sys.argv and "-h" not in sys.argv:
-    os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+    # (RTG_BENCH_QUEUES_AS_GIVEN=1: keep the environment's value, for the A/B)
+    if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < HW_QUEUES and not os.environ.get("RTG_BENCH_QUEUES_AS_GIVEN"):
+        os.environ["GPU_MAX_HW_QUEUES"] = str(HW_QUEUES)
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "advanced-cpu-raytracing_amd")
@@ -51,7 +56,7 @@ SWEEP_K = (1000, 10082, 100352, 1002528)
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=20)
+    p.add_argument("--steps", type=int, default=100)
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--K", type=int, default=100352, help="triangles in the synthetic height field")
     p.add_argument("--width", type=int, default=1920)
@@ -326,7 +331,7 @@ def roofline(kernel, algo_bytes, kernel_ms, pmc):
 
 
 def part_scaling(reps, torch, seed, steps, value, frame_s, counts=(2, 4, 8)):
-    """The N-GPU frame on one GPU: every part r of N (the 16-row bands b % N == r,
+    """The N-GPU frame on one GPU: every part r of N (its 8-row bands, multigpu.py part_runs,
     multigpu.py) rendered alone, with the same frames in flight as the headline steps
     (`reps`: the replicas the steps rotate over).  With one GPU per part the N-GPU node takes
     the slowest part's time per frame, so the predicted strong-scaling efficiency is
@@ -335,15 +340,16 @@ def part_scaling(reps, torch, seed, steps, value, frame_s, counts=(2, 4, 8)):
     out = {}
     F = len(reps)
     for n in counts:
-        ms = []
-        for r in range(n):
+        ms = [0.0] * n
+        order = range(n - 1, -1, -1) if os.environ.get("RTG_BENCH_PARTS_REVERSED") else range(n)
+        for r in order:
             def step(k, r=r, n=n):
                 ds_, h, l, sp = reps[k % F]
                 ds_.render_device(h.data_ptr(), l.data_ptr(), sp, seed=seed, part=(r, n))
             # warm-up: every replica renders this part once (its tile map for the part's rows is
             # built on first use)
             e, _ = measure(step, torch, steps, F, lambda: None, serial=lambda: None)
-            ms.append(e / steps * 1e3)
+            ms[r] = e / steps * 1e3
         worst = max(ms)
         out[str(n)] = {"part_ms": [round(x, 4) for x in ms], "max_part_ms": round(worst, 4),
                        "predicted_efficiency": round(frame_s * 1e3 / (n * worst), 4),
@@ -453,14 +459,14 @@ def main():
             ds.render_device(hdr.data_ptr(), ldr.data_ptr(), sptr, seed=seed, flags=flags, part=part)
 
         # frames in flight: replicas 1..F-1 of the scene, each with its own frame buffers and
-        # stream; step k renders frame k on replica k % F (replica 0 = ds on the current stream)
+        # stream; step k renders frame k on replica k % F (replica 0 = ds, on a stream of its
+        # own when F > 1 -- not torch's current stream, which the serial and counting passes use)
         F = args.inflight or (8 if args.config == "headline" else 1)
-        reps = [(ds, hdr, ldr, sptr)]
-        streams = []
-        for _ in range(F - 1):
-            s = torch.cuda.Stream()
-            streams.append(s)
-            reps.append((rtgpu.DeviceScene(hs, local), torch.empty_like(hdr), torch.empty_like(ldr), s.cuda_stream))
+        streams = [torch.cuda.Stream() for _ in range(F if F > 1 else 0)]
+        reps = [(ds, hdr, ldr, streams[0].cuda_stream if F > 1 else sptr)]
+        for k in range(1, F):
+            reps.append((rtgpu.DeviceScene(hs, local), torch.empty_like(hdr), torch.empty_like(ldr),
+                         streams[k].cuda_stream))
 
         def render_step(k):
             r, h, l, sp = reps[k % F]
@@ -522,8 +528,8 @@ def main():
                 "shadow_wide_node_visits_per_ray": round(st.get("shadow_wide_visits", 0) / max(st["shadow_rays"], 1), 2),
                 "shadow_fallback_rays": int(st.get("shadow_fallbacks", 0)),
                 "shadow_tri_tests_per_ray": round(st["shadow_tri_tests"] / max(st["shadow_rays"], 1), 2),
-                "parallelism": f"image partition x{world}: 16-row bands dealt round-robin, rank r renders bands "
-                               f"b % {world} == r (one frame per step)",
+                "parallelism": f"image partition x{world}: 8-row bands dealt round-robin rotated one slot per round, rank r "
+                               f"renders band k*{world} + ((r - k) mod {world}) (one frame per step)",
                 "frames_in_flight": F,
                 "serial": {"ms_per_step": round(s_el / args.steps * 1e3, 4),
                            "mrays_s": round(rays * args.steps / s_el / 1e6, 2),
@@ -573,7 +579,10 @@ def main():
                 if ph:
                     ph.close()
             if world == 1:
-                result["parts"] = part_scaling(reps, torch, seed, args.steps, value, elapsed / args.steps)
+                # at least 20 frames per replica per part: the steady state of F frames in flight
+                # (a short run is dominated by filling and draining the streams)
+                result["parts"] = part_scaling(reps, torch, seed, max(args.steps, 20 * F), value,
+                                               elapsed / args.steps)
             if world == 1:
                 # opt-in ordered closest hit (RTG_RENDER_ORDERED): same frame, its agreement with
                 # the reference-order walk measured here (pixels whose float bits differ)

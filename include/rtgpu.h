@@ -323,8 +323,10 @@ typedef struct {
     int32_t flags;                /* rtg_render_flags */
     uint64_t seed;                /* counter-based RNG key (stochastic features) */
     /* Image partition (ABI 3).  The rows [row_begin, row_end) are cut into bands of
-     * RTG_PART_BAND_ROWS rows; band b (counted from row_begin) belongs to part
-     * b % part_count.  A render with part_count > 1 computes and writes only the pixels
+     * RTG_PART_BAND_ROWS rows (counted from row_begin), dealt round-robin with the order
+     * rotated by one slot per round (ABI 5): the k-th band of part p of N is band
+     * k * N + ((p - k) mod N) -- so every part samples every position within a round of N
+     * bands, and a cost peak a few bands tall (a horizon) is shared out.  A render with part_count > 1 computes and writes only the pixels
      * of part part_index; the union of parts 0..part_count-1 is bit-identical to the
      * whole render (pixels are independent, the RNG is keyed by pixel).  Exception: for
      * a camera with a <Tonemap>, a part's LDR rows hold clamp((int)c), not the tonemapped
@@ -336,7 +338,9 @@ typedef struct {
     int32_t part_index, part_count;
 } rtg_render_opts;
 
-#define RTG_PART_BAND_ROWS 16
+/* ABI 5: 8-row bands (16 in ABI 3-4): 1080 rows over 8 parts give 17 or 16 bands per part
+ * (a 0.7 % imbalance) instead of 9 or 8 (6.6 %) */
+#define RTG_PART_BAND_ROWS 8
 
 /* The rows of part `part_index` of `part_count` within [row_begin, row_end), as maximal
  * runs of consecutive rows: runs[2k] = first row, runs[2k+1] = one past the last.  Writes

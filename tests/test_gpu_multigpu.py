@@ -1,6 +1,6 @@
 """Image partition across GPUs (multigpu.py), on the product path.
 
-The frame is dealt in 16-row bands (band b -> part b % N).  Every way of running the
+The frame is dealt in 8-row bands (the k-th band of part p is band k*N + (p - k) mod N).  Every way of running the
 partition must give the single-GPU image bit for bit:
 
 * part renders (rtg_render with part_index / part_count) composed into one frame;
