@@ -1136,7 +1136,8 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
             if (rc) return rc;
             acc = s->wave.accum;
         }
-        HIP_TRY(rtg::launch_tree(s->tree, ds, C, P, d_hdr, d_ldr, acc, s->counters.p, stats, s->feat, stream, ev));
+        HIP_TRY(rtg::launch_tree(s->tree, ds, C, P, d_hdr, d_ldr, acc, s->counters.p, stats, s->feat, s->shade_sk,
+                                 stream, ev));
         if (ev) s->timed_layout = rtg::LAYOUT_TREE;
         return RTG_OK;
     }

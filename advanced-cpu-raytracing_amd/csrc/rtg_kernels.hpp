@@ -21,7 +21,7 @@ hipError_t launch_wave(const DevScene& S, const DevCamera& C, const RenderParams
 struct TreeState;
 void tree_destroy(TreeState* tree);
 hipError_t launch_tree(TreeState*& tree, const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr,
-                       unsigned char* ldr, float4* accum, DevCounters* counters, bool stats, int feat,
+                       unsigned char* ldr, float4* accum, DevCounters* counters, bool stats, int feat, int sk,
                        hipStream_t stream, hipEvent_t* ev);
 // wavefront path tracing (rtg_path.hip): path-tracing cameras without motion blur; path
 // queues and frame stacks kept in `path`.  hipErrorNotSupported: a pass needed more than

@@ -85,8 +85,13 @@ DEV int seg_append(bool want, int* lds_count) {
     return want ? base + __popcll(mask & ((1ull << lane) - 1ull)) : -1;
 }
 
-template <bool STATS>
-__global__ __launch_bounds__(256, RTG_TREE_SHADE_WAVES) void k_tree_shade(const DevScene S, const DevCamera C, const TreeLevel L,
+// SK: shading features the scene may use (rtg_common.hpp SK_*): the general variant and one
+// without BRDFs and env / spot / mesh lights (C5: textures, point lights).
+#ifndef RTG_TREE_SHADE_WAVES_LEAN
+#define RTG_TREE_SHADE_WAVES_LEAN 2
+#endif
+template <bool STATS, int SK = SK_ALL>
+__global__ __launch_bounds__(256, SK == SK_ALL ? RTG_TREE_SHADE_WAVES : RTG_TREE_SHADE_WAVES_LEAN) void k_tree_shade(const DevScene S, const DevCamera C, const TreeLevel L,
                                                     const int level, const RenderParams P, const TreeSegs G,
                                                     DevCounters* counters) {
     __shared__ int nShadow, nChild;
@@ -119,11 +124,11 @@ __global__ __launch_bounds__(256, RTG_TREE_SHADE_WAVES) void k_tree_shade(const 
             f3 v;
             if (level == 0) {
                 const int pixel = part_pixel(P, C.width, i);
-                v = miss_color(S, C, pixel % C.width, pixel / C.width, r.d);
+                v = miss_color<SK>(S, C, pixel % C.width, pixel / C.width, r.d);
             } else {
                 const float4 m = L.miss[i];
                 v = __float_as_int(m.w) == TM_ENV
-                        ? (S.num_env > 0 ? env_sample(S, 0, mk(m.x, m.y, m.z)) : mk(0, 0, 0))
+                        ? (((SK & SK_XLIGHT) && S.num_env > 0) ? env_sample(S, 0, mk(m.x, m.y, m.z)) : mk(0, 0, 0))
                         : mk(0, 0, 0);
             }
             L.base[i] = make_float4(0, 0, 0, __int_as_float(TK_FINAL));
@@ -137,7 +142,7 @@ __global__ __launch_bounds__(256, RTG_TREE_SHADE_WAVES) void k_tree_shade(const 
             h.o = r.o;
             c.ob = &ob;
             c.mat = &S.materials[ob.material];
-            c.s = surface<STATS>(S, r, 0.f, h, cn);
+            c.s = surface<STATS, (SK & SK_TEX) != 0>(S, r, 0.f, h, cn);
             const f3 eye = level == 0 ? ld3(C.pos) : r.o;
             w_o = makeUnit(sub(eye, c.s.p));
             const DevMaterial& mat = *c.mat;
@@ -146,7 +151,7 @@ __global__ __launch_bounds__(256, RTG_TREE_SHADE_WAVES) void k_tree_shade(const 
                 const f3 e = muls(muls(ld3(mat.radiance), 2.0f), (float)RT_PI);
                 L.base[i] = make_float4(0, 0, 0, __int_as_float(TK_FINAL));
                 L.value[i] = make_float4(e.x, e.y, e.z, __int_as_float(1));
-            } else if (ob.tex_replace_all >= 0) {                       // replace_all (:87-89)
+            } else if ((SK & SK_TEX) && ob.tex_replace_all >= 0) {      // replace_all (:87-89)
                 const f3 e = tex_rgb(S, S.textures[ob.tex_replace_all], c.s.u, c.s.v);
                 L.base[i] = make_float4(0, 0, 0, __int_as_float(TK_FINAL));
                 L.value[i] = make_float4(e.x, e.y, e.z, __int_as_float(1));
@@ -269,8 +274,8 @@ __global__ __launch_bounds__(256, RTG_TREE_SHADE_WAVES) void k_tree_shade(const 
     for (int l = 0; l < ns; ++l) {
         LightSample ls;
         if (lit) {
-            ls = light_sample(S, l, c.s.p, c.s.n, key);
-            const f3 t = shade(S, c, ls.w_i, w_o, ls.E);
+            ls = light_sample<SK>(S, l, c.s.p, c.s.n, key);
+            const f3 t = shade<false, SK>(S, c, ls.w_i, w_o, ls.E);
             L.term[(size_t)i * ns + l] = make_float4(t.x, t.y, t.z, 0.f);
             L.occ[(size_t)i * ns + l] = 0;
         }
@@ -499,6 +504,7 @@ struct TreeState {
     int* d_counts = nullptr;    // kMaxLevels + 1 ints, [kMaxLevels] = overflow
     std::vector<size_t> plan;
     std::vector<long long> plan_key;
+    int sk = SK_ALL;            // the scene's shading features (k_tree_shade variant)
     ~TreeState() {
         auto f = [](void* p) { if (p) (void)hipFree(p); };
         for (auto& lv : levels) {
@@ -548,7 +554,10 @@ static void level_launches(TreeState& T, const DevScene& S, const DevCamera& C, 
                            hipStream_t st) {
     if (level == 0) hipLaunchKernelGGL(k_tree_gen, dim3(blocks), dim3(256), 0, st, C, P, s, L);
     hipLaunchKernelGGL((k_tree_trace<STATS, FEAT>), dim3(blocks), dim3(256), 0, st, S, L, level, cnt);
-    hipLaunchKernelGGL((k_tree_shade<STATS>), dim3(blocks), dim3(256), 0, st, S, C, L, level, P, T.G, cnt);
+    if ((T.sk & ~SK_TEX) == 0)
+        hipLaunchKernelGGL((k_tree_shade<STATS, SK_TEX>), dim3(blocks), dim3(256), 0, st, S, C, L, level, P, T.G, cnt);
+    else
+        hipLaunchKernelGGL((k_tree_shade<STATS, SK_ALL>), dim3(blocks), dim3(256), 0, st, S, C, L, level, P, T.G, cnt);
     if (ns > 0) {
         WaveBufs W{};
         W.q_o = T.G.q_o; W.q_d = T.G.q_d; W.q_slot = T.G.q_slot; W.q_count = T.G.q_count;
@@ -727,9 +736,10 @@ static hipError_t tree_run(TreeState& T, const DevScene& S, const DevCamera& C, 
 }
 
 hipError_t launch_tree(TreeState*& T, const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr,
-                       unsigned char* l, float4* accum, DevCounters* cnt, bool stats, int feat, hipStream_t st,
-                       hipEvent_t* ev) {
+                       unsigned char* l, float4* accum, DevCounters* cnt, bool stats, int feat, int sk,
+                       hipStream_t st, hipEvent_t* ev) {
     if (!T) T = new TreeState();
+    T->sk = sk;
     const bool big = (feat & FEAT_BIGLEAF) != 0;
     const int base = feat & ~FEAT_BIGLEAF;
 #define RTG_TREE(F)                                                                     \
