@@ -21,14 +21,16 @@ if [ $skip -eq 0 ]; then
   rc=$?; echo "smoke rc=$rc" >> $st
   if [ $rc -ne 0 ]; then exit $rc; fi
 fi
-timeout -k 10 300 python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-sweep $extra > $out/bench.log 2>&1
+timeout -k 10 600 python bench.py $extra > $out/bench.log 2>&1
 rc=$?; echo "bench rc=$rc" >> $st
 if [ $rc -ne 0 ]; then exit $rc; fi
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o run -- python bench.py --steps 20 --warmup 3 --no-cpu-baseline --no-sweep --no-extras $extra > $out/prof.log 2>&1
+# kernel trace of serial frames (--inflight 1): its per-kernel averages are the live event
+# timings' (with frames in flight, overlapping kernels stretch each other's durations)
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o run -- python bench.py --steps 20 --warmup 3 --inflight 1 --no-cpu-baseline --no-sweep --no-extras $extra > $out/prof.log 2>&1
 rc=$?; echo "prof rc=$rc" >> $st
 if [ $rc -ne 0 ]; then exit $rc; fi
 timeout -k 10 60 rocprofv3 -L > $out/counters.txt 2>&1
-args="--steps 3 --warmup 1 --no-cpu-baseline --no-sweep --no-extras $extra"
+args="--steps 3 --warmup 1 --inflight 1 --no-cpu-baseline --no-sweep --no-extras $extra"
 k=0
 for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM" \
             "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH" \
