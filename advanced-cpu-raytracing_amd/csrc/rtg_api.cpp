@@ -1163,7 +1163,7 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
         if (ev) s->timed_layout = layout;
         return RTG_OK;
     }
-    HIP_TRY(rtg::launch_mega(ds, C, P, d_hdr, d_ldr, d_accum, s->counters.p, stats, stream, ev));
+    HIP_TRY(rtg::launch_mega(ds, C, P, d_hdr, d_ldr, d_accum, s->counters.p, stats, s->shade_sk, s->feat, stream, ev));
     if (ev) s->timed_layout = rtg::LAYOUT_MEGA;
     return RTG_OK;
 }

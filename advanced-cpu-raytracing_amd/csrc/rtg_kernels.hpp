@@ -10,8 +10,14 @@ namespace rtg {
 int max_supported_depth();
 // fused kernel (rtg_mega.hip): any scene
 // `ev` (nullable): events recorded around every kernel of the last sample pass
+// sk / feat: the scene's shading / traversal features (path-tracing variants, rtg_mega_pt.hip)
 hipError_t launch_mega(const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr, unsigned char* ldr,
-                       float* accum, DevCounters* counters, bool stats, hipStream_t stream, hipEvent_t* ev);
+                       float* accum, DevCounters* counters, bool stats, int sk, int feat, hipStream_t stream,
+                       hipEvent_t* ev);
+hipError_t launch_mega_pt(const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr, unsigned char* ldr,
+                          float* accum, DevCounters* counters, int sk, int feat, hipStream_t stream);
+hipError_t launch_mega_wh(const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr, unsigned char* ldr,
+                          float* accum, DevCounters* counters, int sk, int feat, hipStream_t stream);
 // wavefront pipeline (rtg_wave.hip): scenes without secondary rays / motion blur
 hipError_t launch_wave(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W, float* hdr,
                        unsigned char* ldr, DevCounters* counters, bool stats, int feat, int sk, hipStream_t stream,

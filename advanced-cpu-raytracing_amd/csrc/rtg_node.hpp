@@ -269,13 +269,13 @@ DEV bool rest_call(const DevScene& S, const DevCamera& C, const RestArgs& a, f3&
 
 // shade_node_pre + its shade_rest: returns true and fills `f`/`ch` if the node spawns a child
 // ray (path tracing: its GI ray first); otherwise `out` is the node's final colour.
-template <int MAXD, bool STATS, bool PT>
+template <int MAXD, bool STATS, bool PT, int SK = SK_ALL, int FEAT = FEAT_ALL>
 DEV bool shade_node(const DevScene& S, const DevCamera& C, const Node& cur, int level, f3& out, FrameT<PT>& f, Child& ch,
                     Cnt<STATS>& cn) {
     RestArgs a;
-    const int r = shade_node_pre<STATS, PT>(S, C, cur, level, MAXD, out, f, ch, a, cn);
+    const int r = shade_node_pre<STATS, PT, SK>(S, C, cur, level, MAXD, out, f, ch, a, cn);
     if (r != NS_REST) return r == NS_SPAWN;
-    return rest_call<STATS, PT>(S, C, a, out, f, ch, cn);
+    return rest_call<STATS, PT, SK, FEAT>(S, C, a, out, f, ch, cn);
 }
 
 template <int SK = SK_ALL>
@@ -416,14 +416,14 @@ DEV void rest_done(bool spawned, const RestArgs& a, const FrameT<PT>& f, const C
 
 // resume_pre + its shade_rest: returns true if the frame spawns its next child (the pending
 // ray `p`; `f` stays on the stack), false if it is finished (`v` = its value).
-template <bool STATS, bool PT>
+template <bool STATS, bool PT, int SK = SK_ALL, int FEAT = FEAT_ALL>
 DEV bool resume_frame(const DevScene& S, const DevCamera& C, FrameT<PT>& f, ChildVal& v, Pending& p, Cnt<STATS>& cn) {
     RestArgs a;
-    const int r = resume_pre<STATS, PT>(S, C, f, v, p, a, cn);
+    const int r = resume_pre<STATS, PT, SK>(S, C, f, v, p, a, cn);
     if (r != NS_REST) return r == NS_SPAWN;
     Child ch;
     f3 out;
-    const bool spawned = rest_call<STATS, PT>(S, C, a, out, f, ch, cn);
+    const bool spawned = rest_call<STATS, PT, SK, FEAT>(S, C, a, out, f, ch, cn);
     rest_done<STATS, PT>(spawned, a, f, ch, out, p, v, cn);
     return spawned;
 }
