@@ -68,8 +68,8 @@ def parse():
     p.add_argument("--config", default="headline", choices=["headline", "c2", "c3", "c3ton", "c4", "c5"],
                    help="BASELINE.json configuration (c2-c5: one frame = all camera samples)")
     p.add_argument("--inflight", type=int, default=0,
-                   help="frames in flight (scene replicas / streams the steps rotate over); 0 = 8 for the "
-                        "headline, 1 for c2-c5")
+                   help="frames in flight (scene replicas / streams the steps rotate over); 0 = 8, "
+                        "1 for c5")
     return p.parse_args()
 
 
@@ -461,7 +461,10 @@ def main():
         # frames in flight: replicas 1..F-1 of the scene, each with its own frame buffers and
         # stream; step k renders frame k on replica k % F (replica 0 = ds, on a stream of its
         # own when F > 1 -- not torch's current stream, which the serial and counting passes use)
-        F = args.inflight or (8 if args.config == "headline" else 1)
+        # (C5's 4K x 64 spp frames fill the GPU on their own and its ray-tree levels take ~10 GB
+        # per replica: one; the others 8 -- C3 1 892 -> 4 153 Mrays/s, C4 1 653 -> 2 102, C2
+        # 7 792 -> 14 083: a frame's slowest waves no longer idle the GPU, profiles/r03v)
+        F = args.inflight or (1 if args.config == "c5" else 8)
         streams = [torch.cuda.Stream() for _ in range(F if F > 1 else 0)]
         reps = [(ds, hdr, ldr, streams[0].cuda_stream if F > 1 else sptr)]
         for k in range(1, F):
