@@ -1337,7 +1337,7 @@ int rtg_tonemap(const float* hdr, int32_t w, int32_t h, const rtg_tonemap_params
 }
 
 int rtg_tonemap_log_average(const float* hdr, int32_t w, int32_t h, int32_t mode, double* avg_out, int32_t device) {
-    if (!hdr || !avg_out || w <= 0 || h <= 0 || mode > 2) return set_err(RTG_ERR_INVALID, "bad log-average arguments");
+    if (!hdr || !avg_out || w <= 0 || h <= 0 || mode > 3) return set_err(RTG_ERR_INVALID, "bad log-average arguments");
     HIP_TRY(hipSetDevice(device));
     const size_t n = (size_t)w * h;
     float* dh = nullptr;

@@ -33,11 +33,13 @@ namespace {
 
 constexpr int kTmThreads = 256;
 
-// log-sum mode: 2 = windowed exact sum (k_tm_winsum), 1 = the plain chain (k_tm_seqsum),
-// 0 = parallel fixed-order reduction (not the reference's rounding).  The environment
-// variable RTG_TM_SEQSUM overrides it at run time (A/B and diagnostics).
+// log-sum mode: 3 = windowed exact sum with the windows summarised in parallel beforehand
+// (k_tm_wtot / k_tm_wguess / k_tm_wsumm + k_tm_winsum<true>), 2 = windowed exact sum
+// (k_tm_winsum<false>), 1 = the plain chain (k_tm_seqsum), 0 = parallel fixed-order reduction
+// (not the reference's rounding).  The environment variable RTG_TM_SEQSUM overrides it at run
+// time (A/B and diagnostics).
 #ifndef RTG_TM_SEQSUM
-#define RTG_TM_SEQSUM 2
+#define RTG_TM_SEQSUM 3
 #endif
 
 __device__ __forceinline__ uint32_t float_key(float x) {
@@ -160,14 +162,170 @@ constexpr int kWinThreads = 64 * kWinWaves;
 constexpr int kWin = kWinThreads * kWinPer;
 constexpr int kWinSlowRun = 4;
 constexpr int kWinChainRun = 16;
+
+// Mode 3: every aligned window of kWin terms summarised in parallel before the sequential
+// pass.  The binade the running sum will be in at a window's start is guessed from an
+// approximate prefix of the window totals (k_tm_wtot, k_tm_wguess); with that binade's unit u,
+// k_tm_wsumm forms each term's k = rint(x / u) and the window's total Q and the least and
+// greatest of its running partial sums (the prefixes after each term).  The sequential pass
+// (k_tm_winsum<true>) then crosses a whole window in one step when the guess is the binade the
+// exact running sum s actually has, no term is a tie or too large, sum |k| < 2^52 (so every
+// partial sum above is exact), and s + u * partial stays strictly inside the binade for every
+// prefix -- exactly the conditions under which the per-window scan of mode 2 would have
+// consumed the window whole, with the same result s + u * Q.  Any other window (the binade
+// crossings, the first windows while |s| is small, ties) takes mode 2's scan.
+struct WinSumm {
+    double q, pmin, pmax;   // total and extreme running partials of k = rint(x / u), units of u
+    int e, ok;              // guessed binade exponent (frexp) at the window start; usable
+};
+
+// approximate window totals (any order)
+__global__ __launch_bounds__(256) void k_tm_wtot(const double* __restrict__ logs, long long n, double* __restrict__ wtot) {
+    __shared__ double red[256];
+    const long long a = (long long)blockIdx.x * kWin;
+    double t = 0.0;
+    for (int j = threadIdx.x; j < kWin; j += 256) {
+        const long long i = a + j;
+        if (i < n) t += logs[i];
+    }
+    red[threadIdx.x] = t;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if ((int)threadIdx.x < w) red[threadIdx.x] += red[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) wtot[blockIdx.x] = red[0];
+}
+
+// approximate running sum at each window start (exclusive prefix of the totals) -> its binade
+__global__ void k_tm_wguess(const double* __restrict__ wtot, int nw, WinSumm* __restrict__ summ) {
+    if (threadIdx.x != 0) return;
+    double s = 0.0;
+    for (int w = 0; w < nw; ++w) {
+        int e = 0;
+        (void)frexp(s, &e);
+        summ[w].e = s != 0.0 ? e : INT_MIN;
+        s += wtot[w];
+    }
+}
+
+// window summaries (one block per window, kWinPer consecutive terms per thread)
+__global__ __launch_bounds__(kWinThreads) void k_tm_wsumm(const double* __restrict__ logs, long long n,
+                                                          WinSumm* __restrict__ summ) {
+    __shared__ double wtot[kWinWaves], wlo[kWinWaves], whi[kWinWaves], wabs[kWinWaves];
+    __shared__ int wbad[kWinWaves];
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const long long a = (long long)blockIdx.x * kWin;
+    const int e = summ[blockIdx.x].e;
+    const bool valid = e != INT_MIN;
+    double kk[kWinPer];
+    double tot = 0.0, absum = 0.0;
+    int bad = 0;
+#pragma unroll
+    for (int t = 0; t < kWinPer; ++t) {
+        const long long idx = a + tid * kWinPer + t;
+        kk[t] = 0.0;
+        if (idx < n && valid) {
+            const double y = ldexp(logs[idx], 53 - e);
+            const double r = rint(y);
+            const bool ok = fabs(y) < 4503599627370496.0 && fabs(y - r) != 0.5;
+            bad |= ok ? 0 : 1;
+            kk[t] = ok ? r : 0.0;
+        }
+        tot += kk[t];
+        absum += fabs(kk[t]);
+    }
+    // running partials inside the thread, relative to its start
+    double run = 0.0, lo = INFINITY, hi = -INFINITY;
+#pragma unroll
+    for (int t = 0; t < kWinPer; ++t) {
+        const long long idx = a + tid * kWinPer + t;
+        run += kk[t];
+        if (idx < n) {
+            lo = fmin(lo, run);
+            hi = fmax(hi, run);
+        }
+    }
+    // block exclusive scan of the thread totals
+    double incl = tot;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const double o = __shfl_up(incl, d);
+        if (lane >= d) incl += o;
+    }
+    if (lane == 63) wtot[wave] = incl;
+    __syncthreads();
+    double woff = 0.0;
+    for (int w = 0; w < wave; ++w) woff += wtot[w];
+    double excl = __shfl_up(incl, 1);
+    if (lane == 0) excl = 0.0;
+    excl += woff;
+    lo += excl;
+    hi += excl;
+    // block min / max / sum of |k| / any bad
+    double absw = absum;
+#pragma unroll
+    for (int d = 32; d > 0; d >>= 1) {
+        lo = fmin(lo, __shfl_xor(lo, d));
+        hi = fmax(hi, __shfl_xor(hi, d));
+        absw += __shfl_xor(absw, d);
+        bad |= __shfl_xor(bad, d);
+    }
+    if (lane == 0) {
+        wlo[wave] = lo;
+        whi[wave] = hi;
+        wabs[wave] = absw;
+        wbad[wave] = bad;
+    }
+    __syncthreads();
+    if (tid == 0) {
+        double L = INFINITY, H = -INFINITY, A = 0.0, Q = 0.0;
+        int B = 0;
+        for (int w = 0; w < kWinWaves; ++w) {
+            L = fmin(L, wlo[w]);
+            H = fmax(H, whi[w]);
+            A += wabs[w];
+            Q += wtot[w];
+            B |= wbad[w];
+        }
+        WinSumm& S = summ[blockIdx.x];
+        S.q = Q;
+        S.pmin = L;
+        S.pmax = H;
+        S.ok = valid && !B && A < 4503599627370496.0;   // every partial exact and within +-2^52
+    }
+}
+
+// The same sequential sum, an 8 192-term window per step (one block of eight waves, 16
+// consecutive terms per thread) instead of an 8 192-add chain.  While
+// the running sum s keeps one binade [2^(e-1), 2^e), every representable value there is a
+// multiple of u = 2^(e-53), so RN(s + x) = s + u * round(x / u) exactly -- unless x / u is a
+// tie (then the parity of s decides) or s + x leaves the binade.  Each thread takes 16
+// consecutive terms: k = rint(x / u) (an exact power-of-two scale), a lane-sequential prefix
+// and a block scan of the integer-valued k give the running sum in units of u after every term; the
+// first term whose result is not strictly inside the binade (or is a tie, or s = 0) stops
+// the window.  s jumps to that term's exact running value, the stopping term is added with
+// one rounded double add (the reference's own step), and the next window starts after it.
+// A window that stops within its first 64 terms (|s| small or near a power of two) is
+// finished with the plain rounded chain.  Such a window costs the scan on top of the chain,
+// so an input whose running sum keeps hovering near a binade boundary would run slower than
+// the plain chain; after kWinSlowRun consecutive short windows the kernel therefore runs
+// kWinChainRun windows as the plain chain (no scan) before it tries the shortcut again.
+// SUMM (mode 3): windows end at the aligned kWin boundaries, and an aligned window whose
+// summary (k_tm_wsumm) applies to the exact running sum is crossed in one step.
+// The result is the reference's sum bit for bit on any input.
+template <bool SUMM>
 __global__ __launch_bounds__(kWinThreads) void k_tm_winsum(const double* __restrict__ logs, long long n,
+                                                           const WinSumm* __restrict__ summ,
                                                            double* __restrict__ avg, uint32_t* __restrict__ sel,
                                                            uint32_t k) {
     __shared__ double buf[kWin];
     __shared__ double wtot[kWinWaves];
     __shared__ int wmin[kWinWaves];
     __shared__ double pshare;
+    __shared__ WinSumm sc[kWinThreads];      // SUMM: summaries of windows [cbase, cbase + kWinThreads)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const double lo = 4503599627370497.0, hi = 9007199254740990.0;   // 2^52 + 1, 2^53 - 2
     auto load = [&](double* v, long long at) {
 #pragma unroll
         for (int t = 0; t < kWinPer; ++t) {
@@ -179,20 +337,50 @@ __global__ __launch_bounds__(kWinThreads) void k_tm_winsum(const double* __restr
     load(cur, 0);
     double s = 0.0;   // the running sum: the same value in every thread
     long long a = 0;
+    long long cbase = -1;
     int slow = 0;     // consecutive short windows; >= kWinSlowRun: chain mode
     while (a < n) {
+        if (SUMM && a % kWin == 0 && slow < kWinSlowRun) {
+            const long long w = a / kWin;
+            if (cbase < 0 || w >= cbase + kWinThreads) {
+                __syncthreads();
+                cbase = w;
+                const long long nw = (n + kWin - 1) / kWin;
+                if (cbase + tid < nw) sc[tid] = summ[cbase + tid];
+                __syncthreads();
+            }
+            const WinSumm S = sc[w - cbase];
+            int e = 0;
+            const double fr = frexp(s, &e);
+            if (S.ok && s != 0.0 && e == S.e) {
+                const double M = ldexp(fr, 53);
+                const bool inside = s > 0.0 ? (M + S.pmin >= lo && M + S.pmax <= hi)
+                                            : (M + S.pmax <= -lo && M + S.pmin >= -hi);
+                if (inside) {   // the whole window: the scan would have consumed it
+                    s = ldexp(M + S.q, e - 53);
+                    a += kWin;
+                    continue;
+                }
+            }
+            load(cur, a);
+        }
+        // this window: [a, lim); SUMM: up to the next aligned boundary
+        const long long lim = SUMM ? ((a / kWin + 1) * kWin < n ? (a / kWin + 1) * kWin : n) : n;
+        const long long rem = lim - a;
+        const int wl = rem < kWin ? (int)rem : kWin;   // the window's terms
 #pragma unroll
         for (int t = 0; t < kWinPer; ++t) buf[tid * kWinPer + t] = cur[t];
-        load(nxt, a + kWin);   // speculative: the next window if this one is consumed whole
-        const long long rem = n - a;
+        if (!SUMM) load(nxt, a + kWin);   // speculative: the next window if this one is consumed whole
         if (slow >= kWinSlowRun) {         // chain mode: the reference's rounded adds, no scan
             __syncthreads();
-            const int m = rem < kWin ? (int)rem : kWin;
 #pragma unroll 8
-            for (int j = 0; j < m; ++j) s = s + buf[j];
-            a += kWin;
+            for (int j = 0; j < wl; ++j) s = s + buf[j];
+            a += wl;
+            if (SUMM) { if (a < n) load(cur, a); }
+            else {
 #pragma unroll
-            for (int t = 0; t < kWinPer; ++t) cur[t] = nxt[t];
+                for (int t = 0; t < kWinPer; ++t) cur[t] = nxt[t];
+            }
             if (++slow >= kWinSlowRun + kWinChainRun) slow = 0;
             __syncthreads();
             continue;
@@ -205,7 +393,6 @@ __global__ __launch_bounds__(kWinThreads) void k_tm_winsum(const double* __restr
         // that term is used
         const double M = s != 0.0 ? ldexp(fr, 53) : 0.0;
         const bool neg = s < 0.0;
-        const double lo = 4503599627370497.0, hi = 9007199254740990.0;   // 2^52 + 1, 2^53 - 2
         double kk[kWinPer];
         double tot = 0.0;
         int bad = kWinPer;   // first term of this thread that cannot take the shortcut
@@ -266,24 +453,28 @@ __global__ __launch_bounds__(kWinThreads) void k_tm_winsum(const double* __restr
         __syncthreads();
         const double pf = f >= kWin ? M + all : pshare;
         if (f > 0) s = ldexp(pf, e - 53);
-        if (f >= kWin) {   // the whole window took the shortcut
+        if (f >= wl) {   // every term of the window took the shortcut
             slow = 0;
-            a += kWin;
+            a += wl;
+            if (SUMM) { if (a < n && a % kWin != 0) load(cur, a); }
+            else {
 #pragma unroll
-            for (int t = 0; t < kWinPer; ++t) cur[t] = nxt[t];
+                for (int t = 0; t < kWinPer; ++t) cur[t] = nxt[t];
+            }
             __syncthreads();
             continue;
         }
-        if ((long long)f >= rem) break;   // every remaining term took the shortcut
         s = s + buf[f];                    // the stopping term: the reference's rounded add
         if (f < 64) {                      // slow region: finish the window as a chain
             ++slow;
-            const int m = rem < kWin ? (int)rem : kWin;
 #pragma unroll 8
-            for (int j = f + 1; j < m; ++j) s = s + buf[j];
-            a += kWin;
+            for (int j = f + 1; j < wl; ++j) s = s + buf[j];
+            a += wl;
+            if (SUMM) { if (a < n && (a % kWin != 0 || slow >= kWinSlowRun)) load(cur, a); }
+            else {
 #pragma unroll
-            for (int t = 0; t < kWinPer; ++t) cur[t] = nxt[t];
+                for (int t = 0; t < kWinPer; ++t) cur[t] = nxt[t];
+            }
         } else {
             slow = 0;
             a += f + 1;
@@ -390,8 +581,9 @@ __global__ __launch_bounds__(kTmThreads) void k_tm_map(const float* __restrict__
 }  // namespace
 
 size_t tonemap_scratch_bytes(long long pixels) {
+    const size_t nw = (size_t)((pixels + kWin - 1) / kWin);
     return 1024 * sizeof(double) + 2 * sizeof(double) + 258 * sizeof(uint32_t) + 256 +
-           (size_t)pixels * sizeof(double);
+           (size_t)pixels * sizeof(double) + nw * (sizeof(double) + sizeof(WinSumm)) + 16;
 }
 
 // avg = exp(sum of log(delta + Y) / pixelCount) into the scratch's avg slot (tonemap_avg_offset);
@@ -410,8 +602,19 @@ void launch_log_average(const float* hdr, long long n, int mode, uint32_t idx, v
     if (mode > 0) {
         hipLaunchKernelGGL(k_tm_log, dim3((unsigned)((n + kTmThreads - 1) / kTmThreads)), dim3(kTmThreads), 0, st,
                            hdr, n, logs);
-        if (mode == 1) hipLaunchKernelGGL(k_tm_seqsum, dim3(1), dim3(64), 0, st, logs, n, avg, sel, idx);
-        else hipLaunchKernelGGL(k_tm_winsum, dim3(1), dim3(kWinThreads), 0, st, logs, n, avg, sel, idx);
+        if (mode == 1) {
+            hipLaunchKernelGGL(k_tm_seqsum, dim3(1), dim3(64), 0, st, logs, n, avg, sel, idx);
+        } else if (mode == 2) {
+            hipLaunchKernelGGL(k_tm_winsum<false>, dim3(1), dim3(kWinThreads), 0, st, logs, n, nullptr, avg, sel, idx);
+        } else {
+            const int nw = (int)((n + kWin - 1) / kWin);
+            double* wtot = logs + n;
+            WinSumm* summ = reinterpret_cast<WinSumm*>(wtot + nw);
+            hipLaunchKernelGGL(k_tm_wtot, dim3(nw), dim3(256), 0, st, logs, n, wtot);
+            hipLaunchKernelGGL(k_tm_wguess, dim3(1), dim3(64), 0, st, wtot, nw, summ);
+            hipLaunchKernelGGL(k_tm_wsumm, dim3(nw), dim3(kWinThreads), 0, st, logs, n, summ);
+            hipLaunchKernelGGL(k_tm_winsum<true>, dim3(1), dim3(kWinThreads), 0, st, logs, n, summ, avg, sel, idx);
+        }
     } else {
         const int nb = (int)((n + kTmThreads - 1) / kTmThreads < 1024 ? (n + kTmThreads - 1) / kTmThreads : 1024);
         hipLaunchKernelGGL(k_tm_logsum, dim3(nb), dim3(kTmThreads), 0, st, hdr, n, partial);

@@ -431,8 +431,10 @@ int rtg_tonemap(const float* hdr_rgb, int32_t width, int32_t height, const rtg_t
                 uint8_t* ldr_rgb, int32_t device);
 /* Tonemapper::avgLuminance (tonemapper.h:35-48): exp(sum of log(0.01f + Y) / pixelCount) with
  * the sum taken as the reference takes it, sequentially in pixel order, on host buffers
- * (synchronous).  mode: -1 the library default, 2 windowed exact sum, 1 plain sequential
- * chain, 0 parallel fixed-order reduction (last bits differ from the reference's). */
+ * (synchronous).  mode: -1 the library default (3), 3 windowed exact sum with the windows
+ * summarised in parallel beforehand (ABI 5), 2 windowed exact sum, 1 plain sequential chain
+ * (modes 1-3 give the same bits), 0 parallel fixed-order reduction (last bits differ from
+ * the reference's). */
 int rtg_tonemap_log_average(const float* hdr_rgb, int32_t width, int32_t height, int32_t mode, double* avg_out,
                             int32_t device);
 

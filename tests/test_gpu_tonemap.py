@@ -90,17 +90,24 @@ def _log_inputs():
     yield "black", np.zeros((200, 333, 3), np.float32)
     yield "ragged_1x1", np.full((1, 1, 3), 2.0, np.float32)
     yield "ragged_7x150", rng.lognormal(0.0, 2.0, size=(7, 150, 3)).astype(np.float32)
+    # 4K, a sum that crosses zero and many binades: the mode-3 summaries fail and succeed
+    yield "mixed_4k", np.concatenate([rng.lognormal(1.0, 1.0, size=(1080, 3840, 3)),
+                                      rng.lognormal(-2.0, 1.0, size=(1080, 3840, 3))]).astype(np.float32)
 
 
 @pytest.mark.parametrize("name,hdr", list(_log_inputs()), ids=[n for n, _ in _log_inputs()])
 def test_log_average_sequential(name, hdr):
-    """The windowed sum (mode 2, the default) equals the plain sequential chain (mode 1) bit for
-    bit, and both equal the reference's host sum (glibc log) to the last bit where the device
-    log agrees with glibc's (asserted within 1e-15 relative; exact equality is reported)."""
+    """The windowed sums -- with the windows summarised in parallel first (mode 3, the default)
+    and without (mode 2) -- equal the plain sequential chain (mode 1) bit for bit, and all equal
+    the reference's host sum (glibc log) to the last bit where the device log agrees with
+    glibc's (asserted within 1e-15 relative; exact equality is reported)."""
     win = rtgpu.tonemap_log_average(hdr, 2)
+    summ = rtgpu.tonemap_log_average(hdr, 3)
     chain = rtgpu.tonemap_log_average(hdr, 1)
     assert win == chain or (math.isnan(win) and math.isnan(chain)), (name, win.hex(), chain.hex())
-    assert rtgpu.tonemap_log_average(hdr, -1) == win
+    assert summ == chain or (math.isnan(summ) and math.isnan(chain)), (name, summ.hex(), chain.hex())
+    dflt = rtgpu.tonemap_log_average(hdr, -1)
+    assert dflt == summ or (math.isnan(dflt) and math.isnan(summ))
     ref = _seq_log_average(hdr)
     print(name, "window == chain;", "== host reference" if win == ref else f"host {ref!r} vs {win!r}")
     assert abs(win - ref) <= 1e-15 * abs(ref), (name, win, ref)
