@@ -76,3 +76,85 @@ def test_window_sum_equals_sequential(name):
     assert got == ref, (name, got.hex(), ref.hex())
     if name in ("lognormal", "bright", "black"):
         assert fast > 0.6 * len(x), (name, fast, len(x))   # the shortcut carries most of the sum
+
+
+def summaries(x):
+    """k_tm_wtot / k_tm_wguess / k_tm_wsumm: per aligned window, the guessed binade exponent at
+    its start (from an approximate prefix of the window totals), the total Q of k = rint(x/u)
+    and the least / greatest running partial, and whether the window is usable."""
+    n = len(x)
+    nw = (n + WIN - 1) // WIN
+    tots = [float(np.sum(x[w * WIN:(w + 1) * WIN])) for w in range(nw)]
+    out, s = [], 0.0
+    for w in range(nw):
+        e = math.frexp(s)[1] if s != 0.0 else None
+        s += tots[w]
+        win = x[w * WIN:(w + 1) * WIN]
+        if e is None:
+            out.append((None, 0, 0, 0, False))
+            continue
+        y = np.ldexp(win, 53 - e)
+        r = np.rint(y)
+        ok = (np.abs(y) < 2.0 ** 52) & (np.abs(y - r) != 0.5)
+        k = np.where(ok, r, 0.0)
+        usable = bool(ok.all()) and float(np.abs(k).sum()) < 2.0 ** 52
+        P = np.cumsum(k.astype(np.int64))
+        out.append((e, int(P[-1]), int(P.min()), int(P.max()), usable))
+    return out
+
+
+def summarised_sum(x):
+    """k_tm_winsum<true>: windows end at aligned boundaries; an aligned window whose summary
+    applies to the exact running sum is crossed in one step, every other takes the window rule."""
+    n = len(x)
+    summ = summaries(x)
+    s, a, skipped = 0.0, 0, 0
+    while a < n:
+        if a % WIN == 0:
+            e_g, Q, pmin, pmax, usable = summ[a // WIN]
+            if usable and s != 0.0:
+                fr, e = math.frexp(s)
+                if e == e_g:
+                    M = int(math.ldexp(fr, 53))
+                    inside = (M + pmin >= LO and M + pmax <= HI) if s > 0 else (M + pmax <= -LO and M + pmin >= -HI)
+                    if inside:
+                        s = math.ldexp(float(M + Q), e - 53)
+                        skipped += min(WIN, n - a)
+                        a += WIN
+                        continue
+        lim = min(n, (a // WIN + 1) * WIN)
+        win = x[a:lim]
+        fr, e = math.frexp(s)
+        M = int(math.ldexp(fr, 53)) if s != 0.0 else 0
+        y = np.ldexp(win, 53 - e)
+        r = np.rint(y)
+        ok = (s != 0.0) & (np.abs(y) < 2.0 ** 52) & (np.abs(y - r) != 0.5)
+        k = np.where(ok, r, 0.0).astype(np.int64)
+        P = M + np.cumsum(k)
+        mag = -P if s < 0.0 else P
+        bad = ~ok | (mag < LO) | (mag > HI)
+        f = int(np.argmax(bad)) if bad.any() else len(win)
+        if f > 0:
+            s = math.ldexp(float(M + int(k[:f].sum())), e - 53)
+        if f == len(win):
+            a = lim
+            continue
+        s = s + float(win[f])
+        if f < 64:
+            for v in win[f + 1:].tolist():
+                s = s + v
+            a = lim
+        else:
+            a += f + 1
+    return s, skipped
+
+
+@pytest.mark.parametrize("name", sorted(CASES))
+def test_summarised_window_sum_equals_sequential(name):
+    """Mode 3's rule (windows summarised in parallel, then crossed whole where the summary
+    applies) gives the left-to-right double sum bit for bit."""
+    x = np.ascontiguousarray(CASES[name](np.random.default_rng(7)), np.float64)
+    (got, skipped), ref = summarised_sum(x), seq_sum(x)
+    assert got == ref, (name, got.hex(), ref.hex())
+    if name in ("bright", "black"):   # sums that run away from zero: most windows crossed whole
+        assert skipped > 0.5 * len(x), (name, skipped, len(x))
