@@ -905,6 +905,141 @@ DEV int walk_wide_any(const DevScene& S, int node, const Ray& lr, float minT0, f
     return undecided ? -1 : 0;
 }
 
+// The same walk as a wave packet (RTG_ANY_PACKET): the wave visits one node sequence, the
+// union of its live lanes' walks, so node, face and reference-leaf records are wave-uniform
+// (scalar loads through the scalar cache, nothing through the vector memory path) and the
+// stack is wave-uniform too (64 LDS words per wave, written by one live lane).  A lane tests a child, a face or a
+// leaf box wherever the wave goes, also below boxes it failed itself: every decision is the
+// exact one above (sufficient -> 1, necessary only -> undecided), so extra tests change no
+// answer, and every leaf a lane's own walk reaches is still visited.  A lane leaves the packet
+// at its first sufficient face; the wave stops when no live lane is left or the stack is empty.
+// The nearest inner child of the first live lane goes next, the others onto the stack.
+#ifndef RTG_ANY_PACKET
+#define RTG_ANY_PACKET 0
+#endif
+#define RTG_PK_STACK 64
+#ifndef RTG_PK_MAX_STEPS
+#define RTG_PK_MAX_STEPS 4096
+#endif
+// Wave-uniform records through the scalar cache (the compiler keeps vector loads here: the
+// kernels store to global memory, so it cannot prove the records unclobbered).  Read-only
+// scene data, written by copies before the launch.
+typedef int rtg_s16 __attribute__((ext_vector_type(16)));
+typedef int rtg_s8 __attribute__((ext_vector_type(8)));
+typedef int rtg_s4 __attribute__((ext_vector_type(4)));
+DEV const void* uniform_ptr(const void* p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (const void*)(((uint64_t)hi << 32) | lo);
+}
+DEV void sload_wnode(const WNode* p, rtg_s16& a, rtg_s16& b) {   // 128 B
+    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(a), "=&s"(b) : "s"(uniform_ptr(p)) : "memory");
+}
+DEV void sload_rec(const float4* p, rtg_s8& a, rtg_s4& b) {      // 48 B: a face record
+    asm volatile("s_load_dwordx8 %0, %2, 0x0\n\ts_load_dwordx4 %1, %2, 0x20\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(a), "=&s"(b) : "s"(uniform_ptr(p)) : "memory");
+}
+DEV void sload_node(const float4* p, rtg_s8& a) {                // 32 B: a reference BVH node
+    asm volatile("s_load_dwordx8 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=&s"(a) : "s"(uniform_ptr(p)) : "memory");
+}
+DEV float4 f4(int x, int y, int z, int w) {
+    return make_float4(__int_as_float(x), __int_as_float(y), __int_as_float(z), __int_as_float(w));
+}
+template <bool STATS>
+DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0, float limit, bool inst_conf,
+                         Cnt<STATS>& c) {
+    const RayRcp q = ray_rcp(lr);
+    const float minTc = minT0 * (1.0f + 0x1p-21f);
+    const SlabRay sr = slab_ray(lr, q);
+    bool live = q.fast;                              // still walking
+    bool occ = false;                                // a sufficient face found
+    bool undecided = !q.fast;                        // zero / tiny direction component: reference walk
+    __shared__ int pk_stack[4][RTG_PK_STACK];        // the wave's stack (256-thread blocks)
+    int* const stk = pk_stack[(threadIdx.x >> 6) & 3];
+    int sp = 0;                                      // wave-uniform
+    node = __builtin_amdgcn_readfirstlane(node);
+    int steps = 0;                                   // bound: a walk visits each node once
+    while (__ballot(live)) {
+        if (++steps > RTG_PK_MAX_STEPS) {
+            undecided |= live;
+            break;
+        }
+        node = __builtin_amdgcn_readfirstlane(node);
+        rtg_s16 na, nb;
+        sload_wnode(S.anodes + node, na, nb);
+        const float4 lox = f4(na[0], na[1], na[2], na[3]), hix = f4(na[4], na[5], na[6], na[7]);
+        const float4 loy = f4(na[8], na[9], na[10], na[11]), hiy = f4(na[12], na[13], na[14], na[15]);
+        const float4 loz = f4(nb[0], nb[1], nb[2], nb[3]), hiz = f4(nb[4], nb[5], nb[6], nb[7]);
+        const int4 ch = make_int4(nb[8], nb[9], nb[10], nb[11]), lf = make_int4(nb[12], nb[13], nb[14], nb[15]);
+        if (live) c.wnode();
+        float tn[4];
+        bool h[4];
+        h[0] = slab_cons(lox.x, loy.x, loz.x, hix.x, hiy.x, hiz.x, sr, minTc, tn[0]) & live;
+        h[1] = slab_cons(lox.y, loy.y, loz.y, hix.y, hiy.y, hiz.y, sr, minTc, tn[1]) & live;
+        h[2] = slab_cons(lox.z, loy.z, loz.z, hix.z, hiy.z, hiz.z, sr, minTc, tn[2]) & live;
+        h[3] = slab_cons(lox.w, loy.w, loz.w, hix.w, hiy.w, hiz.w, sr, minTc, tn[3]) & live;
+        const int cidx[4] = {ch.x, ch.y, ch.z, ch.w};
+        const int lidx[4] = {lf.x, lf.y, lf.z, lf.w};
+        const uint64_t lm = __ballot(live);
+        const int lead = __ffsll((long long)lm) - 1;
+        int next = -1;
+        float nextT = INFINITY;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int cr = cidx[k];
+            if (cr == WCHILD_EMPTY || !__ballot(h[k])) continue;
+            if (cr >= 0) {
+                const float t = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tn[k]), lead));
+                int spill = cr;
+                if (t < nextT) {
+                    spill = next;
+                    next = cr;
+                    nextT = t;
+                }
+                if (spill >= 0) {
+                    if (sp < RTG_PK_STACK) {             // written by the first live lane
+                        if ((int)(threadIdx.x & 63) == lead) stk[sp] = spill;
+                        ++sp;
+                    }
+                    else undecided |= live;
+                }
+                continue;
+            }
+            const int first = lidx[k] >> 8, cnt = lidx[k] & 255;
+            for (int e = first; e < first + cnt; ++e) {
+                rtg_s8 ra;
+                rtg_s4 rb;
+                sload_rec(S.ahtris + 3 * (size_t)e, ra, rb);
+                if (!h[k]) continue;
+                c.template tri<true>();
+                const float4 R[3] = {f4(ra[0], ra[1], ra[2], ra[3]), f4(ra[4], ra[5], ra[6], ra[7]), f4(rb[0], rb[1], rb[2], rb[3])};
+                float t;
+                if (!tri_test_fast_rec(R, lr, limit, t)) continue;
+                rtg_s8 rn;
+                sload_node(S.nodes + 2 * ra[3], rn);
+                const float4 a = f4(rn[0], rn[1], rn[2], rn[3]), b = f4(rn[4], rn[5], rn[6], rn[7]);
+                if (!box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, minT0)) continue;   // leaf unreachable
+                if (inst_conf && box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, limit)) {
+                    live = false;
+                    occ = true;
+                    h[k] = false;
+                    continue;
+                }
+                undecided = true;
+            }
+        }
+        if (!__ballot(live)) break;
+        if (next >= 0) {
+            node = next;
+            continue;
+        }
+        if (sp == 0) break;
+        node = stk[--sp];
+    }
+    return occ ? 1 : (undecided ? -1 : 0);
+}
+
 // CastShadowRay on the wide BVH: objects in any order (the answer is a boolean), spheres
 // exactly (a sphere hit with t < limit is accepted at any minT_cur >= limit, one with
 // t >= limit never decides).  Returns 1 / 0 / -1 (undecided: run trace<true>).
@@ -939,7 +1074,8 @@ DEV int trace_any_wide(const DevScene& S, const Ray& r, float minT0, float limit
         }
         const Ray lr = (FEAT & FEAT_XFORM) ? trav_ray(ob, r, 0.f) : r;
         if (ob.aroot < 0) return -1;                 // no any-hit tree for this mesh: reference walk
-        const int res = walk_wide_any<STATS>(S, ob.aroot, lr, minT0, limit, conf, c);
+        const int res = RTG_ANY_PACKET ? walk_wide_any_pk<STATS>(S, ob.aroot, lr, minT0, limit, conf, c)
+                                       : walk_wide_any<STATS>(S, ob.aroot, lr, minT0, limit, conf, c);
         if (res > 0) return 1;
         undecided |= res < 0;
     }
