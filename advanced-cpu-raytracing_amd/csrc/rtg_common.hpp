@@ -797,11 +797,19 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
 #ifndef RTG_WIDE_STACK
 #define RTG_WIDE_STACK 24
 #endif
-// k_shadow<FAST> (the wide walk + the in-place reference fallback) compiled for this many
-// waves per SIMD: five (96 VGPRs, no spills) measured 0.228 ms on the headline against 0.291 at six
-// (76 B of spills) and 0.26 at the natural four; instance scenes keep RTG_INST_WAVES
+// Shadow rays walk the any-hit tree as wave packets (walk_wide_any_pk) -- 1, the default:
+// headline k_shade_shadow 0.246 -> 0.211 ms, 0 differing pixels (profiles/r03pk*) -- or per
+// lane (walk_wide_any) -- 0.
+#ifndef RTG_ANY_PACKET
+#define RTG_ANY_PACKET 1
+#endif
+// k_shadow<FAST> / the fused shade kernel (the wide walk + the in-place reference fallback)
+// compiled for this many waves per SIMD.  Per-lane walk (RTG_ANY_PACKET=0): five (96 VGPRs, no
+// spills) measured 0.228 ms on the headline against 0.291 at six (76 B of spills) and 0.26 at the
+// natural four.  Packet walk (default): 81 VGPRs and no LDS stack at five, six 0.211 ms, seven
+// 0.215, eight 0.216 (profiles/r03pk4_*); instance scenes keep RTG_INST_WAVES
 #ifndef RTG_WIDE_WAVES_PLAIN
-#define RTG_WIDE_WAVES_PLAIN 5
+#define RTG_WIDE_WAVES_PLAIN (RTG_ANY_PACKET ? 6 : 5)
 #endif
 #define RTG_WIDE_WAVES(FEAT) (((FEAT) & FEAT_INSTANCE) ? RTG_INST_WAVES : RTG_WIDE_WAVES_PLAIN)
 
@@ -914,9 +922,6 @@ DEV int walk_wide_any(const DevScene& S, int node, const Ray& lr, float minT0, f
 // answer, and every leaf a lane's own walk reaches is still visited.  A lane leaves the packet
 // at its first sufficient face; the wave stops when no live lane is left or the stack is empty.
 // The nearest inner child of the first live lane goes next, the others onto the stack.
-#ifndef RTG_ANY_PACKET
-#define RTG_ANY_PACKET 0
-#endif
 #define RTG_PK_STACK 64
 #ifndef RTG_PK_MAX_STEPS
 #define RTG_PK_MAX_STEPS 4096
@@ -1048,15 +1053,26 @@ DEV int trace_any_wide(const DevScene& S, const Ray& r, float minT0, float limit
     const RayRcp rq = (FEAT & FEAT_INSTANCE) ? ray_rcp(r) : RayRcp{};
     if ((FEAT & FEAT_INSTANCE) && !rq.fast) return -1;
     bool undecided = false;
+    int gskip = 0;                   // packet walks: this lane skips objects below gskip
     for (int k = 0; k < S.num_objects; ++k) {
         const DevObject& ob = S.objects[k];
         if ((FEAT & FEAT_INSTANCE) && ob.group_end > k) {
             const float4 ga = S.group_box[2 * k], gb = S.group_box[2 * k + 1];
-            if (!box_hit_fast(ga.x, ga.y, ga.z, gb.x, gb.y, gb.z, r, rq, minT0)) {
+            if (RTG_ANY_PACKET) {
+                // the packet walk needs one object (one root) per wave: a lane whose group box
+                // fails sits the group out, and the wave jumps over it when every lane does
+                if (k >= gskip && !box_hit_fast(ga.x, ga.y, ga.z, gb.x, gb.y, gb.z, r, rq, minT0))
+                    gskip = ob.group_end;
+                if (!__ballot(k >= gskip)) {
+                    k = ob.group_end - 1;
+                    continue;
+                }
+            } else if (!box_hit_fast(ga.x, ga.y, ga.z, gb.x, gb.y, gb.z, r, rq, minT0)) {
                 k = ob.group_end - 1;
                 continue;
             }
         }
+        if (RTG_ANY_PACKET && k < gskip) continue;
         c.obj();
         if ((FEAT & FEAT_SPHERE) && ob.kind == OBJ_SPHERE) {
             c.sph();
