@@ -210,6 +210,8 @@ DEV RayRcp ray_rcp(const Ray& r) {
     q.fast = ax >= lo && ax <= hi && ay >= lo && ay <= hi && az >= lo && az <= hi;
     return q;
 }
+// UNI: the exact fallback as a wave-uniform branch (wave packets: every lane tests the same box)
+template <bool UNI = false>
 DEV bool box_hit_fast(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, const Ray& r,
                       const RayRcp& q, float minT) {
     // branch-free: every condition is evaluated (bitwise &, no short circuit), so the
@@ -225,7 +227,13 @@ DEV bool box_hit_fast(float mnx, float mny, float mnz, float mxx, float mxy, flo
     const bool sure = (int)q.fast & (atmax >= 1e-30f) & (atmax <= 1e30f) & (atmin <= 1e30f) &
                       (fabsf(tmax - tmin) > slack) &
                       ((minT == INFINITY) | (fabsf(tmin - minT) > 0x1p-20f * atmin + 1e-30f));
-    const bool hit = (tmax > 0) & (tmax >= tmin) & (tmin < minT);
+    bool hit = (tmax > 0) & (tmax >= tmin) & (tmin < minT);
+    if constexpr (UNI) {
+        if (__builtin_expect(__ballot(!sure) != 0, 0)) {
+            if (!sure) hit = box_hit(mnx, mny, mnz, mxx, mxy, mxz, r, minT);
+        }
+        return hit;
+    }
     if (__builtin_expect(!sure, 0)) return box_hit(mnx, mny, mnz, mxx, mxy, mxz, r, minT);
     return hit;
 }
@@ -338,6 +346,43 @@ DEV bool tri_test_fast_rec(const float4* R, const Ray& r, float minT, float& tou
         }
     }
     return tri_test_rec(R, r, minT, tout);
+}
+
+// tri_test_fast_rec for wave packets (every lane tests the same face): the same decisions,
+// taken with selects -- the early outs become lane masks, and the two costly parts (the t
+// division, the exact fallback) wave-uniform branches taken when some lane needs them.
+DEV bool tri_test_fast_pk(const float4* R, const Ray& r, float limit, float& tout) {
+    const float4 A = R[0], E1 = R[1], E2 = R[2];
+    const float dx = r.d.x, dy = r.d.y, dz = r.d.z;
+    const float detA = det3(E1.x, E2.x, dx, E1.y, E2.y, dy, E1.z, E2.z, dz);
+    const float ad = fabsf(detA);
+    const float rd = __builtin_amdgcn_rcpf(detA);
+    const float sx = A.x - r.o.x, sy = A.y - r.o.y, sz = A.z - r.o.z;
+    const float nb = det3(sx, E2.x, dx, sy, E2.y, dy, sz, E2.z, dz);
+    const float ng = det3(E1.x, sx, dx, E1.y, sy, dy, E1.z, sz, dz);
+    const float beta = nb * rd, gama = ng * rd, sum = gama + beta;
+    const bool zero = detA == 0;
+    const bool range = (ad >= 0x1p-100f) & (ad <= 0x1p100f);
+    const bool bsure = (nb == 0.0f) | (fabsf(beta) > 1e-30f);
+    const bool gsure = (ng == 0.0f) | (fabsf(gama) > 1e-30f);
+    const bool ssure = fabsf(sum - 1.0f) > 0x1p-19f * sum + 0x1p-22f;
+    // tri_test_fast_rec's decision tree: false / t test / exact fallback
+    const bool b_out = range & bsure & (beta < 0);
+    const bool g_out = range & bsure & !(beta < 0) & gsure & (gama < 0);
+    const bool s_ok = range & bsure & !(beta < 0) & gsure & !(gama < 0) & ssure;
+    const bool no = zero | b_out | g_out | (s_ok & (sum > 1));
+    const bool tt = !zero & s_ok & !(sum > 1);
+    bool hit = false;
+    if (__ballot(tt)) {
+        const float t = det3(E1.x, E2.x, sx, E1.y, E2.y, sy, E1.z, E2.z, sz) / detA;
+        tout = t;
+        hit = tt & (t > 0.0f) & (t < limit);
+    }
+    const bool unsure = !no & !tt;
+    if (__builtin_expect(__ballot(unsure) != 0, 0)) {
+        if (unsure) hit = tri_test_rec(R, r, limit, tout);
+    }
+    return hit;
 }
 
 // 64-bit lexicographic (t, face) key of a candidate hit; t > 0, so the float bits order
@@ -923,6 +968,11 @@ DEV int walk_wide_any(const DevScene& S, int node, const Ray& lr, float minT0, f
 // at its first sufficient face; the wave stops when no live lane is left or the stack is empty.
 // The nearest inner child of the first live lane goes next, the others onto the stack.
 #define RTG_PK_STACK 64
+// the packet walk's face tests with selects and wave-uniform branches (1: k_shade_shadow 0.211 ->
+// 0.190 ms, profiles/r03sel_ab.txt) or per-lane early outs (0)
+#ifndef RTG_PK_SELECT
+#define RTG_PK_SELECT 1
+#endif
 #ifndef RTG_PK_MAX_STEPS
 #define RTG_PK_MAX_STEPS 4096
 #endif
@@ -1016,6 +1066,26 @@ DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0
                 rtg_s8 ra;
                 rtg_s4 rb;
                 sload_rec(S.ahtris + 3 * (size_t)e, ra, rb);
+#if RTG_PK_SELECT
+                if (h[k]) c.template tri<true>();
+                const float4 R[3] = {f4(ra[0], ra[1], ra[2], ra[3]), f4(ra[4], ra[5], ra[6], ra[7]), f4(rb[0], rb[1], rb[2], rb[3])};
+                float t;
+                const bool ok = tri_test_fast_pk(R, lr, limit, t) & h[k];
+                if (!__ballot(ok)) continue;
+                rtg_s8 rn;
+                sload_node(S.nodes + 2 * ra[3], rn);
+                const bool reach = ok & box_hit_fast<true>(__int_as_float(rn[0]), __int_as_float(rn[1]), __int_as_float(rn[2]),
+                                                           __int_as_float(rn[3]), __int_as_float(rn[4]), __int_as_float(rn[5]),
+                                                           lr, q, minT0);
+                const bool suff = reach & inst_conf &
+                                  box_hit_fast<true>(__int_as_float(rn[0]), __int_as_float(rn[1]), __int_as_float(rn[2]),
+                                                     __int_as_float(rn[3]), __int_as_float(rn[4]), __int_as_float(rn[5]),
+                                                     lr, q, limit);
+                occ |= suff;
+                live &= !suff;
+                h[k] &= !suff;
+                undecided |= reach & !suff;
+#else
                 if (!h[k]) continue;
                 c.template tri<true>();
                 const float4 R[3] = {f4(ra[0], ra[1], ra[2], ra[3]), f4(ra[4], ra[5], ra[6], ra[7]), f4(rb[0], rb[1], rb[2], rb[3])};
@@ -1032,6 +1102,7 @@ DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0
                     continue;
                 }
                 undecided = true;
+#endif
             }
         }
         if (!__ballot(live)) break;
