@@ -348,10 +348,11 @@ DEV bool tri_test_fast_rec(const float4* R, const Ray& r, float minT, float& tou
     return tri_test_rec(R, r, minT, tout);
 }
 
-// tri_test_fast_rec for wave packets (every lane tests the same face): the same decisions,
-// taken with selects -- the early outs become lane masks, and the two costly parts (the t
-// division, the exact fallback) wave-uniform branches taken when some lane needs them.
-DEV bool tri_test_fast_pk(const float4* R, const Ray& r, float limit, float& tout) {
+// tri_test_fast_rec with selects (wave packets, where every lane tests the same face, and the
+// per-lane walk under RTG_SEQ_SEL): the same decisions -- the early outs become lane masks,
+// and the two costly parts (the t division, the exact fallback) wave-uniform branches taken
+// when some lane needs them.
+DEV bool tri_test_sel(const float4* R, const Ray& r, float limit, float& tout) {
     const float4 A = R[0], E1 = R[1], E2 = R[2];
     const float dx = r.d.x, dy = r.d.y, dz = r.d.z;
     const float detA = det3(E1.x, E2.x, dx, E1.y, E2.y, dy, E1.z, E2.z, dz);
@@ -422,6 +423,12 @@ DEV uint64_t wave_min_key(uint64_t key, uint64_t em) {
 // the faces after it, Aila & Laine HPG 2009 -- measured slower: k_primary 0.238 -> 0.309 ms,
 // C5 1471 -> 954 Mrays/s; profiles/r03l_*.  The lanes that reach a leaf early idle in the box
 // loop, and every lane pays the loop's exit bookkeeping per node.)
+// the per-lane walk's face test with selects (tri_test_sel) and the slab test's exact fallback
+// as a wave-uniform branch (1: k_primary 0.238 -> 0.228 ms, profiles/r03seq_ab.txt) or with
+// per-lane early outs and a divergent fallback (0)
+#ifndef RTG_SEQ_SEL
+#define RTG_SEQ_SEL 1
+#endif
 template <bool ANY, bool STATS>
 DEV bool walk_bvh_seq(const DevScene& S, int i, const int end, const Ray& r, float& minT, int& hitFace, float limit,
                       Cnt<STATS>& c) {
@@ -432,7 +439,7 @@ DEV bool walk_bvh_seq(const DevScene& S, int i, const int end, const Ray& r, flo
         const float4 b = S.nodes[2 * i + 1];
         c.template node<ANY>();
         const int skip = __float_as_int(b.z);
-        if (box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, r, q, minT)) {
+        if (box_hit_fast<RTG_SEQ_SEL != 0>(a.x, a.y, a.z, a.w, b.x, b.y, r, q, minT)) {
             const int leaf = __float_as_int(b.w);
             if (leaf >= 0) {
                 int first = leaf >> 8, cnt = leaf & 255;
@@ -444,7 +451,7 @@ DEV bool walk_bvh_seq(const DevScene& S, int i, const int end, const Ray& r, flo
                 for (int f = first; f < first + cnt; ++f) {
                     c.template tri<ANY>();
                     float t;
-                    if (tri_test_fast(S, f, r, minT, t)) {
+                    if (RTG_SEQ_SEL ? tri_test_sel(S.tris + 3 * f, r, minT, t) : tri_test_fast(S, f, r, minT, t)) {
                         minT = t;
                         hitFace = f;
                         hit = true;
@@ -1070,7 +1077,7 @@ DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0
                 if (h[k]) c.template tri<true>();
                 const float4 R[3] = {f4(ra[0], ra[1], ra[2], ra[3]), f4(ra[4], ra[5], ra[6], ra[7]), f4(rb[0], rb[1], rb[2], rb[3])};
                 float t;
-                const bool ok = tri_test_fast_pk(R, lr, limit, t) & h[k];
+                const bool ok = tri_test_sel(R, lr, limit, t) & h[k];
                 if (!__ballot(ok)) continue;
                 rtg_s8 rn;
                 sload_node(S.nodes + 2 * ra[3], rn);

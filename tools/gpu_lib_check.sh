@@ -12,9 +12,9 @@ RTGPU_LIB=$PWD/advanced-cpu-raytracing_amd/$lib timeout -k 10 600 python -u -m p
 rc=$?; echo "pytest rc=$rc" >> $st
 [ $rc -ne 0 ] && exit $rc
 for c in $cfgs; do
-  for l in base $lib; do
+  for l in $lib base; do
     if [ $l = base ]; then unset RTGPU_LIB; else export RTGPU_LIB=$PWD/advanced-cpu-raytracing_amd/$l; fi
-    timeout -k 10 200 python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline > $out/bench_${c}_$l.log 2>&1
+    timeout -k 10 200 python bench.py --config $c --steps 10 --warmup 2 --no-cpu-baseline --no-extras > $out/bench_${c}_$l.log 2>&1
     rc=$?; echo "bench $c $l rc=$rc" >> $st
     [ $rc -ne 0 ] && exit $rc
   done
