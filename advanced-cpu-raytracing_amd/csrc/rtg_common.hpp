@@ -424,12 +424,13 @@ DEV uint64_t wave_min_key(uint64_t key, uint64_t em) {
 // C5 1471 -> 954 Mrays/s; profiles/r03l_*.  The lanes that reach a leaf early idle in the box
 // loop, and every lane pays the loop's exit bookkeeping per node.)
 // the per-lane walk's face test with selects (tri_test_sel) and the slab test's exact fallback
-// as a wave-uniform branch (1: k_primary 0.238 -> 0.228 ms, profiles/r03seq_ab.txt) or with
-// per-lane early outs and a divergent fallback (0)
+// as a wave-uniform branch (1: k_primary 0.238 -> 0.228 ms, C5 1488 -> 1584 Mrays/s,
+// profiles/r03seq_ab.txt) or with per-lane early outs and a divergent fallback (0).  Kernels
+// with the cooperative large-leaf walk keep 0 (C3-ton's k_shadow 0.711 -> 0.774 ms with 1)
 #ifndef RTG_SEQ_SEL
 #define RTG_SEQ_SEL 1
 #endif
-template <bool ANY, bool STATS>
+template <bool ANY, bool STATS, bool SEL = RTG_SEQ_SEL != 0>
 DEV bool walk_bvh_seq(const DevScene& S, int i, const int end, const Ray& r, float& minT, int& hitFace, float limit,
                       Cnt<STATS>& c) {
     bool hit = false;
@@ -439,7 +440,7 @@ DEV bool walk_bvh_seq(const DevScene& S, int i, const int end, const Ray& r, flo
         const float4 b = S.nodes[2 * i + 1];
         c.template node<ANY>();
         const int skip = __float_as_int(b.z);
-        if (box_hit_fast<RTG_SEQ_SEL != 0>(a.x, a.y, a.z, a.w, b.x, b.y, r, q, minT)) {
+        if (box_hit_fast<SEL>(a.x, a.y, a.z, a.w, b.x, b.y, r, q, minT)) {
             const int leaf = __float_as_int(b.w);
             if (leaf >= 0) {
                 int first = leaf >> 8, cnt = leaf & 255;
@@ -451,7 +452,7 @@ DEV bool walk_bvh_seq(const DevScene& S, int i, const int end, const Ray& r, flo
                 for (int f = first; f < first + cnt; ++f) {
                     c.template tri<ANY>();
                     float t;
-                    if (RTG_SEQ_SEL ? tri_test_sel(S.tris + 3 * f, r, minT, t) : tri_test_fast(S, f, r, minT, t)) {
+                    if (SEL ? tri_test_sel(S.tris + 3 * f, r, minT, t) : tri_test_fast(S, f, r, minT, t)) {
                         minT = t;
                         hitFace = f;
                         hit = true;
@@ -552,7 +553,7 @@ DEV bool walk_bvh(const DevScene& S, int i, const int end, const Ray& r, float& 
     if constexpr (!COOP) return walk_bvh_seq<ANY, STATS>(S, i, end, r, minT, hitFace, limit, c);
     // general kernels (the fused one) on scenes without large leaves: the plain walk, without
     // the wave-uniform loop and its per-step ballots (a uniform branch)
-    if (!S.coop) return walk_bvh_seq<ANY, STATS>(S, i, end, r, minT, hitFace, limit, c);
+    if (!S.coop) return walk_bvh_seq<ANY, STATS, false>(S, i, end, r, minT, hitFace, limit, c);
     bool hit = false;
     const RayRcp q = ray_rcp(r);
     bool active = i < end;
