@@ -16,12 +16,15 @@
 //     passes the triangle up to the rounding of Cramer's rule: the computed beta, gamma, t
 //     differ from the exact ones by ~ 5 u |A - o| / (sin(alpha) sin(theta)) in position
 //     (u = 2^-24, alpha the triangle's angle at v0, theta the ray's angle to its plane), and
-//     |A - o| <= `reach`.  The pad 2^-12 kappa reach (kappa = |E1||E2| / |E1 x E2| =
-//     1 / sin(alpha)) covers that for every ray more than 0.14 degrees off the face's plane;
+//     |A - o| <= `reach`.  The pad 2^p kappa reach (kappa = |E1||E2| / |E1 x E2| =
+//     1 / sin(alpha); p = pad_exp(), -16 as shipped) covers that for every ray with
+//     sin(theta) >= 5 u 2^-p = 5 * 2^-8, i.e. more than 1.1 degrees off the face's plane
+//     (2.2 degrees with a factor-2 margin on the estimate; p = -12 would give 0.07 / 0.14);
 //     a face with kappa > 64 (a sliver) keeps B_L as its cull box instead;
 // so the walk's answer equals the reference's up to rays that graze a face of a large leaf
-// within 0.14 degrees and are accepted by rounding alone (tested against the
-// reference walk, RTG_RENDER_EXACT_SHADOW, image for image).
+// within ~1-2 degrees and are accepted by rounding alone.  That is why the split tree is
+// opt-in (RTG_AHB=split) and the default tree keeps every reference leaf whole (DESIGN.md §2;
+// both tested against the reference walk, RTG_RENDER_EXACT_SHADOW, image for image).
 #include "rtg_ahb.hpp"
 
 #include <algorithm>

@@ -80,6 +80,19 @@ void f4(float* dst, const rtg_float3& v, float w = 0.f) { dst[0] = v.x; dst[1] =
 
 }  // namespace
 
+// Wavefront work buffers of one render context (rtg_scene::work).
+struct WaveWork {
+    size_t pixels = 0, tiles = 0;
+    int slots = 0;
+    void* mem = nullptr;
+    rtg::WaveBufs W{};
+};
+constexpr int kWorkCtx = 3;
+struct TileMap {
+    int tx, ty, mode;
+    DevBuf<int> map;
+};
+
 struct rtg_scene {
     int device = 0;
     rtg::DevScene ds;
@@ -121,18 +134,20 @@ struct rtg_scene {
     int feat = rtg::FEAT_ALL;         // scene feature bits (traversal specialisation)
     int num_slots = 0;                // lights per pixel (wavefront light slots)
     int shade_sk = rtg::SK_ALL;       // shading features (k_shade variant, rtg_common.hpp SK_*)
-    // wavefront buffers, grown on demand
-    size_t wave_pixels = 0, wave_tiles = 0;
-    int wave_slots = 0;
-    void* wave_mem = nullptr;
-    rtg::WaveBufs wave;
+    // wavefront buffers, grown on demand: work context 0 for every render, 1 and 2 for the
+    // row chunks of rtg_render's overlapped host path (two chunks in flight on two streams)
+    WaveWork work[kWorkCtx];
     // scratch for the host-buffer entry point
     float* d_hdr = nullptr;
     unsigned char* d_ldr = nullptr;
     size_t d_pixels = 0;
-    // block -> tile table for the last (tiles_x, tiles_y)
-    DevBuf<int> tile_map;
-    int tm_x = -1, tm_y = -1, tm_mode = -1;
+    // block -> tile tables, one per (tiles_x, tiles_y, mode) met (never re-uploaded: kernels of
+    // several streams may be reading them)
+    std::vector<std::unique_ptr<TileMap>> tile_maps;
+    // rtg_render's overlapped host path: the chunk streams and the copy stream
+    hipStream_t chunk_stream[2] = {nullptr, nullptr};
+    hipStream_t copy_stream = nullptr;
+    std::vector<hipEvent_t> chunk_ev;
     // RTG_RENDER_TIMING events (stage k runs between ev[k] and ev[k+1])
     hipEvent_t ev[rtg::MAX_STAGES + 1] = {};
     int timed_layout = -1;            // stage layout of the last timed render (rtg_kernels.hpp LAYOUT_*)
@@ -158,7 +173,13 @@ struct rtg_scene {
             if (e) (void)hipEventDestroy(e);
         if (d_hdr) (void)hipFree(d_hdr);
         if (d_ldr) (void)hipFree(d_ldr);
-        if (wave_mem) (void)hipFree(wave_mem);
+        for (auto& w : work)
+            if (w.mem) (void)hipFree(w.mem);
+        for (auto& c : chunk_stream)
+            if (c) (void)hipStreamDestroy(c);
+        if (copy_stream) (void)hipStreamDestroy(copy_stream);
+        for (auto& e : chunk_ev)
+            if (e) (void)hipEventDestroy(e);
     }
 };
 
@@ -1005,12 +1026,18 @@ static std::vector<int> build_tile_map(int tx, int ty, int mode) {
     return map;
 }
 
-static int ensure_tile_map(rtg_scene* s, int tx, int ty) {
+static int ensure_tile_map(rtg_scene* s, int tx, int ty, const int** out) {
     const int mode = tile_map_mode();
-    if (s->tm_x == tx && s->tm_y == ty && s->tm_mode == mode) return RTG_OK;
+    for (auto& m : s->tile_maps)
+        if (m->tx == tx && m->ty == ty && m->mode == mode) {
+            *out = m->map.p;
+            return RTG_OK;
+        }
     HIP_TRY(hipSetDevice(s->device));
-    HIP_TRY(s->tile_map.upload(build_tile_map(tx, ty, mode)));
-    s->tm_x = tx; s->tm_y = ty; s->tm_mode = mode;
+    std::unique_ptr<TileMap> m(new TileMap{tx, ty, mode, {}});
+    HIP_TRY(m->map.upload(build_tile_map(tx, ty, mode)));
+    *out = m->map.p;
+    s->tile_maps.push_back(std::move(m));
     return RTG_OK;
 }
 
@@ -1057,19 +1084,20 @@ static int prepare(rtg_scene* s, const rtg_render_opts* o, rtg::DevCamera& C, rt
     P.num_tiles = P.tiles_x * P.tiles_y;
     if (P.num_tiles == 0) return RTG_OK;   // nothing of this part in the row range
     P.seed = o->seed;
-    int rc = ensure_tile_map(s, P.tiles_x, P.tiles_y);
+    const int* map = nullptr;
+    int rc = ensure_tile_map(s, P.tiles_x, P.tiles_y, &map);
     if (rc) return rc;
-    P.tile_map = s->tile_map.p;
+    P.tile_map = map;
     return RTG_OK;
 }
 
 // Sizes the wavefront buffers for `pixels` pixels x `slots` light slots and `tiles`
 // shade blocks (queue segments of 256 * slots entries), one allocation.
-static int ensure_wave(rtg_scene* s, size_t pixels, int slots, size_t tiles) {
-    if (s->wave_mem && s->wave_pixels >= pixels && s->wave_slots >= slots && s->wave_tiles >= tiles) return RTG_OK;
-    if (s->wave_mem) { (void)hipFree(s->wave_mem); s->wave_mem = nullptr; }
-    pixels = std::max(pixels, s->wave_pixels);
-    tiles = std::max(tiles, s->wave_tiles);
+static int ensure_wave(WaveWork& ww, size_t pixels, int slots, size_t tiles) {
+    if (ww.mem && ww.pixels >= pixels && ww.slots >= slots && ww.tiles >= tiles) return RTG_OK;
+    if (ww.mem) { (void)hipFree(ww.mem); ww.mem = nullptr; }
+    pixels = std::max(pixels, ww.pixels);
+    tiles = std::max(tiles, ww.tiles);
     const size_t ns = pixels * (size_t)std::max(slots, 1);
     const size_t nq = tiles * 256 * (size_t)std::max(slots, 1);
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
@@ -1077,22 +1105,37 @@ static int ensure_wave(rtg_scene* s, size_t pixels, int slots, size_t tiles) {
     const size_t sz[12] = {pixels * 4, pixels * 4, pixels * 4, pixels * 16, ns * 16, ns, nq * 16, nq * 16, nq * 4,
                            tiles * 4, pixels * 16, slots <= 1 ? nq * 32 : 0};
     for (int k = 0; k < 12; ++k) { off[k] = total; total += al(sz[k]); }
-    HIP_TRY(hipMalloc(&s->wave_mem, total));
-    char* b = (char*)s->wave_mem;
-    rtg::WaveBufs& W = s->wave;
+    HIP_TRY(hipMalloc(&ww.mem, total));
+    char* b = (char*)ww.mem;
+    rtg::WaveBufs& W = ww.W;
     W.hit_t = (float*)(b + off[0]); W.hit_obj = (int*)(b + off[1]); W.hit_face = (int*)(b + off[2]);
     W.base = (float4*)(b + off[3]); W.term = (float4*)(b + off[4]); W.occ = (unsigned char*)(b + off[5]);
     W.q_o = (float4*)(b + off[6]); W.q_d = (float4*)(b + off[7]); W.q_slot = (int*)(b + off[8]);
     W.q_count = (int*)(b + off[9]); W.accum = (float4*)(b + off[10]);
     W.q_pay = slots <= 1 ? (float4*)(b + off[11]) : nullptr;
-    s->wave_pixels = pixels;
-    s->wave_slots = slots;
-    s->wave_tiles = tiles;
+    ww.pixels = pixels;
+    ww.slots = slots;
+    ww.tiles = tiles;
     return RTG_OK;
 }
 
+// The render pipeline a frame part takes (launch): path tracer, ray trees, wavefront, fused.
+enum { PIPE_PATH, PIPE_TREE, PIPE_WAVE, PIPE_MEGA };
+static int pipeline(const rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& C, const rtg::RenderParams& P) {
+    if (C.path_tracing && s->path_ok && !(o->flags & RTG_RENDER_FUSED) && (o->flags & RTG_RENDER_TREE)) return PIPE_PATH;
+    const long long work = (long long)P.part_rows * C.width * P.sample_count;
+    const bool fused_only = (o->flags & RTG_RENDER_FUSED) || C.path_tracing;
+    if (s->tree_ok && !fused_only && ((o->flags & RTG_RENDER_TREE) || work >= (1ll << 21))) return PIPE_TREE;
+    if (s->wave_ok && !fused_only) return PIPE_WAVE;
+    return PIPE_MEGA;
+}
+
+// ctx: the wavefront work context (rtg_scene::work); pipe >= 0 forces the pipeline chosen
+// for the whole frame (row chunks of one frame must not fall below the ray-tree threshold)
 static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& C, const rtg::RenderParams& P,
-                  float* d_hdr, uint8_t* d_ldr, float* d_accum, hipStream_t stream) {
+                  float* d_hdr, uint8_t* d_ldr, float* d_accum, hipStream_t stream, int ctx = 0, int pipe = -1) {
+    WaveWork& ww = s->work[ctx];
+    if (pipe < 0) pipe = pipeline(s, o, C, P);
     const bool stats = (o->flags & RTG_RENDER_COUNT_STATS) != 0;
     // RTG_RENDER_EXACT_SHADOW: shadow rays walk the reference BVH (cross-checks of the wide one)
     rtg::DevScene ds = s->ds;
@@ -1105,17 +1148,23 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
         ev = s->ev;
     }
     // ray trees: the wavefront tree pipeline for large frames (it synchronises once per tree
-    // level), the fused kernel otherwise; RTG_RENDER_TREE / RTG_RENDER_FUSED force either
-    const long long work = (long long)P.part_rows * C.width * P.sample_count;
-    // path tracing: the fused kernel; the wavefront path tracer (rtg_path.hip, same image bit
+    // level), the fused kernel otherwise; RTG_RENDER_TREE / RTG_RENDER_FUSED force either.
+    // Path tracing: the fused kernel; the wavefront path tracer (rtg_path.hip, same image bit
     // for bit) with RTG_RENDER_TREE -- measured slower than the fused kernel on the path-tracing
     // fixtures, so it is opt-in
-    if (C.path_tracing && s->path_ok && !(o->flags & RTG_RENDER_FUSED) && (o->flags & RTG_RENDER_TREE)) {
+    if (pipe == PIPE_PATH) {
         float4* acc = (float4*)d_accum;
         if (!P.accum_only && C.spp > 1) {   // internal accumulator indexed by absolute pixel
-            int rc = ensure_wave(s, (size_t)C.width * C.height, s->num_slots, (size_t)P.num_tiles);
+            int rc = ensure_wave(ww, (size_t)C.width * C.height, s->num_slots, (size_t)P.num_tiles);
             if (rc) return rc;
-            acc = s->wave.accum;
+            acc = ww.W.accum;
+        }
+        // a counted render that falls back to the fused kernel must not keep the abandoned
+        // pass's counts: snapshot the counters, restore them before the fused kernel runs
+        rtg::DevCounters snap{};
+        if (stats) {
+            HIP_TRY(hipMemcpyAsync(&snap, s->counters.p, sizeof(snap), hipMemcpyDeviceToHost, stream));
+            HIP_TRY(hipStreamSynchronize(stream));
         }
         const hipError_t pe = rtg::launch_path(s->path, ds, C, P, d_hdr, d_ldr, acc, s->counters.p, stats, s->feat,
                                                s->shade_sk, stream, ev);
@@ -1125,35 +1174,37 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
         }
         if (pe != hipErrorNotSupported) HIP_TRY(pe);
         (void)hipGetLastError();
+        if (stats) {
+            HIP_TRY(hipMemcpyAsync(s->counters.p, &snap, sizeof(snap), hipMemcpyHostToDevice, stream));
+            HIP_TRY(hipStreamSynchronize(stream));
+        }
+        pipe = PIPE_MEGA;                   // path-tracing cameras: the fused kernel
     }
-    const bool fused_only = (o->flags & RTG_RENDER_FUSED) || C.path_tracing;
-    const bool use_tree = s->tree_ok && !fused_only &&
-                          ((o->flags & RTG_RENDER_TREE) || work >= (1ll << 21));
-    if (use_tree) {
+    if (pipe == PIPE_TREE) {
         float4* acc = (float4*)d_accum;
         if (!P.accum_only && C.spp > 1) {   // internal accumulator indexed by absolute pixel
-            int rc = ensure_wave(s, (size_t)C.width * C.height, s->num_slots, (size_t)P.num_tiles);
+            int rc = ensure_wave(ww, (size_t)C.width * C.height, s->num_slots, (size_t)P.num_tiles);
             if (rc) return rc;
-            acc = s->wave.accum;
+            acc = ww.W.accum;
         }
         HIP_TRY(rtg::launch_tree(s->tree, ds, C, P, d_hdr, d_ldr, acc, s->counters.p, stats, s->feat, s->shade_sk,
                                  stream, ev));
         if (ev) s->timed_layout = rtg::LAYOUT_TREE;
         return RTG_OK;
     }
-    if (s->wave_ok && !fused_only) {
+    if (pipe == PIPE_WAVE) {
         const size_t rows = (size_t)P.part_rows;
-        int rc = ensure_wave(s, rows * C.width, s->num_slots, (size_t)P.num_tiles);
+        int rc = ensure_wave(ww, rows * C.width, s->num_slots, (size_t)P.num_tiles);
         if (rc) return rc;
-        rtg::WaveBufs W = s->wave;
+        rtg::WaveBufs W = ww.W;
         W.num_slots = s->num_slots;
         if (P.accum_only) W.accum = (float4*)d_accum;
         else if (C.spp > 1) {   // internal accumulator indexed by absolute pixel
             size_t need = (size_t)C.width * C.height;
-            if (need > s->wave_pixels) {
-                int rc2 = ensure_wave(s, need, s->num_slots, (size_t)P.num_tiles);
+            if (need > ww.pixels) {
+                int rc2 = ensure_wave(ww, need, s->num_slots, (size_t)P.num_tiles);
                 if (rc2) return rc2;
-                W = s->wave;
+                W = ww.W;
                 W.num_slots = s->num_slots;
             }
         }
@@ -1212,10 +1263,69 @@ int rtg_copy_part_to_host(rtg_scene* s, const rtg_render_opts* o, const float* d
     return copy_part(o, c.width, c.height, d_hdr, d_ldr, hdr_rgb, ldr_rgb, (hipStream_t)stream);
 }
 
+// The overlapped host path of rtg_render (one device, frames of >= kChunkMinPixels): the
+// frame part is rendered in row chunks, alternately on two streams with their own work
+// buffers (rtg_scene::work 1 and 2), and each chunk's rows are copied to the host on a third
+// stream as soon as the chunk is done -- the D2H copy of chunk j runs under the rendering of
+// chunks j+1.., so only the last chunk's copy adds to the frame.  A chunk is a run of whole
+// rounds of the partition's bands (8 x part_count rows per round): part p's bands inside a
+// chunk starting at round m are the bands of part (p - m) mod part_count of that chunk (the
+// rotation of part_band), so the chunks together cover exactly part p's rows.  Pixels are
+// keyed by their image position (RNG included): the image is the one-launch image bit for bit.
+constexpr int kChunks = 8;
+constexpr long long kChunkMinPixels = 1ll << 20;
+static bool chunk_disabled() { return std::getenv("RTG_HOST_CHUNKS_OFF") != nullptr; }
+
+static int render_chunked(rtg_scene* s, const rtg_render_opts* o, const rtg::RenderParams& P0, int pipe, int width,
+                          float* hdr_rgb, uint8_t* ldr_rgb) {
+    const int N = P0.part_count, per_round = RTG_PART_BAND_ROWS * N;
+    const int rounds = (P0.row_end - P0.row_begin + per_round - 1) / per_round;
+    int cr = (rounds + kChunks - 1) / kChunks;
+    cr += cr & 1;                                    // even: a chunk's compact rows fill whole 16-row tiles
+    for (auto& c : s->chunk_stream)
+        if (!c) HIP_TRY(hipStreamCreateWithFlags(&c, hipStreamNonBlocking));
+    if (!s->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&s->copy_stream, hipStreamNonBlocking));
+    const int nc = (rounds + cr - 1) / cr;
+    while ((int)s->chunk_ev.size() < nc) {
+        hipEvent_t e;
+        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+        s->chunk_ev.push_back(e);
+    }
+    // the chunks start after whatever the scene's stream holds
+    HIP_TRY(hipEventRecord(s->done, s->stream));
+    for (auto& c : s->chunk_stream) HIP_TRY(hipStreamWaitEvent(c, s->done, 0));
+    for (int j = 0; j < nc; ++j) {
+        const int m0 = j * cr;
+        rtg_render_opts oj = *o;
+        oj.row_begin = P0.row_begin + m0 * per_round;
+        oj.row_end = std::min(P0.row_end, P0.row_begin + (m0 + cr) * per_round);
+        oj.part_count = N;
+        oj.part_index = ((P0.part_index - m0) % N + N) % N;
+        rtg::DevCamera C;
+        rtg::RenderParams P;
+        int rc = prepare(s, &oj, C, P);
+        if (rc) return rc;
+        if (P.num_tiles == 0) continue;
+        hipStream_t st = s->chunk_stream[j & 1];
+        rc = launch(s, &oj, C, P, s->d_hdr, s->d_ldr, nullptr, st, 1 + (j & 1), pipe);
+        if (rc) return rc;
+        HIP_TRY(hipEventRecord(s->chunk_ev[j], st));
+        HIP_TRY(hipStreamWaitEvent(s->copy_stream, s->chunk_ev[j], 0));
+        rc = copy_part(&oj, width, C.height, s->d_hdr, s->d_ldr, hdr_rgb, ldr_rgb, s->copy_stream);
+        if (rc) return rc;
+    }
+    // the scene's stream (rtg_render_device callers, the next rtg_render) follows the copies
+    HIP_TRY(hipEventRecord(s->done, s->copy_stream));
+    HIP_TRY(hipStreamWaitEvent(s->stream, s->done, 0));
+    HIP_TRY(hipStreamSynchronize(s->copy_stream));
+    return RTG_OK;
+}
+
 // Replaces main.cpp:164-185.  With replicas (rtg_scene_create_multi) replica i renders part
 // i of n on its own stream and copies its rows into the caller's buffers; the renders of all
 // replicas are enqueued before any copy (a copy to pageable memory may block the host), then
-// every stream is synchronised -- never the whole device.
+// every stream is synchronised -- never the whole device.  One device: frames of a million
+// pixels or more take the overlapped chunked path above (render_chunked).
 int rtg_render(rtg_scene* s, const rtg_render_opts* o, float* hdr_rgb, uint8_t* ldr_rgb) {
     if (!s || !o) return set_err(RTG_ERR_INVALID, "null argument");
     if (o->flags & RTG_RENDER_ACCUM_ONLY) return set_err(RTG_ERR_INVALID, "use rtg_render_device for RTG_RENDER_ACCUM_ONLY");
@@ -1228,6 +1338,28 @@ int rtg_render(rtg_scene* s, const rtg_render_opts* o, float* hdr_rgb, uint8_t* 
     const rtg_camera& cam = s->cameras[o->camera];
     std::vector<rtg_render_opts> ro(n, *o);
     bool whole = false;
+    if (n == 1 && !chunk_disabled() && !(o->flags & (RTG_RENDER_TIMING | RTG_RENDER_COUNT_STATS)) &&
+        (long long)cam.width * cam.height >= kChunkMinPixels && !(cam.has_tonemapper)) {
+        rtg::DevCamera C;
+        rtg::RenderParams P;
+        int rc = prepare(s, o, C, P);
+        if (rc) return rc;
+        const int pipe = pipeline(s, o, C, P);
+        if (P.num_tiles > 0 && (pipe == PIPE_WAVE || pipe == PIPE_MEGA)) {
+            HIP_TRY(hipSetDevice(s->device));
+            const size_t pixels = (size_t)C.width * C.height;
+            if (s->d_pixels < pixels) {
+                HIP_TRY(hipStreamSynchronize(s->stream));
+                if (s->d_hdr) { (void)hipFree(s->d_hdr); s->d_hdr = nullptr; }
+                if (s->d_ldr) { (void)hipFree(s->d_ldr); s->d_ldr = nullptr; }
+                s->d_pixels = 0;
+                HIP_TRY(hipMalloc(&s->d_hdr, pixels * 3 * sizeof(float)));
+                HIP_TRY(hipMalloc(&s->d_ldr, pixels * 3));
+                s->d_pixels = pixels;
+            }
+            return render_chunked(s, o, P, pipe, C.width, hdr_rgb, ldr_rgb);
+        }
+    }
     for (int i = 0; i < n; ++i) {
         rtg_scene* r = reps[i];
         if (n > 1) { ro[i].part_index = i; ro[i].part_count = n; }

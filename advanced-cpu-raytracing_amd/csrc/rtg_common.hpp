@@ -211,9 +211,10 @@ DEV RayRcp ray_rcp(const Ray& r) {
     return q;
 }
 // UNI: the exact fallback as a wave-uniform branch (wave packets: every lane tests the same box)
+// `on` (UNI only): lanes whose result is used -- the others do not vote for the fallback
 template <bool UNI = false>
 DEV bool box_hit_fast(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, const Ray& r,
-                      const RayRcp& q, float minT) {
+                      const RayRcp& q, float minT, bool on = true) {
     // branch-free: every condition is evaluated (bitwise &, no short circuit), so the
     // common path is straight-line code with one rarely taken branch to the exact test
     const float tx1 = (mnx - r.o.x) * q.ix, tx2 = (mxx - r.o.x) * q.ix;
@@ -229,8 +230,8 @@ DEV bool box_hit_fast(float mnx, float mny, float mnz, float mxx, float mxy, flo
                       ((minT == INFINITY) | (fabsf(tmin - minT) > 0x1p-20f * atmin + 1e-30f));
     bool hit = (tmax > 0) & (tmax >= tmin) & (tmin < minT);
     if constexpr (UNI) {
-        if (__builtin_expect(__ballot(!sure) != 0, 0)) {
-            if (!sure) hit = box_hit(mnx, mny, mnz, mxx, mxy, mxz, r, minT);
+        if (__builtin_expect(__ballot(on & !sure) != 0, 0)) {
+            if (on & !sure) hit = box_hit(mnx, mny, mnz, mxx, mxy, mxz, r, minT);
         }
         return hit;
     }
@@ -352,7 +353,8 @@ DEV bool tri_test_fast_rec(const float4* R, const Ray& r, float minT, float& tou
 // per-lane walk under RTG_SEQ_SEL): the same decisions -- the early outs become lane masks,
 // and the two costly parts (the t division, the exact fallback) wave-uniform branches taken
 // when some lane needs them.
-DEV bool tri_test_sel(const float4* R, const Ray& r, float limit, float& tout) {
+// `on`: lanes whose result is used (the others neither take the division nor the fallback)
+DEV bool tri_test_sel(const float4* R, const Ray& r, float limit, float& tout, bool on = true) {
     const float4 A = R[0], E1 = R[1], E2 = R[2];
     const float dx = r.d.x, dy = r.d.y, dz = r.d.z;
     const float detA = det3(E1.x, E2.x, dx, E1.y, E2.y, dy, E1.z, E2.z, dz);
@@ -371,8 +373,8 @@ DEV bool tri_test_sel(const float4* R, const Ray& r, float limit, float& tout) {
     const bool b_out = range & bsure & (beta < 0);
     const bool g_out = range & bsure & !(beta < 0) & gsure & (gama < 0);
     const bool s_ok = range & bsure & !(beta < 0) & gsure & !(gama < 0) & ssure;
-    const bool no = zero | b_out | g_out | (s_ok & (sum > 1));
-    const bool tt = !zero & s_ok & !(sum > 1);
+    const bool no = zero | b_out | g_out | (s_ok & (sum > 1)) | !on;
+    const bool tt = on & !zero & s_ok & !(sum > 1);
     bool hit = false;
     if (__ballot(tt)) {
         const float t = det3(E1.x, E2.x, sx, E1.y, E2.y, sy, E1.z, E2.z, sz) / detA;
@@ -384,6 +386,32 @@ DEV bool tri_test_sel(const float4* R, const Ray& r, float limit, float& tout) {
         if (unsure) hit = tri_test_rec(R, r, limit, tout);
     }
     return hit;
+}
+
+// Wave-uniform records through the scalar cache (the compiler keeps vector loads here: the
+// kernels store to global memory, so it cannot prove the records unclobbered).  Read-only
+// scene data, written by copies before the launch.
+typedef int rtg_s16 __attribute__((ext_vector_type(16)));
+typedef int rtg_s8 __attribute__((ext_vector_type(8)));
+typedef int rtg_s4 __attribute__((ext_vector_type(4)));
+DEV const void* uniform_ptr(const void* p) {
+    const uint64_t v = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return (const void*)(((uint64_t)hi << 32) | lo);
+}
+DEV void sload_wnode(const WNode* p, rtg_s16& a, rtg_s16& b) {   // 128 B
+    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(a), "=&s"(b) : "s"(uniform_ptr(p)) : "memory");
+}
+DEV void sload_rec(const float4* p, rtg_s8& a, rtg_s4& b) {      // 48 B: a face record
+    asm volatile("s_load_dwordx8 %0, %2, 0x0\n\ts_load_dwordx4 %1, %2, 0x20\n\ts_waitcnt lgkmcnt(0)"
+                 : "=&s"(a), "=&s"(b) : "s"(uniform_ptr(p)) : "memory");
+}
+DEV void sload_node(const float4* p, rtg_s8& a) {                // 32 B: a reference BVH node
+    asm volatile("s_load_dwordx8 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=&s"(a) : "s"(uniform_ptr(p)) : "memory");
+}
+DEV float4 f4(int x, int y, int z, int w) {
+    return make_float4(__int_as_float(x), __int_as_float(y), __int_as_float(z), __int_as_float(w));
 }
 
 // 64-bit lexicographic (t, face) key of a candidate hit; t > 0, so the float bits order
@@ -639,7 +667,13 @@ DEV int wave_min_int(int v) {
     return v;
 }
 
-template <bool ANY, bool STATS>
+// SC (RTG_PRIMARY_PACKET 2): the round-3 machinery of the any-hit packet walk -- the 32-B node
+// and 48-B face records through the scalar cache (inline s_load: one load per wave), the face
+// test with selects (tri_test_sel: early outs as lane masks, the t division and the exact
+// fallback as wave-uniform branches) and the slab test's exact fallback as a wave-uniform
+// branch; lanes outside their own walk take no part in either fallback.  SC = false: round 2's
+// form (vector loads of the uniform address, per-lane face tests).
+template <bool ANY, bool STATS, bool SC = false>
 DEV bool walk_bvh_packet(const DevScene& S, const int begin, const int end, const Ray& r, float& minT, int& hitFace,
                          float limit, Cnt<STATS>& c) {
     bool hit = false;
@@ -649,7 +683,7 @@ DEV bool walk_bvh_packet(const DevScene& S, const int begin, const int end, cons
     int i = begin;                                   // wave-uniform
     while (i < end) {
         bool act = resume <= i;
-        if (!__ballot(act)) {                        // only after ANY lanes finished
+        if (ANY && !__ballot(act)) {                 // only after ANY lanes finished
             const int all = __ballot(1) == ~0ull ? wave_min_int(resume) : [&] {
                 int m = kDone;
                 uint64_t em = __ballot(1);
@@ -665,15 +699,30 @@ DEV bool walk_bvh_packet(const DevScene& S, const int begin, const int end, cons
             continue;
         }
         i = __builtin_amdgcn_readfirstlane(i);
-        const float4 a = S.nodes[2 * i];
-        const float4 b = S.nodes[2 * i + 1];
+        float4 a, b;
+        if constexpr (SC) {
+            rtg_s8 nd;
+            sload_node(S.nodes + 2 * i, nd);
+            a = f4(nd[0], nd[1], nd[2], nd[3]);
+            b = f4(nd[4], nd[5], nd[6], nd[7]);
+        } else {
+            a = S.nodes[2 * i];
+            b = S.nodes[2 * i + 1];
+        }
         const int skip = __float_as_int(b.z);
         const int leaf = __float_as_int(b.w);
-        bool pass = false;
-        if (act) {
-            c.template node<ANY>();
-            pass = box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, r, q, minT);
-            if (!pass) resume = skip;
+        bool pass;
+        if constexpr (SC) {
+            if (act) c.template node<ANY>();
+            pass = act & box_hit_fast<true>(a.x, a.y, a.z, a.w, b.x, b.y, r, q, minT, act);
+            resume = (act & !pass) ? skip : resume;
+        } else {
+            pass = false;
+            if (act) {
+                c.template node<ANY>();
+                pass = box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, r, q, minT);
+                if (!pass) resume = skip;
+            }
         }
         const bool any = __ballot(pass) != 0;
         if (leaf >= 0) {
@@ -681,11 +730,28 @@ DEV bool walk_bvh_packet(const DevScene& S, const int begin, const int end, cons
                 int first = leaf >> 8, cnt = leaf & 255;
                 if (leaf == LEAF_EXT) {
                     const int2 e = S.node_ext[i];
-                    first = e.x;
-                    cnt = e.y;
+                    first = __builtin_amdgcn_readfirstlane(e.x);
+                    cnt = __builtin_amdgcn_readfirstlane(e.y);
                 }
                 for (int f = first; f < first + cnt; ++f) {
-                    if (pass) {
+                    if constexpr (SC) {
+                        rtg_s8 ra;
+                        rtg_s4 rb;
+                        sload_rec(S.tris + 3 * (size_t)f, ra, rb);
+                        const float4 R[3] = {f4(ra[0], ra[1], ra[2], ra[3]), f4(ra[4], ra[5], ra[6], ra[7]),
+                                             f4(rb[0], rb[1], rb[2], rb[3])};
+                        if (pass) c.template tri<ANY>();
+                        float t;
+                        const bool ok = pass & tri_test_sel(R, r, minT, t, pass);
+                        minT = ok ? t : minT;
+                        hitFace = ok ? f : hitFace;
+                        hit |= ok;
+                        if (ANY) {
+                            const bool fin = ok & (t < limit);
+                            pass &= !fin;
+                            resume = fin ? kDone : resume;
+                        }
+                    } else if (pass) {
                         c.template tri<ANY>();
                         float t;
                         if (tri_test_fast(S, f, r, minT, t)) {
@@ -817,7 +883,9 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
         int face = -1;
         float t = h.t;
         bool found;
-        if constexpr (PK) found = walk_bvh_packet<ANY, STATS>(S, ob.node_begin, ob.node_end, lr, t, face, limit, c);
+        if constexpr (PK)
+            found = walk_bvh_packet<ANY, STATS, RTG_PRIMARY_PACKET == 2>(S, ob.node_begin, ob.node_end, lr, t, face,
+                                                                           limit, c);
         else found = walk_bvh<ANY, STATS, (FEAT & FEAT_BIGLEAF) != 0>(S, ob.node_begin, ob.node_end, lr, t, face, limit, c);
         if (found) {
             h.t = t; h.obj = k; h.face = face; h.o = r.o;
@@ -984,31 +1052,6 @@ DEV int walk_wide_any(const DevScene& S, int node, const Ray& lr, float minT0, f
 #ifndef RTG_PK_MAX_STEPS
 #define RTG_PK_MAX_STEPS 4096
 #endif
-// Wave-uniform records through the scalar cache (the compiler keeps vector loads here: the
-// kernels store to global memory, so it cannot prove the records unclobbered).  Read-only
-// scene data, written by copies before the launch.
-typedef int rtg_s16 __attribute__((ext_vector_type(16)));
-typedef int rtg_s8 __attribute__((ext_vector_type(8)));
-typedef int rtg_s4 __attribute__((ext_vector_type(4)));
-DEV const void* uniform_ptr(const void* p) {
-    const uint64_t v = (uint64_t)p;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v), hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
-    return (const void*)(((uint64_t)hi << 32) | lo);
-}
-DEV void sload_wnode(const WNode* p, rtg_s16& a, rtg_s16& b) {   // 128 B
-    asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
-                 : "=&s"(a), "=&s"(b) : "s"(uniform_ptr(p)) : "memory");
-}
-DEV void sload_rec(const float4* p, rtg_s8& a, rtg_s4& b) {      // 48 B: a face record
-    asm volatile("s_load_dwordx8 %0, %2, 0x0\n\ts_load_dwordx4 %1, %2, 0x20\n\ts_waitcnt lgkmcnt(0)"
-                 : "=&s"(a), "=&s"(b) : "s"(uniform_ptr(p)) : "memory");
-}
-DEV void sload_node(const float4* p, rtg_s8& a) {                // 32 B: a reference BVH node
-    asm volatile("s_load_dwordx8 %0, %1, 0x0\n\ts_waitcnt lgkmcnt(0)" : "=&s"(a) : "s"(uniform_ptr(p)) : "memory");
-}
-DEV float4 f4(int x, int y, int z, int w) {
-    return make_float4(__int_as_float(x), __int_as_float(y), __int_as_float(z), __int_as_float(w));
-}
 template <bool STATS>
 DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0, float limit, bool inst_conf,
                          Cnt<STATS>& c) {

@@ -189,8 +189,9 @@ struct DevCamera {
     int path_tracing, next_event, importance_sampling, russian_roulette;   // RendererParams (rendererParams.h)
 };
 
-// Image partition (multi-GPU): the rows [row_begin, row_end) are cut into 16-row bands
-// (the tile height), band b counted from row_begin belongs to part b % part_count.  A
+// Image partition (multi-GPU): the rows [row_begin, row_end) are cut into 8-row bands (one
+// wave's 8x8 pixel block), dealt round-robin with the order rotated one slot per round: the
+// k-th band of part p of N is band k*N + ((p - k) mod N) (rtg_part_runs).  A
 // render covers its part's rows only; they are numbered densely ("compact rows", 0 ..
 // part_rows-1) for the per-pixel work buffers, and part_row() maps them back to image rows.
 struct RenderParams {

@@ -8,6 +8,14 @@
 namespace rtg {
 
 int max_supported_depth();
+// FNV-1a of a camera's device record (view, image size, samples, renderer flags): the ray-tree and
+// path plans are kept per frame part of one camera
+inline unsigned long long camera_hash(const DevCamera& C) {
+    const unsigned char* p = reinterpret_cast<const unsigned char*>(&C);
+    unsigned long long h = 1469598103934665603ull;
+    for (size_t i = 0; i < sizeof(DevCamera); ++i) h = (h ^ p[i]) * 1099511628211ull;
+    return h;
+}
 // fused kernel (rtg_mega.hip): any scene
 // `ev` (nullable): events recorded around every kernel of the last sample pass
 // sk / feat: the scene's shading / traversal features (path-tracing variants, rtg_mega_pt.hip)

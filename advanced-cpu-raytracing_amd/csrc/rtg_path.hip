@@ -323,7 +323,13 @@ static hipError_t ensure_paths(PathState& T, size_t n, int levels) {
     levels = std::max(levels, T.levels);
     T.release();
     hipError_t e;
-#define A_(ptr, bytes) if ((e = hipMalloc(&ptr, bytes)) != hipSuccess) return e
+    // an allocation that fails leaves the render to the fused kernel (hipErrorNotSupported)
+#define A_(ptr, bytes)                                  \
+    if ((e = hipMalloc(&ptr, bytes)) != hipSuccess) {   \
+        (void)hipGetLastError();                        \
+        T.release();                                    \
+        return hipErrorNotSupported;                    \
+    }
     A_(T.B.ro, n * 16); A_(T.B.rd, n * 16); A_(T.B.key, n * 8); A_(T.B.tp, n * 16);
     A_(T.B.frames, n * (size_t)levels * kFrameChunks * 16);
     A_(T.B.act0, n * 4); A_(T.B.act1, n * 4); A_(T.B.cnt, (kPathMaxIter + 2) * sizeof(int));
@@ -397,11 +403,21 @@ static hipError_t path_run(PathState& T, const PathKernels& K, bool stats, const
     hipError_t e;
     if (!T.h && (e = hipHostMalloc(&T.h, 2 * sizeof(int))) != hipSuccess) return e;
     const int npix = P.part_rows * C.width;
-    // paths per pass: up to 2^20 (the frame stacks: 208 B x maxd levels per path)
-    const int chunk = std::min(npix, 1 << 20);
+    // paths per pass: up to 2^20, and at most half the device memory free now (the frame stacks:
+    // 208 B x maxd levels per path -- 6.9 GB at 2^20 paths x 32 levels)
+    const size_t per_path = (size_t)maxd * kFrameChunks * 16 + 96;
+    size_t mem_free = 0, mem_total = 0;
+    if (hipMemGetInfo(&mem_free, &mem_total) != hipSuccess) {
+        (void)hipGetLastError();
+        mem_free = (size_t)1 << 40;
+    }
+    mem_free += T.cap * (size_t)T.levels * kFrameChunks * 16;        // the buffers held now are reusable
+    const long long budget = std::max<long long>(1 << 16, (long long)(mem_free / 2 / per_path));
+    const int chunk = (int)std::min<long long>(std::min(npix, 1 << 20), budget);
     if ((e = ensure_paths(T, (size_t)chunk, maxd)) != hipSuccess) return e;
     const std::vector<long long> key = {P.row_begin, P.row_end, P.part_index, P.part_count, C.width, C.height,
-                                        (long long)(size_t)S.objects, S.max_depth, (long long)chunk, maxd};
+                                        (long long)(size_t)S.objects, S.max_depth, (long long)chunk, maxd,
+                                        (long long)camera_hash(C)};
     for (int attempt = 0; attempt < 2; ++attempt) {
         // attempt 0: planned passes when this frame part has a plan (the first pass otherwise
         // host-driven, planning the rest); attempt 1 (a plan was too short): host-driven.

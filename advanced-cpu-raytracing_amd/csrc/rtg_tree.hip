@@ -669,8 +669,10 @@ static hipError_t tree_run(TreeState& T, const DevScene& S, const DevCamera& C, 
         if ((e = hipMalloc(&T.d_counts, (kMaxLevels + 1) * sizeof(int))) != hipSuccess) return e;
     }
     const int ns = S.num_point + S.num_area + S.num_env + S.num_dir + S.num_spot + S.num_mesh;
+    // the plan belongs to one frame part of one camera (its view and samples decide the level
+    // sizes): two cameras of a scene at the same size keep apart
     const std::vector<long long> key = {P.row_begin, P.row_end, P.part_index, P.part_count, C.width, C.height,
-                                        (long long)(size_t)S.objects, S.max_depth};
+                                        (long long)(size_t)S.objects, S.max_depth, (long long)camera_hash(C)};
     auto prepare = [&]() -> hipError_t {
         // capacities and block segments of the plan; the overflow flag cleared
         hipError_t r;
@@ -696,7 +698,9 @@ static hipError_t tree_run(TreeState& T, const DevScene& S, const DevCamera& C, 
         // attempt 0: planned passes when this frame part has a plan, else the first pass
         // host-driven and the rest planned from it; attempt 1 (a level outgrew the plan):
         // every pass host-driven, re-planning
-        const bool adapt = attempt == 0 && !tree_sync_only();
+        // (counted renders stay host-driven: a planned render that overflows would be redone and
+        // its discarded pass counted twice)
+        const bool adapt = attempt == 0 && !tree_sync_only() && !STATS;
         bool planned = adapt && T.plan_key == key && !T.plan.empty();
         bool any_async = false;
         if (planned && (e = prepare()) != hipSuccess) return e;

@@ -136,10 +136,20 @@ class SharedFrame:
 
 
 def render_part(ds, rank: int, world: int, d_hdr: int, d_ldr: int, stream: int, frame: SharedFrame | None = None,
-                camera: int = 0, seed: int = 0x5EED, flags: int = 0):
-    """Rank ``rank``'s share of one frame: render part rank/world into its device buffers
-    (full-frame sized; only its rows are written) and, with a ``frame``, enqueue the DMA of
-    those rows into the shared host framebuffer.  Asynchronous on ``stream``."""
+                camera: int = 0, seed: int = 0x5EED, flags: int = 0, overlap: bool = True):
+    """Rank ``rank``'s share of one frame.
+
+    With a ``frame`` and ``overlap`` (the default): rtg_render of part rank/world straight into
+    the shared host framebuffer -- for frames of a million pixels or more the library renders
+    the part in row chunks on two streams and DMAs each chunk's rows while the next chunks
+    render (rtg_api.cpp render_chunked), so only the last chunk's copy adds to the frame time.
+    Synchronous; the device buffers are not written.
+    Otherwise: render the part into its device buffers (full-frame sized; only its rows are
+    written) and, with a ``frame``, enqueue the DMA of those rows into the shared host
+    framebuffer after it.  Asynchronous on ``stream``."""
+    if frame is not None and overlap:
+        ds.render(camera, flags=flags, seed=seed, part=(rank, world), out=(frame.hdr, frame.ldr))
+        return
     ds.render_device(d_hdr, d_ldr, stream, camera=camera, seed=seed, flags=flags, part=(rank, world))
     if frame is not None:
         ds.copy_part_to_host(d_hdr if frame.hdr is not None else 0, d_ldr if frame.ldr is not None else 0,

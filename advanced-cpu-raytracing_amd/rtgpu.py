@@ -203,7 +203,7 @@ class HostScene:
         _check(lib().rtg_desc_counts(self.desc, *[ctypes.byref(x) for x in v]))
         return dict(zip(("objects", "faces", "nodes", "lights"), (x.value for x in v)))
 
-    def anyhit_check(self, mode: int = 2) -> dict:
+    def anyhit_check(self, mode: int = 1) -> dict:
         """Host-only build + structural check of the shadow rays' any-hit trees
         (rtg_desc_anyhit_check; mode 0 reference collapse, 1 SAH over leaves (default), 2 split)."""
         out = (ctypes.c_int64 * 8)()

@@ -200,6 +200,7 @@ def measure(render, torch, steps, warmup, barrier, serial=None):
     t0 = time.perf_counter()
     for k in range(steps):
         render(k)
+    measure.issue_s = time.perf_counter() - t0    # host time to issue the steps (launch-bound if ~elapsed)
     torch.cuda.synchronize()
     barrier()
     elapsed = time.perf_counter() - t0
@@ -239,12 +240,16 @@ def kernel_bytes(st, W, H):
             "tree_levels": ext + shd, "frame": ext + shd + 15 * W * H}
 
 
-def pmc_summary(kernel, K, world):
+def pmc_summary(kernel, K, world, share=1.0):
     """Counter-measured bytes per launch of `kernel` for the K-triangle headline scene from
     the newest committed summary (profiles/r*_pmc*.json, tools/pmc_summary.py over separate
     rocprofv3 --pmc passes of this bench, tools/pmc_kernels.py): HBM traffic = 2 x FETCH_SIZE +
     WRITE_SIZE (gfx950 correction, MI355X_MICROARCH.md), L2 hit rate from TCC_HIT / TCC_MISS,
-    L2 requests, vL1D hit rate, SQ instruction counts and wave-cycle split.  None if absent."""
+    L2 requests, vL1D hit rate, SQ instruction counts and wave-cycle split.  None if absent.
+
+    N > 1 (no committed profile of a 1/N part): the N = 1 counters with every extensive count
+    (instructions, bytes, requests, waves) scaled by this rank's share of the frame's rays and
+    the ratios (hit rates, wave-cycle fractions) kept -- labelled as such in `source`."""
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc*.json"))):
         rec = json.load(open(f))
@@ -258,6 +263,13 @@ def pmc_summary(kernel, K, world):
             best.setdefault("l2_request_bytes", 128 * v["l2_requests"] if "l2_requests" in v else None)
             if best["l2_request_bytes"] is None:
                 del best["l2_request_bytes"]
+    if best is None and world > 1:
+        one = pmc_summary(kernel, K, 1)
+        if one:
+            best = {k: (v * share if isinstance(v, (int, float)) and not k.endswith(("_frac", "_rate")) else v)
+                    for k, v in one.items()}
+            best["source"] = (f"{one['source']} (N=1 counters; extensive counts x {share:.4f}, this rank's share "
+                              f"of the frame's rays)")
     return best
 
 
@@ -341,6 +353,7 @@ def part_scaling(reps, torch, seed, steps, value, frame_s, counts=(2, 4, 8)):
     F = len(reps)
     for n in counts:
         ms = [0.0] * n
+        issue = [0.0] * n
         order = range(n - 1, -1, -1) if os.environ.get("RTG_BENCH_PARTS_REVERSED") else range(n)
         for r in order:
             def step(k, r=r, n=n):
@@ -350,8 +363,10 @@ def part_scaling(reps, torch, seed, steps, value, frame_s, counts=(2, 4, 8)):
             # built on first use)
             e, _ = measure(step, torch, steps, F, lambda: None, serial=lambda: None)
             ms[r] = e / steps * 1e3
+            issue[r] = measure.issue_s / steps * 1e3
         worst = max(ms)
         out[str(n)] = {"part_ms": [round(x, 4) for x in ms], "max_part_ms": round(worst, 4),
+                       "issue_ms": [round(x, 4) for x in issue],
                        "predicted_efficiency": round(frame_s * 1e3 / (n * worst), 4),
                        "predicted_mrays_s": round(value * frame_s * 1e3 / worst, 1)}
         log(f"parts x{n}: max part {worst:.4f} ms, predicted efficiency {out[str(n)]['predicted_efficiency']}")
@@ -501,7 +516,8 @@ def main():
         kbytes = {k: v / max(1, cam["spp"]) for k, v in kernel_bytes(part_st, W, H).items()}
         dom = max((k for k in ktimes if k in kbytes), key=lambda k: ktimes[k])
         K = int(args.K) if args.config == "headline" else None
-        rl = roofline(dom, kbytes[dom], ktimes[dom], pmc_summary(dom, K, world) if K else None)
+        share = part_rays / max(rays, 1)
+        rl = roofline(dom, kbytes[dom], ktimes[dom], pmc_summary(dom, K, world, share) if K else None)
         rl.update({"kernels_ms": {k: round(v, 4) for k, v in ktimes.items()}, "frame_ms": round(kern_ms, 4),
                    "frame_algo_bytes": int(kernel_bytes(st, W, H)["frame"]),
                    "frame_l2_frac": round(kernel_bytes(st, W, H)["frame"] / (kern_ms * 1e-3) / 1e9 / L2_PEAK_GBS, 4)})
@@ -623,10 +639,13 @@ def main():
                 log(f"sweep K={Ks}")
                 sweep[str(Ks)] = sweep_point(args, torch, rtgpu, local, Ks, hdr, ldr)
             result["sweep_K"] = sweep
-        if rank == 0 and world == 1 and not args.no_cpu_baseline and args.config == "headline":
+        # the reference's CPU path on this host, rank 0 only, outside the timed region, at every N
+        # (the same whole frame: its rate does not depend on how the GPUs split it)
+        if rank == 0 and not args.no_cpu_baseline and args.config == "headline":
             result["cpu_baseline"] = cpu_baseline(tmp, xml, rays, args.cpu_reps)
         if rank == 0:
             print(json.dumps(result), flush=True)
+        barrier()     # the other ranks wait for rank 0's CPU leg before tearing the group down
     finally:
         if frame is not None:
             frame.close()

@@ -163,6 +163,15 @@ public:
         for (int i = 0; i < 512; ++i) perm[i] = kPerm256[i & 255];
     }
 
+    // Test diagnostics (oracle_render_pixel): an environment lookup whose texel coordinate
+    // (width * u or height * v, before the int truncation) lies within env_eps of a texel
+    // boundary is "near"; near lookups are numbered in evaluation order, and those whose bit is
+    // set in env_flip take the texel on the other side of the boundary -- what a last-ulp
+    // different atan2f / acosf result does on the device.
+    float env_eps = 0.0f;
+    uint64_t env_flip = 0;
+    int env_near = 0;
+
     // Raytracer::PerPixel (raytracer.cpp:38-63)
     Vec3f PerPixel(int coordX, int coordY, uint64_t key) {
         Ray ray = GenerateRay(coordX, coordY, key);
@@ -656,6 +665,17 @@ private:
         float v = std::acos(dir.y) / M_PI;
         int i = im.width * u;
         int j = im.height * v;
+        if (env_eps > 0.0f) {
+            auto flip = [&](float c, int& k) {
+                const float fr = c - std::floor(c);
+                if (fr < env_eps || fr > 1.0f - env_eps) {
+                    if ((env_flip >> env_near) & 1) k += fr < 0.5f ? -1 : 1;
+                    ++env_near;
+                }
+            };
+            flip(im.width * u, i);
+            flip(im.height * v, j);
+        }
         return Texel(im, i, j) * 2 * M_PI;
     }
     Vec3f EnvDirection(Vec3f surfaceNormal, uint64_t key, int e) {         // sphericalEnvironmentLight.h:36-61
@@ -1117,9 +1137,67 @@ unsigned char Clamp8(float c) {
     return (unsigned char)(i < 0 ? 0 : (i > 255 ? 255 : i));
 }
 
+// renderThreadMain's per-pixel sample loop (main.cpp:60-121): the colour at 1 spp, else the
+// Gaussian-weighted mean of the samples; with `accum`, (sum w*c, sum w) goes there and false is
+// returned.
+bool PixelValue(Tracer& tr, int x, int y, int W, int spp, uint64_t seed, int sample_begin, int sample_count,
+                float* accum, Vec3f& color) {
+    const int pixel = x + y * W;
+    const int nRows = std::sqrt(spp), nCols = nRows;
+    if (spp <= 1 && !accum) {
+        color = tr.PerPixel(x, y, root_key(seed, pixel, 0));
+        return true;
+    }
+    Vec3f acc;
+    float sumW = 0.0f;
+    for (int s = sample_begin; s < sample_begin + sample_count; ++s) {
+        uint64_t key = root_key(seed, pixel, s);
+        float sx = 0.f, sy = 0.f;
+        if (s < nRows * nCols) {
+            int row = s / nCols, col = s % nCols;
+            float psi1 = rnd(key, RP_JITTER, 0), psi2 = rnd(key, RP_JITTER, 1);
+            sx = (col + psi1) / nCols;
+            sy = (row + psi2) / nRows;
+        }
+        Vec3f c = tr.PerPixel(x, y, key);
+        float gw = GaussWeight(sx - 0.5f, sy - 0.5f);
+        acc.x += c.x * gw;
+        acc.y += c.y * gw;
+        acc.z += c.z * gw;
+        sumW += gw;
+    }
+    if (accum) {
+        float* a = accum + 4 * (size_t)pixel;
+        a[0] = acc.x; a[1] = acc.y; a[2] = acc.z; a[3] = sumW;
+        return false;
+    }
+    color = V(acc.x / sumW, acc.y / sumW, acc.z / sumW);
+    return true;
+}
+
 }  // namespace
 
 extern "C" {
+
+// Test diagnostics: pixel (x, y) of camera `camera` as oracle_render computes it, with the
+// environment-lookup flips of Tracer::env_eps / env_flip (tests/test_gpu_configs.py explains
+// each pixel outside the parity bound by the texel flips of last-ulp atan2f / acosf results).
+// n_near receives the number of lookups within env_eps of a texel boundary.
+int oracle_render_pixel(const rtg_scene_desc* desc, int camera, int x, int y, uint64_t seed, float env_eps,
+                        uint64_t env_flip, float* rgb, int32_t* n_near) {
+    if (!desc || camera < 0 || camera >= desc->num_cameras || !rgb) return -1;
+    const rtg_camera& cam = desc->cameras[camera];
+    if (x < 0 || y < 0 || x >= cam.width || y >= cam.height) return -1;
+    Counters cnt;
+    Tracer tr(*desc, cam, cnt);
+    tr.env_eps = env_eps;
+    tr.env_flip = env_flip;
+    Vec3f c;
+    PixelValue(tr, x, y, cam.width, cam.spp < 1 ? 1 : cam.spp, seed, 0, cam.spp < 1 ? 1 : cam.spp, nullptr, c);
+    rgb[0] = c.x; rgb[1] = c.y; rgb[2] = c.z;
+    if (n_near) *n_near = tr.env_near;
+    return 0;
+}
 
 // Renders camera `camera` rows [row_begin,row_end) (row_end<=0: all) into
 // hdr (w*h*3 floats) / ldr (w*h*3 bytes); either may be NULL.  accum (w*h*4), if
@@ -1143,39 +1221,11 @@ int oracle_render(const rtg_scene_desc* desc, int camera, int row_begin, int row
     std::vector<Counters> counts(threads);
     auto work = [&](int t) {
         Tracer tr(*desc, cam, counts[t]);
-        const int nRows = std::sqrt(spp), nCols = nRows;
         for (int y = row_begin + t; y < row_end; y += threads) {
             for (int x = 0; x < W; ++x) {
                 const int pixel = x + y * W;
                 Vec3f color;
-                if (spp <= 1 && !accum) {
-                    color = tr.PerPixel(x, y, root_key(seed, pixel, 0));
-                } else {
-                    Vec3f acc;
-                    float sumW = 0.0f;
-                    for (int s = sample_begin; s < sample_begin + sample_count; ++s) {
-                        uint64_t key = root_key(seed, pixel, s);
-                        float sx = 0.f, sy = 0.f;
-                        if (s < nRows * nCols) {
-                            int row = s / nCols, col = s % nCols;
-                            float psi1 = rnd(key, RP_JITTER, 0), psi2 = rnd(key, RP_JITTER, 1);
-                            sx = (col + psi1) / nCols;
-                            sy = (row + psi2) / nRows;
-                        }
-                        Vec3f c = tr.PerPixel(x, y, key);
-                        float gw = GaussWeight(sx - 0.5f, sy - 0.5f);
-                        acc.x += c.x * gw;
-                        acc.y += c.y * gw;
-                        acc.z += c.z * gw;
-                        sumW += gw;
-                    }
-                    if (accum) {
-                        float* a = accum + 4 * (size_t)pixel;
-                        a[0] = acc.x; a[1] = acc.y; a[2] = acc.z; a[3] = sumW;
-                        continue;
-                    }
-                    color = V(acc.x / sumW, acc.y / sumW, acc.z / sumW);
-                }
+                if (!PixelValue(tr, x, y, W, spp, seed, sample_begin, sample_count, accum, color)) continue;
                 const size_t idx = 3 * (size_t)pixel;
                 if (hdr) { hdr[idx] = color.x; hdr[idx + 1] = color.y; hdr[idx + 2] = color.z; }
                 if (ldr) { ldr[idx] = Clamp8(color.x); ldr[idx + 1] = Clamp8(color.y); ldr[idx + 2] = Clamp8(color.z); }

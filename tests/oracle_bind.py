@@ -58,6 +58,48 @@ def render(host_scene, camera=0, rows=(0, 0), seed=0x5EED, threads=None, sample_
     return hdr, ldr, dict(zip(STAT_NAMES, map(int, st)))
 
 
+def render_pixel(host_scene, x, y, camera=0, seed=0x5EED, env_eps=0.0, env_flip=0):
+    """One pixel as render() computes it -> (rgb float32[3], n_near).  With env_eps > 0 the
+    environment lookups whose texel coordinate lies within env_eps of a texel boundary are
+    numbered ("near", n_near of them) and those whose bit is set in env_flip take the texel on
+    the other side: the effect of a last-ulp different atan2f / acosf on the device."""
+    L = lib()
+    L.oracle_render_pixel.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
+                                      ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]
+    rgb = np.zeros(3, np.float32)
+    n = ctypes.c_int32()
+    if L.oracle_render_pixel(host_scene.desc, camera, x, y, seed, env_eps, env_flip, rgb.ctypes.data,
+                             ctypes.byref(n)):
+        raise RuntimeError("oracle_render_pixel failed")
+    return rgb, n.value
+
+
+def explain_env_flips(host_scene, got, ref, rows=(0, 0), camera=0, seed=0x5EED, env_eps=2e-3, rel=1e-4):
+    """Every pixel of `got` (GPU, rows [rows[0], ...) of the frame) outside the parity bound of
+    `ref` (oracle), explained: some set of environment lookups within env_eps of a texel
+    boundary, flipped to the neighbouring texel (render_pixel), reproduces the GPU's value within
+    the bound.  Returns (failing pixels, unexplained [(y, x, n_near)])."""
+    got = np.asarray(got, np.float32)
+    ref = np.asarray(ref, np.float32)
+    ok = np.abs(got.astype(np.float64) - ref) <= rel * np.maximum(1.0, np.abs(ref.astype(np.float64)))
+    bad = np.argwhere(~ok.all(axis=-1))
+    unexplained = []
+    for yy, xx in bad:
+        y = int(yy) + rows[0]
+        g = got[yy, xx].astype(np.float64)
+        base, n = render_pixel(host_scene, int(xx), y, camera, seed, env_eps, 0)
+        assert np.array_equal(base, ref[yy, xx]), "render_pixel differs from render"
+        found = False
+        for mask in range(1, 1 << min(n, 8)):
+            v, _ = render_pixel(host_scene, int(xx), y, camera, seed, env_eps, mask)
+            if np.all(np.abs(g - v) <= rel * np.maximum(1.0, np.abs(v.astype(np.float64)))):
+                found = True
+                break
+        if not found:
+            unexplained.append((y, int(xx), n))
+    return len(bad), unexplained
+
+
 def tonemap(hdr, key=0.18, burn=1.0, saturation=1.0, gamma=2.2):
     """CPU restatement of Tonemapper::Tonemap (tonemapper.h:28-60)."""
     hdr = np.ascontiguousarray(hdr, np.float32)

@@ -58,7 +58,7 @@ def test_c3_blob_1080p_4spp(in_tmp):
     ohdr, _, _ = ob.render(hs, seed=11)
     r = ob.compare(hdr, ohdr, REL)
     print(r)
-    assert r["rel_pass"] >= 0.9999, r
+    assert r["n_fail"] == 0, r
 
 
 def test_c3_ton_roosendaal_1080p_4spp(in_tmp):
@@ -71,22 +71,37 @@ def test_c3_ton_roosendaal_1080p_4spp(in_tmp):
     ohdr, _, _ = ob.render(hs, seed=13)
     r = ob.compare(hdr, ohdr, REL)
     print(r)
-    assert r["rel_pass"] >= 0.9999, r
+    assert r["n_fail"] == 0, r
+
+
+# C4's pixels outside the bound, all eight bands (round 4, seed 5): 10 values in 10 pixels
+C4_FAIL_CAP = 10
 
 
 def test_c4_forest_1080p_16spp(in_tmp):
+    """Eight 16-row bands against the oracle.  The only pixels outside the 1e-4 bound are
+    explained one by one: the spherical environment light's lookup (sphericalEnvironmentLight.h:
+    22-34) truncates width * u and height * v to a texel, u and v coming from atan2f / acosf, so
+    a last-ulp different device result at a coordinate within ulps of a texel boundary picks the
+    neighbouring texel.  Each failing pixel must be reproduced by the oracle with some of its
+    lookups that lie within 2e-3 texel of a boundary flipped (ob.explain_env_flips), and their
+    number may not exceed this round's count."""
     xml = scenes.config_c4(in_tmp)
     hs, ds = _scene(xml)
     c = hs.camera(0)
     assert (c["width"], c["height"], c["spp"]) == (1920, 1080, 16) and hs.counts()["objects"] == 102
     hdr, _ = ds.render(0, seed=5)
     # eight 16-row bands spread over the frame (128 rows x 1920 x 16 spp = 3.9 M camera rays)
+    total = 0
     for r0 in (48, 176, 304, 432, 560, 688, 816, 944):
         rows = (r0, r0 + 16)
         ohdr, _, _ = ob.render(hs, rows=rows, seed=5)
         r = ob.compare(hdr[rows[0]:rows[1]], ohdr[rows[0]:rows[1]], REL)
-        print(rows, r)
-        assert r["rel_pass"] >= 0.9995, (rows, r)
+        nbad, unexplained = ob.explain_env_flips(hs, hdr[rows[0]:rows[1]], ohdr[rows[0]:rows[1]], rows, seed=5)
+        print(rows, r, "failing pixels", nbad, "unexplained", unexplained)
+        assert not unexplained, (rows, unexplained)
+        total += nbad
+    assert total <= C4_FAIL_CAP, total
 
 
 def test_c5_dragon_4k_64spp(in_tmp):
@@ -132,7 +147,7 @@ def test_large_leaf_cooperative_walk_small(cfg, in_tmp):
     ohdr, _, _ = ob.render(hs, seed=3)
     r = ob.compare(hdr, ohdr, REL)
     print(r)
-    assert r["rel_pass"] >= 0.999, r
+    assert r["n_fail"] == 0, r
     xml0 = scenes.with_depth(xml, os.path.join(in_tmp, "d0.xml"), 0)
     hs0, ds0 = _scene(xml0)
     a, _ = ds0.render(0, seed=3)

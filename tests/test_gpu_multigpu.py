@@ -207,3 +207,27 @@ def test_cli_devices(tmp_path):
         pngs.append(np.asarray(Image.open(tmp_path / (os.path.splitext(name)[0] + ".png")).convert("RGB")))
     assert np.array_equal(pngs[0], pngs[1])
     shutil.rmtree(tmp_path, ignore_errors=True)
+
+
+@pytest.mark.parametrize("part,rows", [((0, 1), (0, 0)), ((1, 2), (0, 0)), ((2, 3), (0, 0)), ((5, 8), (0, 0)),
+                                       ((0, 1), (100, 1000)), ((3, 4), (37, 1080))])
+def test_overlapped_host_path_equals_one_launch(part, rows, tmp_path, monkeypatch):
+    """rtg_render's overlapped host path (frames of >= 1 M pixels: row chunks of whole band
+    rounds on two streams, each chunk's rows copied while the next render) writes exactly the
+    rows and bits of the one-launch path (RTG_HOST_CHUNKS_OFF), for whole frames, parts of a
+    partition and row ranges."""
+    import scenes
+    xml = scenes.synthetic_heightfield(str(tmp_path), K=10082, width=1920, height=1080)
+    old = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        hs = rtgpu.HostScene(xml)
+        ds = rtgpu.DeviceScene(hs, 0)
+        init = lambda: (np.full((1080, 1920, 3), -1.0, np.float32), np.full((1080, 1920, 3), 7, np.uint8))  # noqa: E731
+        a = ds.render(0, rows=rows, part=part, seed=3, out=init())
+        monkeypatch.setenv("RTG_HOST_CHUNKS_OFF", "1")
+        b = ds.render(0, rows=rows, part=part, seed=3, out=init())
+    finally:
+        os.chdir(old)
+    assert _same(a[0], b[0]) and _same(a[1], b[1])
+    assert (a[1] != 7).any()

@@ -2,8 +2,9 @@
 (MeshLight::getSample, meshLight.h:27-47; SampleDirectLighting :780-803) on the GPU.
 
 * Per pixel, GPU == CPU oracle on the same counter-RNG keys (tolerance 1e-4 relative,
-  north_star's bound); a GI direction computed with a last-ulp different sinf/acosf can
-  flip a grazing hit, so a sliver of pixels may differ (<= 0.5 %).
+  north_star's bound), every pixel, with the same camera / secondary / shadow ray counts (a
+  GI direction computed with a last-ulp different sinf/acosf could flip a grazing hit; on the
+  six scenes at 4 spp none does).
 * Against the reference itself: statistical goldens (tests/golden/pt_*.npz, and
   <name>_avg.npz for the area-light, environment-light, DOF + motion-blur and C3 fixtures: the
   per-pixel mean of 1024 reference samples and its variance) vs the GPU at 4096 spp, 8x8-block
@@ -48,10 +49,12 @@ def test_gpu_equals_oracle(name, tmp_path):
     ohdr, _, ost = ob.render(hs, seed=99)
     r = ob.compare(hdr, ohdr, REL)
     print(name, r, st, ost)
-    assert r["rel_pass"] >= 0.995, r
+    # round 4: every pixel within the bound and the same rays on all six scenes (a last-ulp
+    # different sinf / acosf in a GI direction moved one triangle test of pt_cornell, no ray)
+    assert r["n_fail"] == 0, r
     assert np.array_equal(ldr, ob.clamp_ldr(hdr))
     for k in ("camera_rays", "secondary_rays", "shadow_rays"):
-        assert abs(st[k] - ost[k]) <= max(8, 0.002 * ost[k]), (k, st[k], ost[k])
+        assert st[k] == ost[k], (k, st[k], ost[k])
 
 
 STOCH = sorted(k for k, v in ob.manifest().items() if v["kind"] == "stochastic" and "avg_samples" in v)

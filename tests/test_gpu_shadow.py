@@ -72,6 +72,10 @@ def test_wide_shadow_headline_full_size(tmp_path):
         hdr, ldr = ds.render(0)
         ehdr, eldr = ds.render(0, flags=rtgpu.RTG_RENDER_EXACT_SHADOW)
         assert _same(hdr, ehdr) and _same(ldr, eldr)
+        # the production render (what bench.py times) against the CPU restatement itself
+        ohdr, oldr, _ = ob.render(hs)
+        r = ob.compare(hdr, ohdr)
+        assert r["n_fail"] == 0 and _same(ldr, oldr), r
         w = _stats(ds, 0)
         e = _stats(ds, rtgpu.RTG_RENDER_EXACT_SHADOW)
         print("wide", w, "\nexact", e)

@@ -1,0 +1,63 @@
+#!/bin/bash
+# Round-4 GPU sequence.  Usage: gpurun --timeout 1200 -- bash tools/gpu_r04.sh <tag> <step>... [-- bench args]
+# steps: tests (pytest -m gpu + smoke), slivers (tools/diag_slivers.py), bench, prof (kernel
+# trace of serial frames), pmc (limiter + HBM counter passes, one rocprofv3 --pmc run each),
+# configs (bench --config c2..c5), ab (tools/gpu_ab_head.sh over the libraries in $AB_LIBS,
+# e.g. AB_LIBS="base libpk2.so").  Every step has its own
+# time limit; the first failing step ends the script.
+cd "$GRAFT_REPO_ROOT"
+export TMPDIR=/tmp
+tag=$1; shift
+out=gpurun_out/$tag
+mkdir -p $out
+st=$out/status.txt
+: > $st
+steps=()
+while [ $# -gt 0 ] && [ "$1" != "--" ]; do steps+=("$1"); shift; done
+[ "$1" == "--" ] && shift
+extra="$@"
+run() {   # name timeout cmd...
+  local name=$1 to=$2; shift 2
+  echo "$(date +%T) start $name" >> $st
+  timeout -k 10 $to "$@" > $out/$name.log 2>&1
+  local rc=$?
+  echo "$(date +%T) $name rc=$rc" >> $st
+  if [ $rc -ne 0 ]; then exit $rc; fi
+}
+for s in "${steps[@]}"; do
+  case $s in
+    tests)
+      run pytest 900 python -u -m pytest tests -v -m gpu -x --timeout 300 --timeout-method thread -s
+      run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
+    slivers)
+      run slivers 600 python -u tools/diag_slivers.py $out/slivers.json ;;
+    bench)
+      run bench 600 python bench.py $extra ;;
+    prof)
+      run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o run -- python bench.py --steps 20 --warmup 3 --inflight 1 --no-cpu-baseline --no-sweep --no-extras $extra ;;
+    pmc)
+      args="--steps 3 --warmup 1 --inflight 1 --no-cpu-baseline --no-sweep --no-extras $extra"
+      k=0
+      for pass in "SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM" \
+                  "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_INSTS_LDS SQ_INSTS_SMEM SQ_INSTS_BRANCH" \
+                  "TCC_HIT_sum TCC_MISS_sum TCC_REQ_sum" \
+                  "WRITE_SIZE" \
+                  "FETCH_SIZE" \
+                  "TCP_TOTAL_CACHE_ACCESSES_sum TCP_TCC_READ_REQ_sum TCP_TCC_WRITE_REQ_sum TCP_PENDING_STALL_CYCLES_sum"; do
+        k=$((k+1))
+        echo "$(date +%T) start pmc$k" >> $st
+        timeout -s KILL 90 rocprofv3 --pmc $pass --kernel-include-regex "rtg::k_" -f csv -d $out/pmc$k -o run -- python bench.py $args > $out/pmc$k.log 2>&1
+        rc=$?; echo "$(date +%T) pmc$k ($pass) rc=$rc" >> $st
+        if [ $rc -ne 0 ]; then exit $rc; fi
+      done ;;
+    configs)
+      for c in c2 c3 c3ton c4 c5; do
+        run cfg_$c 300 python bench.py --config $c --no-cpu-baseline $extra
+      done ;;
+    ab)
+      run ab 1500 bash tools/gpu_ab_head.sh $tag/ab $AB_LIBS ;;
+    *)
+      echo "unknown step $s" >> $st; exit 2 ;;
+  esac
+done
+echo done >> $st
