@@ -351,10 +351,13 @@ int build_ahb(const std::vector<float4>& nodes, const std::vector<int2>& ext, in
             const size_t e0 = entries.size() / 3;
             for (int q = n.pbeg; q < n.pbeg + n.pcnt; ++q)
                 for (int f = P[q].first; f < P[q].first + P[q].count; ++f) {
-                    float4 A = tris[3 * (size_t)f];
+                    // [0].w: the face's reference leaf node; [1].w: the face itself (global
+                    // BVH-order index: the closest-hit walk reports it and orders ties by it)
+                    float4 A = tris[3 * (size_t)f], E1 = tris[3 * (size_t)f + 1];
                     std::memcpy(&A.w, &P[q].ref, 4);
+                    std::memcpy(&E1.w, &f, 4);
                     entries.push_back(A);
-                    entries.push_back(tris[3 * (size_t)f + 1]);
+                    entries.push_back(E1);
                     entries.push_back(tris[3 * (size_t)f + 2]);
                 }
             const size_t cnt = entries.size() / 3 - e0;
@@ -433,6 +436,11 @@ long long ahb_validate(const std::vector<WNode>& out, const std::vector<float4>&
                 rr[0].w = 0.f;
                 got.push_back({key(rr), ref});
                 if (ref < node_begin || ref >= node_end || leaf_of(nodes, ref) < 0) { ++bad; continue; }
+                int face, lfirst, lcount;
+                std::memcpy(&face, &r[1].w, 4);
+                leaf_range(nodes, ext, ref, lfirst, lcount);
+                // the named face is one of its reference leaf's, with this record
+                if (face < lfirst || face >= lfirst + lcount || key(tris + 3 * (size_t)face) != key(rr)) ++bad;
                 const double A[3] = {r[0].x, r[0].y, r[0].z}, E1[3] = {r[1].x, r[1].y, r[1].z},
                              E2[3] = {r[2].x, r[2].y, r[2].z};
                 for (int a = 0; a < 3; ++a) {

@@ -1140,7 +1140,14 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
     // RTG_RENDER_EXACT_SHADOW: shadow rays walk the reference BVH (cross-checks of the wide one)
     rtg::DevScene ds = s->ds;
     if (o->flags & RTG_RENDER_EXACT_SHADOW) ds.exact_shadow = 1;
-    if ((o->flags & RTG_RENDER_ORDERED) && ds.wnodes && ds.face_leaf) ds.ordered = 1;
+    // RTG_RENDER_ORDERED: the closest-hit walk on the any-hit tree (mode 2; its leaf boxes must be
+    // the reference's: not the split tree) or, with RTG_ORDERED_WALK=collapsed, round 3's per-lane
+    // walk of the collapsed reference tree (mode 1)
+    if (o->flags & RTG_RENDER_ORDERED) {
+        const bool collapsed = std::getenv("RTG_ORDERED_WALK") && !std::strcmp(std::getenv("RTG_ORDERED_WALK"), "collapsed");
+        if (!collapsed && ds.anodes && !ds.ahb_split) ds.ordered = 2;
+        else if (ds.wnodes && ds.face_leaf) ds.ordered = 1;
+    }
     hipEvent_t* ev = nullptr;
     if (o->flags & RTG_RENDER_TIMING) {
         for (auto& e : s->ev)
@@ -1272,14 +1279,25 @@ int rtg_copy_part_to_host(rtg_scene* s, const rtg_render_opts* o, const float* d
 // chunk starting at round m are the bands of part (p - m) mod part_count of that chunk (the
 // rotation of part_band), so the chunks together cover exactly part p's rows.  Pixels are
 // keyed by their image position (RNG included): the image is the one-launch image bit for bit.
-constexpr int kChunks = 8;
 constexpr long long kChunkMinPixels = 1ll << 20;
 static bool chunk_disabled() { return std::getenv("RTG_HOST_CHUNKS_OFF") != nullptr; }
+// chunks per frame part (RTG_HOST_CHUNKS: A/B) and whether each chunk's copy goes on the copy
+// stream (default) or on the chunk's own render stream (RTG_HOST_CHUNK_COPY=own: A/B)
+static int host_chunks() {
+    const char* v = std::getenv("RTG_HOST_CHUNKS");
+    return v ? std::max(1, std::atoi(v)) : 8;
+}
+static bool chunk_copy_own() {
+    const char* v = std::getenv("RTG_HOST_CHUNK_COPY");
+    return v && !std::strcmp(v, "own");
+}
 
 static int render_chunked(rtg_scene* s, const rtg_render_opts* o, const rtg::RenderParams& P0, int pipe, int width,
                           float* hdr_rgb, uint8_t* ldr_rgb) {
     const int N = P0.part_count, per_round = RTG_PART_BAND_ROWS * N;
     const int rounds = (P0.row_end - P0.row_begin + per_round - 1) / per_round;
+    const int kChunks = host_chunks();
+    const bool own = chunk_copy_own();
     int cr = (rounds + kChunks - 1) / kChunks;
     cr += cr & 1;                                    // even: a chunk's compact rows fill whole 16-row tiles
     for (auto& c : s->chunk_stream)
@@ -1309,11 +1327,18 @@ static int render_chunked(rtg_scene* s, const rtg_render_opts* o, const rtg::Ren
         hipStream_t st = s->chunk_stream[j & 1];
         rc = launch(s, &oj, C, P, s->d_hdr, s->d_ldr, nullptr, st, 1 + (j & 1), pipe);
         if (rc) return rc;
-        HIP_TRY(hipEventRecord(s->chunk_ev[j], st));
-        HIP_TRY(hipStreamWaitEvent(s->copy_stream, s->chunk_ev[j], 0));
-        rc = copy_part(&oj, width, C.height, s->d_hdr, s->d_ldr, hdr_rgb, ldr_rgb, s->copy_stream);
+        if (!own) {
+            HIP_TRY(hipEventRecord(s->chunk_ev[j], st));
+            HIP_TRY(hipStreamWaitEvent(s->copy_stream, s->chunk_ev[j], 0));
+        }
+        rc = copy_part(&oj, width, C.height, s->d_hdr, s->d_ldr, hdr_rgb, ldr_rgb, own ? st : s->copy_stream);
         if (rc) return rc;
     }
+    if (own)
+        for (auto& c : s->chunk_stream) {
+            HIP_TRY(hipEventRecord(s->chunk_ev[0], c));
+            HIP_TRY(hipStreamWaitEvent(s->copy_stream, s->chunk_ev[0], 0));
+        }
     // the scene's stream (rtg_render_device callers, the next rtg_render) follows the copies
     HIP_TRY(hipEventRecord(s->done, s->copy_stream));
     HIP_TRY(hipStreamWaitEvent(s->stream, s->done, 0));

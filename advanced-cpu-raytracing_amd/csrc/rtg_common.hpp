@@ -1357,6 +1357,219 @@ DEV bool trace_ordered(const DevScene& S, const Ray& r, Hit& h, Cnt<STATS>& c) {
     return true;
 }
 
+// ---------------------------------------------------------------------------
+// Closest hit on the any-hit tree as wave packets (RTG_RENDER_ORDERED, mode 2: the default
+// ordered walk)
+// ---------------------------------------------------------------------------
+// Order candidates by (t, object, face): the face index is the BVH-order one, so within a mesh
+// it is the reference walk's order.  Let C be the faces IntersectFace accepts at minT = inf
+// whose reference leaf box B_L passes the slab test at inf (the faces the reference can reach
+// at all), and V the visible ones: B_L passes at next_up(t_f), i.e. B_L's entry is at most t_f
+// (spheres count as visible).  IntersectObjects returns min(V) -- unless a face of C \ V (a
+// hidden face: hit before its own leaf box's entry, by rounding alone) lies below min(V):
+//   * when the reference reaches the ancestors of v = min(V) its minT exceeds t_v or is already
+//     at most t_v; every ancestor box contains B_L(v), and the slab test is monotone in box and
+//     minT, so the reference ends at or below v;
+//   * a face f of C below the reference's answer h was not accepted although t_f < minT, so an
+//     ancestor failed at some minT > t_f, hence B_L(f) fails at a minT above t_f: f is hidden.
+// This walk finds min(V) on any tree whose boxes contain the reference leaf boxes (the any-hit
+// tree's: unions of the B_L, exact float min / max): a child is culled only when its
+// conservative slab test fails at the lane's best t, which a box holding a face of V below that
+// best cannot do.  Hidden faces met in the walk are kept as a lower candidate; if one lies below
+// the result, the lane takes the reference walk.  A hidden face in a culled box cannot be ruled
+// out by a cheap test (its Cramer-rule t may sit below the box entry by rounding, without bound
+// for rays grazing the face), so the result is checked like round 3's ordered walk: a lane whose
+// culled boxes came within 2^-16 (relative) of its t takes the reference walk too.
+//
+// As a packet: the wave walks one node sequence (scalar-cache node / face / leaf records), the
+// union of its lanes' walks; leaf children are tested before the inner ones (they can only lower
+// t), the first lane with a passing inner child picks the nearest next, the others go onto the
+// wave's LDS stack with the least entry distance of the lanes that passed them, and a popped entry
+// no lane can still use is dropped (recorded as a cull at that distance).  Returns false for a lane
+// whose result is not certain (caller: reference walk).
+DEV bool hit_less(float t, int k, int f, float bt, int bk, int bf) {
+    return (t < bt) | ((t == bt) & ((k < bk) | ((k == bk) & (f < bf))));
+}
+DEV bool slab_cons2(float lx, float ly, float lz, float hx, float hy, float hz, const SlabRay& s, float minTc,
+                    float& tnear, bool& hinf) {
+    const float tx1 = (lx - s.o.x) * s.ix, tx2 = (hx - s.o.x) * s.ix;
+    const float ty1 = (ly - s.o.y) * s.iy, ty2 = (hy - s.o.y) * s.iy;
+    const float tz1 = (lz - s.o.z) * s.iz, tz2 = (hz - s.o.z) * s.iz;
+    const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+    const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+    tnear = tmin;
+    hinf = (tmax > -1e-30f) & (tmax >= tmin * (1.0f - 0x1p-21f) - 1e-30f);
+    return hinf & (tmin < minTc);
+}
+// wave minimum of a non-negative float (the lanes that do not take part hold +inf)
+DEV float wave_min_pos(float v) {
+    uint32_t u = __float_as_uint(v);
+    for (int m = 1; m < 64; m <<= 1) {
+        const uint32_t o = (uint32_t)__shfl_xor((int)u, m);
+        u = o < u ? o : u;
+    }
+    return __uint_as_float(u);
+}
+DEV float cull_limit(float t) { return t * (1.0f + 0x1p-20f); }   // inf stays inf
+
+struct ClosestState {
+    float bestT, hidT, cullMin;
+    int bestK, bestF, hidK, hidF;
+};
+
+template <bool STATS>
+DEV bool walk_closest_pk(const DevScene& S, int node, const int k, const Ray& lr, const RayRcp& q, const SlabRay& sr,
+                         ClosestState& B, Cnt<STATS>& c) {
+    __shared__ int ck_node[4][RTG_PK_STACK];
+    __shared__ float ck_tn[4][RTG_PK_STACK];
+    int* const stk = ck_node[(threadIdx.x >> 6) & 3];
+    float* const stn = ck_tn[(threadIdx.x >> 6) & 3];
+    // the stack is written by the first active lane (edge tiles run with partial waves)
+    const bool writer = (int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1;
+    int sp = 0;                                      // wave-uniform
+    int steps = 0;
+    node = __builtin_amdgcn_readfirstlane(node);
+    while (true) {
+        if (++steps > RTG_PK_MAX_STEPS) return false;
+        node = __builtin_amdgcn_readfirstlane(node);
+        rtg_s16 na, nb;
+        sload_wnode(S.anodes + node, na, nb);
+        const float4 lox = f4(na[0], na[1], na[2], na[3]), hix = f4(na[4], na[5], na[6], na[7]);
+        const float4 loy = f4(na[8], na[9], na[10], na[11]), hiy = f4(na[12], na[13], na[14], na[15]);
+        const float4 loz = f4(nb[0], nb[1], nb[2], nb[3]), hiz = f4(nb[4], nb[5], nb[6], nb[7]);
+        const int cidx[4] = {nb[8], nb[9], nb[10], nb[11]};
+        const int lidx[4] = {nb[12], nb[13], nb[14], nb[15]};
+        c.ewnode();
+        const float minTc = cull_limit(B.bestT);
+        float tn[4];
+        bool h[4], hi[4];
+        h[0] = slab_cons2(lox.x, loy.x, loz.x, hix.x, hiy.x, hiz.x, sr, minTc, tn[0], hi[0]);
+        h[1] = slab_cons2(lox.y, loy.y, loz.y, hix.y, hiy.y, hiz.y, sr, minTc, tn[1], hi[1]);
+        h[2] = slab_cons2(lox.z, loy.z, loz.z, hix.z, hiy.z, hiz.z, sr, minTc, tn[2], hi[2]);
+        h[3] = slab_cons2(lox.w, loy.w, loz.w, hix.w, hiy.w, hiz.w, sr, minTc, tn[3], hi[3]);
+        // leaf children first: their faces can only lower t
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (cidx[j] == WCHILD_EMPTY || cidx[j] >= 0) continue;
+            if (hi[j] & !h[j]) B.cullMin = fminf(B.cullMin, tn[j]);
+            if (!__ballot(h[j])) continue;
+            const int first = lidx[j] >> 8, cnt = lidx[j] & 255;
+            for (int e = first; e < first + cnt; ++e) {
+                rtg_s8 ra;
+                rtg_s4 rb;
+                sload_rec(S.ahtris + 3 * (size_t)e, ra, rb);
+                const float4 R[3] = {f4(ra[0], ra[1], ra[2], ra[3]), f4(ra[4], ra[5], ra[6], ra[7]),
+                                     f4(rb[0], rb[1], rb[2], rb[3])};
+                const int f = ra[7];
+                if (h[j]) c.template tri<false>();
+                float t;
+                const bool ok = h[j] & tri_test_sel(R, lr, INFINITY, t, h[j]);
+                const bool better = ok && hit_less(t, k, f, B.bestT, B.bestK, B.bestF);
+                if (!__ballot(better)) continue;
+                rtg_s8 rn;
+                sload_node(S.nodes + 2 * ra[3], rn);
+                const float bx0 = __int_as_float(rn[0]), by0 = __int_as_float(rn[1]), bz0 = __int_as_float(rn[2]);
+                const float bx1 = __int_as_float(rn[3]), by1 = __int_as_float(rn[4]), bz1 = __int_as_float(rn[5]);
+                // visible: the reference leaf box passes at next_up(t) (its entry is at most t)
+                const bool vis = better & box_hit_fast<true>(bx0, by0, bz0, bx1, by1, bz1, lr, q, next_up(t), better);
+                const bool hcand = better & !vis;
+                // a hidden face counts only if the reference can reach it at all (B_L passes at inf)
+                const bool hid = hcand & box_hit_fast<true>(bx0, by0, bz0, bx1, by1, bz1, lr, q, INFINITY, hcand);
+                if (vis) { B.bestT = t; B.bestK = k; B.bestF = f; }
+                if (hid && hit_less(t, k, f, B.hidT, B.hidK, B.hidF)) { B.hidT = t; B.hidK = k; B.hidF = f; }
+            }
+        }
+        // inner children against the (possibly lowered) best t: the nearest passing child of the
+        // first lane that has one goes next, the others onto the stack
+        const float minTc2 = cull_limit(B.bestT);
+        bool h2[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const bool inner = cidx[j] >= 0;
+            h2[j] = inner & h[j] & (tn[j] < minTc2);
+            if (inner & hi[j] & !h2[j]) B.cullMin = fminf(B.cullMin, tn[j]);
+        }
+        const uint64_t any = __ballot(h2[0] | h2[1] | h2[2] | h2[3]);
+        int next = -1;
+        if (any) {
+            const int lead = __ffsll((long long)any) - 1;
+            float nextT = INFINITY, nextTw = INFINITY;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                if (!__ballot(h2[j])) continue;
+                const float tl = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(h2[j] ? tn[j] : INFINITY), lead));
+                const float tw = wave_min_pos(h2[j] ? fmaxf(tn[j], 0.0f) : INFINITY);
+                int spill = cidx[j];
+                float spillT = tw;
+                if (next < 0 || tl < nextT) {
+                    spill = next;
+                    spillT = nextTw;
+                    next = cidx[j];
+                    nextT = tl;
+                    nextTw = tw;
+                }
+                if (spill >= 0) {
+                    if (sp >= RTG_PK_STACK) return false;   // stack full: every lane takes the reference walk
+                    if (writer) { stk[sp] = spill; stn[sp] = spillT; }
+                    ++sp;
+                }
+            }
+        }
+        if (next >= 0) {
+            node = next;
+            continue;
+        }
+        // pop the next entry some lane can still use; the others are culls at their distance
+        bool found = false;
+        while (sp > 0) {
+            --sp;
+            const int n = stk[sp];
+            const float tw = stn[sp];
+            if (__ballot(tw < cull_limit(B.bestT))) {
+                node = n;
+                found = true;
+                break;
+            }
+            B.cullMin = fminf(B.cullMin, tw);
+        }
+        if (!found) break;
+    }
+    return true;
+}
+
+// IntersectObjects on the any-hit trees (meshes with identity transforms and spheres only:
+// FEAT 0 / FEAT_SPHERE).  true: h holds the reference's answer; false: take the reference walk.
+template <bool STATS, int FEAT>
+DEV bool trace_closest_pk(const DevScene& S, const Ray& r, Hit& h, Cnt<STATS>& c) {
+    static_assert((FEAT & ~FEAT_SPHERE) == 0, "meshes with identity transforms and spheres only");
+    const RayRcp q = ray_rcp(r);
+    const SlabRay sr = slab_ray(r, q);
+    ClosestState B;
+    B.bestT = B.hidT = B.cullMin = INFINITY;
+    B.bestK = B.bestF = B.hidK = B.hidF = 0x7FFFFFFF;
+    bool sure = q.fast;                              // zero / tiny direction component: reference walk
+    for (int k = 0; k < S.num_objects; ++k) {
+        const DevObject& ob = S.objects[k];
+        c.obj();
+        if ((FEAT & FEAT_SPHERE) && ob.kind == OBJ_SPHERE) {
+            c.sph();
+            float t;
+            // a later object wins only with a strictly smaller t (sphere_t: 0 < t < minT)
+            if (sphere_t(ob, r, B.bestT, t)) { B.bestT = t; B.bestK = k; B.bestF = -1; }
+            continue;
+        }
+        if (ob.aroot < 0) return false;
+        sure &= walk_closest_pk<STATS>(S, ob.aroot, k, r, q, sr, B, c);
+    }
+    sure &= !hit_less(B.hidT, B.hidK, B.hidF, B.bestT, B.bestK, B.bestF);
+    sure &= !(B.bestT < INFINITY && B.cullMin <= B.bestT * (1.0f + 0x1p-16f));
+    h.t = B.bestT;
+    h.obj = B.bestT < INFINITY ? B.bestK : -1;
+    h.face = B.bestT < INFINITY ? B.bestF : -1;
+    h.o = r.o;
+    return sure;
+}
+
 // The same decision on the reference BVH itself, walked from the shadow ray's origin
 // upwards.  A shadow ray starts on the surface it leaves (hit point + eps n), so top-down
 // every ancestor of the origin's leaf is hit and both children are tested at every level;

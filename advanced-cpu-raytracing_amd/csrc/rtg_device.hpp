@@ -65,12 +65,14 @@ enum : int { WCHILD_EMPTY = -1 };
 // climb from the ray's origin leaf (trace_any_up).  (Round 2's mode 4, the collapsed tree on
 // compressed 64-B nodes, measured slower -- 0.311 vs 0.273 ms -- and was removed.)  The ray-tree pipeline's k_shadow always
 // uses the per-lane reference walk (its secondary rays are incoherent: modes 1-3 measured
-// slower on C5).  Camera rays: RTG_PRIMARY_PACKET (0: per lane, default).  DESIGN.md §5.
+// slower on C5).  Camera rays: RTG_PRIMARY_PACKET -- 2 (default): the reference walk as wave
+// packets with scalar-cache records and select face tests (k_primary 0.227 -> 0.205 ms on the
+// headline, profiles/r04c_packet_ab.txt); 1: round 2's packet form; 0: per lane.  DESIGN.md §5.
 #ifndef RTG_SHADOW_MODE
 #define RTG_SHADOW_MODE 3
 #endif
 #ifndef RTG_PRIMARY_PACKET
-#define RTG_PRIMARY_PACKET 0
+#define RTG_PRIMARY_PACKET 2
 #endif
 
 struct DevMaterial {

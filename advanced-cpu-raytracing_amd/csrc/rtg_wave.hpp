@@ -25,10 +25,14 @@ namespace rtg {
 
 enum { BASE_FINAL = 1, BASE_ADD_ZERO = 2 };
 
-// ORD: RTG_RENDER_ORDERED (plain mesh scenes): the checked nearest-first wide walk
-// (trace_ordered), the reference walk where its check fails
-template <bool STATS, int FEAT, bool ORD = false>
-__global__ __launch_bounds__(256, ORD ? RTG_WIDE_WAVES_PLAIN : RTG_TRACE_WAVES(FEAT)) void k_primary(
+// ORD: RTG_RENDER_ORDERED (plain mesh scenes): the checked closest-hit walk -- on the any-hit
+// tree as wave packets (trace_closest_pk, ordered mode 2) or nearest-first per lane on the
+// collapsed reference tree (trace_ordered, mode 1) -- the reference walk where its check fails
+#ifndef RTG_ORD_WAVES
+#define RTG_ORD_WAVES RTG_WIDE_WAVES_PLAIN
+#endif
+template <bool STATS, int FEAT, int ORD = 0>
+__global__ __launch_bounds__(256, ORD ? RTG_ORD_WAVES : RTG_TRACE_WAVES(FEAT)) void k_primary(
     const DevScene S, const DevCamera C, const RenderParams P, const int sample, const WaveBufs W,
     DevCounters* counters) {
     int px, py, crow;
@@ -42,7 +46,10 @@ __global__ __launch_bounds__(256, ORD ? RTG_WIDE_WAVES_PLAIN : RTG_TRACE_WAVES(F
         cn.cam();
         Hit h;
         if constexpr (ORD) {
-            if (!trace_ordered<STATS>(S, ray, h, cn)) {
+            bool sure;
+            if constexpr (ORD == 2) sure = trace_closest_pk<STATS, FEAT>(S, ray, h, cn);
+            else sure = trace_ordered<STATS>(S, ray, h, cn);
+            if (!sure) {
                 cn.efallback();
                 trace<false, STATS, FEAT>(S, ray, mbTime, INFINITY, INFINITY, h, cn);
             }
@@ -449,8 +456,11 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
         if (e5) (void)hipEventRecord(e5[0], st);
         bool ordered = false;
         if constexpr (FEAT == 0) {
-            if (S.ordered) {
-                hipLaunchKernelGGL((k_primary<STATS, 0, true>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
+            if (S.ordered == 2) {
+                hipLaunchKernelGGL((k_primary<STATS, 0, 2>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
+                ordered = true;
+            } else if (S.ordered) {
+                hipLaunchKernelGGL((k_primary<STATS, 0, 1>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
                 ordered = true;
             }
         }

@@ -165,12 +165,14 @@ public:
 
     // Test diagnostics (oracle_render_pixel): an environment lookup whose texel coordinate
     // (width * u or height * v, before the int truncation) lies within env_eps of a texel
-    // boundary is "near"; near lookups are numbered in evaluation order, and those whose bit is
-    // set in env_flip take the texel on the other side of the boundary -- what a last-ulp
-    // different atan2f / acosf result does on the device.
+    // boundary is "near"; the distinct near coordinates (axis, value) are numbered in order of
+    // first use, and the lookups at a coordinate whose bit is set in env_flip take the texel on
+    // the other side of the boundary -- what a last-ulp different atan2f / acosf result does on
+    // the device (the same direction, e.g. every sample of a pixel whose camera ray misses,
+    // gives the same result there).
     float env_eps = 0.0f;
     uint64_t env_flip = 0;
-    int env_near = 0;
+    std::vector<std::pair<int, float>> env_near;
 
     // Raytracer::PerPixel (raytracer.cpp:38-63)
     Vec3f PerPixel(int coordX, int coordY, uint64_t key) {
@@ -666,15 +668,17 @@ private:
         int i = im.width * u;
         int j = im.height * v;
         if (env_eps > 0.0f) {
-            auto flip = [&](float c, int& k) {
+            auto flip = [&](int axis, float c, int& k) {
                 const float fr = c - std::floor(c);
                 if (fr < env_eps || fr > 1.0f - env_eps) {
-                    if ((env_flip >> env_near) & 1) k += fr < 0.5f ? -1 : 1;
-                    ++env_near;
+                    size_t id = 0;
+                    while (id < env_near.size() && env_near[id] != std::make_pair(axis, c)) ++id;
+                    if (id == env_near.size()) env_near.push_back({axis, c});
+                    if (id < 64 && ((env_flip >> id) & 1)) k += fr < 0.5f ? -1 : 1;
                 }
             };
-            flip(im.width * u, i);
-            flip(im.height * v, j);
+            flip(0, im.width * u, i);
+            flip(1, im.height * v, j);
         }
         return Texel(im, i, j) * 2 * M_PI;
     }
@@ -1195,7 +1199,7 @@ int oracle_render_pixel(const rtg_scene_desc* desc, int camera, int x, int y, ui
     Vec3f c;
     PixelValue(tr, x, y, cam.width, cam.spp < 1 ? 1 : cam.spp, seed, 0, cam.spp < 1 ? 1 : cam.spp, nullptr, c);
     rgb[0] = c.x; rgb[1] = c.y; rgb[2] = c.z;
-    if (n_near) *n_near = tr.env_near;
+    if (n_near) *n_near = (int32_t)tr.env_near.size();
     return 0;
 }
 

@@ -60,9 +60,10 @@ def render(host_scene, camera=0, rows=(0, 0), seed=0x5EED, threads=None, sample_
 
 def render_pixel(host_scene, x, y, camera=0, seed=0x5EED, env_eps=0.0, env_flip=0):
     """One pixel as render() computes it -> (rgb float32[3], n_near).  With env_eps > 0 the
-    environment lookups whose texel coordinate lies within env_eps of a texel boundary are
-    numbered ("near", n_near of them) and those whose bit is set in env_flip take the texel on
-    the other side: the effect of a last-ulp different atan2f / acosf on the device."""
+    distinct texel coordinates of environment lookups that lie within env_eps of a texel
+    boundary are numbered ("near", n_near of them) and the lookups at those whose bit is set in
+    env_flip take the texel on the other side: the effect of a last-ulp different atan2f /
+    acosf on the device."""
     L = lib()
     L.oracle_render_pixel.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_uint64,
                                       ctypes.c_float, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p]

@@ -3,7 +3,7 @@
 # steps: tests (pytest -m gpu + smoke), slivers (tools/diag_slivers.py), bench, prof (kernel
 # trace of serial frames), pmc (limiter + HBM counter passes, one rocprofv3 --pmc run each),
 # configs (bench --config c2..c5), ab (tools/gpu_ab_head.sh over the libraries in $AB_LIBS,
-# e.g. AB_LIBS="base libpk2.so").  Every step has its own
+# e.g. AB_LIBS="base libpk2.so"), py:<name> (tools/<name>.py).  Every step has its own
 # time limit; the first failing step ends the script.
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -56,6 +56,9 @@ for s in "${steps[@]}"; do
       done ;;
     ab)
       run ab 1500 bash tools/gpu_ab_head.sh $tag/ab $AB_LIBS ;;
+    py:*)
+      t=${s#py:}
+      run $t 600 python -u tools/$t.py ;;
     *)
       echo "unknown step $s" >> $st; exit 2 ;;
   esac
