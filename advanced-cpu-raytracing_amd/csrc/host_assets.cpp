@@ -1,8 +1,9 @@
-// Asset readers for the scene loader: PLY meshes (replaces happly, parser.cpp:1396-1444) and
-// LDR images (PNG / PNM; replaces stb_image as used by LDRImage.h:37-44).  Image decoding is
-// outside the hot path: JPEG and OpenEXR files are refused with
-// RTG_ERR_UNSUPPORTED (a front end over the reference's own loaders -- integration/dorkrt --
-// may still hand decoded texels to rtg_scene_create).
+// Asset readers for the scene loader: PLY meshes (replaces happly, parser.cpp:1396-1444), LDR
+// images (PNG / PNM; replaces stb_image as used by LDRImage.h:37-44) and OpenEXR images (replaces
+// tinyexr as used by HDRImage.h:45-72: the reference's only HDR image path, environment maps
+// included).  JPEG is refused with RTG_ERR_UNSUPPORTED (a parity gap; a front end
+// over the reference's own loaders -- integration/dorkrt -- may still hand decoded texels to
+// rtg_scene_create).
 #include "host_assets.hpp"
 
 #include <zlib.h>
@@ -289,6 +290,195 @@ bool load_image8(const std::string& path, Image8& img, std::string& err) {
     if (data.size() >= 2 && data[0] == 'P' && data[1] >= '1' && data[1] <= '6') return load_pnm(data, img, err);
     err = "unsupported image format (PNG / PPM / PGM only): " + path;
     return false;
+}
+
+// ============================================================================
+// OpenEXR images (replaces tinyexr's LoadEXR as HDRImage.h:45-72 uses it): single-part
+// scanline files, compression NONE / RLE / ZIPS / ZIP, HALF or FLOAT samples.  LoadEXR's
+// behaviour kept: the R, G, B, A channels are looked for among the first four channels of the
+// (name-sorted) channel list, a single-channel image is replicated into R, G, B, A, alpha
+// defaults to 1, HALF samples are widened exactly, and a file with lineOrder != 0 comes out
+// flipped vertically (tinyexr places line y at height-1-y for decreasing order).  HDRImage
+// keeps R, G, B.  Tiled, multi-part, deep and PIZ / PXR24 / B44 / DWA files are refused.
+// ============================================================================
+namespace {
+float half_to_float(uint16_t h) {
+    const uint32_t sign = uint32_t(h >> 15) << 31;
+    const int ex = (h >> 10) & 31;
+    uint32_t man = h & 1023u;
+    uint32_t bits;
+    if (ex == 0) {
+        if (man == 0) {
+            bits = sign;
+        } else {                                  // subnormal half: normalise
+            int e = -1;
+            do { ++e; man <<= 1; } while (!(man & 1024u));
+            bits = sign | (uint32_t(127 - 15 - e) << 23) | ((man & 1023u) << 13);
+        }
+    } else if (ex == 31) {
+        bits = sign | 0x7F800000u | (man << 13);
+    } else {
+        bits = sign | (uint32_t(ex - 15 + 127) << 23) | (man << 13);
+    }
+    float f;
+    std::memcpy(&f, &bits, 4);
+    return f;
+}
+
+// OpenEXR's byte reordering + delta predictor undone (ZIP and RLE share it; ImfZip.cpp)
+void exr_unpredict(std::vector<unsigned char>& t, unsigned char* dst) {
+    for (size_t i = 1; i < t.size(); ++i) t[i] = (unsigned char)(int(t[i - 1]) + int(t[i]) - 128);
+    const size_t n = t.size(), half = (n + 1) / 2;
+    for (size_t i = 0, a = 0, b = half; i < n;) {
+        dst[i++] = t[a++];
+        if (i < n) dst[i++] = t[b++];
+    }
+}
+
+bool exr_rle(const unsigned char* in, size_t inLen, std::vector<unsigned char>& out) {
+    size_t o = 0;
+    while (inLen > 0) {
+        const int c = (signed char)*in;
+        if (c < 0) {
+            const size_t n = size_t(-c);
+            if (inLen < n + 1 || o + n > out.size()) return false;
+            std::memcpy(&out[o], in + 1, n);
+            o += n; in += n + 1; inLen -= n + 1;
+        } else {
+            const size_t n = size_t(c) + 1;
+            if (inLen < 2 || o + n > out.size()) return false;
+            std::memset(&out[o], in[1], n);
+            o += n; in += 2; inLen -= 2;
+        }
+    }
+    return o == out.size();
+}
+
+template <typename T> T rd(const unsigned char* p) { T v; std::memcpy(&v, p, sizeof(T)); return v; }
+}  // namespace
+
+bool load_exr(const std::string& path, int& width, int& height, std::vector<float>& rgb, std::string& err) {
+    std::string file;
+    if (!read_file(path, file)) { err = "cannot open image " + path; return false; }
+    const unsigned char* d = (const unsigned char*)file.data();
+    const size_t n = file.size();
+    if (n < 8 || rd<uint32_t>(d) != 20000630u) { err = "not an OpenEXR file: " + path; return false; }
+    const uint32_t ver = rd<uint32_t>(d + 4);
+    if ((ver & 0xFF) != 2 || (ver & 0x1A00)) { err = "tiled / multi-part / deep EXR not supported: " + path; return false; }
+    struct Chan { std::string name; int type; };
+    std::vector<Chan> chans;
+    int comp = -1, lineOrder = 0;
+    int32_t dw[4] = {0, 0, -1, -1};
+    size_t p = 8;
+    auto cstr = [&](std::string& s) {
+        const size_t e = file.find('\0', p);
+        if (e == std::string::npos) return false;
+        s.assign(file, p, e - p);
+        p = e + 1;
+        return true;
+    };
+    while (true) {
+        std::string name, type;
+        if (!cstr(name)) { err = "truncated EXR header"; return false; }
+        if (name.empty()) break;
+        if (!cstr(type) || p + 4 > n) { err = "truncated EXR header"; return false; }
+        const uint32_t sz = rd<uint32_t>(d + p);
+        p += 4;
+        if (p + sz > n) { err = "truncated EXR header"; return false; }
+        const unsigned char* v = d + p;
+        if (name == "channels") {
+            size_t q = 0;
+            while (q < sz && v[q]) {
+                const char* nm = (const char*)v + q;
+                const size_t L = std::strlen(nm);
+                q += L + 1;
+                if (q + 16 > sz) { err = "bad EXR channel list"; return false; }
+                chans.push_back({std::string(nm, L), rd<int32_t>(v + q)});
+                if (rd<int32_t>(v + q + 8) != 1 || rd<int32_t>(v + q + 12) != 1) {
+                    err = "subsampled EXR channels not supported"; return false;
+                }
+                q += 16;
+            }
+        } else if (name == "compression") {
+            comp = v[0];
+        } else if (name == "dataWindow") {
+            for (int k = 0; k < 4; ++k) dw[k] = rd<int32_t>(v + 4 * k);
+        } else if (name == "lineOrder") {
+            lineOrder = v[0];
+        }
+        p += sz;
+    }
+    width = dw[2] - dw[0] + 1;
+    height = dw[3] - dw[1] + 1;
+    if (chans.empty() || width <= 0 || height <= 0) { err = "EXR without channels / data window"; return false; }
+    int lines;
+    switch (comp) {
+        case 0: case 1: case 2: lines = 1; break;      // NONE, RLE, ZIPS
+        case 3: lines = 16; break;                     // ZIP
+        default: err = "EXR compression " + std::to_string(comp) + " not supported (NONE/RLE/ZIPS/ZIP)"; return false;
+    }
+    size_t pixBytes = 0;
+    std::vector<size_t> choff;
+    for (const Chan& c : chans) {
+        if (c.type != 1 && c.type != 2) { err = "EXR UINT channels not supported"; return false; }
+        choff.push_back(pixBytes);
+        pixBytes += c.type == 1 ? 2 : 4;
+    }
+    // LoadEXR: R/G/B/A among the first four channels; one channel -> grey
+    int iR = -1, iG = -1, iB = -1, iA = -1;
+    for (size_t c = 0; c < chans.size() && c < 4; ++c) {
+        if (chans[c].name == "R") iR = (int)c;
+        else if (chans[c].name == "G") iG = (int)c;
+        else if (chans[c].name == "B") iB = (int)c;
+        else if (chans[c].name == "A") iA = (int)c;
+    }
+    if (chans.size() == 1) iR = iG = iB = 0;
+    else if (iR < 0 || iG < 0 || iB < 0) { err = "EXR without R, G, B channels: " + path; return false; }
+    (void)iA;
+    const int nblocks = (height + lines - 1) / lines;
+    if (p + size_t(nblocks) * 8 > n) { err = "truncated EXR offset table"; return false; }
+    rgb.assign(size_t(width) * height * 3, 0.f);
+    std::vector<unsigned char> raw, tmp;
+    for (int b = 0; b < nblocks; ++b) {
+        const uint64_t off = rd<uint64_t>(d + p + 8 * size_t(b));
+        if (off + 8 > n) { err = "bad EXR chunk offset"; return false; }
+        const int y = rd<int32_t>(d + off);
+        const uint32_t len = rd<uint32_t>(d + off + 4);
+        if (off + 8 + len > n) { err = "truncated EXR chunk"; return false; }
+        const int line0 = y - dw[1];
+        const int nl = std::min(lines, height - line0);
+        if (line0 < 0 || nl <= 0) { err = "bad EXR chunk line"; return false; }
+        const size_t need = size_t(nl) * width * pixBytes;
+        const unsigned char* src = d + off + 8;
+        raw.resize(need);
+        if (comp == 0 || len == need) {                 // stored (also a chunk that did not compress)
+            if (len != need) { err = "bad EXR chunk size"; return false; }
+            std::memcpy(raw.data(), src, need);
+        } else if (comp == 1) {
+            tmp.assign(need, 0);
+            if (!exr_rle(src, len, tmp)) { err = "EXR RLE decode failed"; return false; }
+            exr_unpredict(tmp, raw.data());
+        } else {
+            tmp.assign(need, 0);
+            uLongf outLen = need;
+            if (uncompress(tmp.data(), &outLen, src, len) != Z_OK || outLen != need) { err = "EXR inflate failed"; return false; }
+            exr_unpredict(tmp, raw.data());
+        }
+        for (int v = 0; v < nl; ++v) {
+            const int row = lineOrder == 0 ? line0 + v : height - 1 - (line0 + v);
+            const unsigned char* lineBase = raw.data() + size_t(v) * width * pixBytes;
+            const int ci[3] = {iR, iG, iB};
+            for (int k = 0; k < 3; ++k) {
+                const Chan& c = chans[ci[k]];
+                const unsigned char* cb = lineBase + choff[ci[k]] * width;
+                for (int x = 0; x < width; ++x) {
+                    const float f = c.type == 1 ? half_to_float(rd<uint16_t>(cb + 2 * size_t(x))) : rd<float>(cb + 4 * size_t(x));
+                    rgb[3 * (size_t(row) * width + x) + k] = f;
+                }
+            }
+        }
+    }
+    return true;
 }
 
 // ============================================================================

@@ -652,9 +652,10 @@ void Loader::parseTextures(XmlNode* root, RefStream& stream) {   // parser.cpp:8
             HostScene::ImageStore st;
             std::string err;
             if (filename.find(".exr") != std::string::npos) {          // HDRImage (parser.cpp:103-107)
-                // image decoding is outside the hot path; HDR texels reach the
-                // device only through a front end that decodes them (rtg_scene_desc images)
-                fail(RTG_ERR_UNSUPPORTED, "OpenEXR images are not supported by this loader: " + filename);
+                if (!load_exr("inputs/" + filename, st.width, st.height, st.texels, err))
+                    fail(err.find("not supported") != std::string::npos ? RTG_ERR_UNSUPPORTED : RTG_ERR_IO, err);
+                st.channels = 3;
+                st.is_hdr = 1;
             } else {                                                    // LDRImage (parser.cpp:110)
                 Image8 img;
                 if (!load_image8("inputs/" + filename, img, err))

@@ -1,13 +1,16 @@
-"""Image-decoder fixtures: small PNG files and the texels the reference's own LDRImage
-(stbi_load, LDRImage.h:37-44) reads from them, through `oracle/_ref/refdriver imgdump` (the
-reference compiled here, oracle/Makefile).  Writes tests/golden/images/<name>.png and
+"""Image-decoder fixtures: small PNG and OpenEXR files and the texels the reference's own image
+classes read from them -- LDRImage (stbi_load, LDRImage.h:37-44) and HDRImage (tinyexr LoadEXR,
+HDRImage.h:45-72) -- through `oracle/_ref/refdriver imgdump` (the reference compiled here,
+oracle/Makefile).  Writes tests/golden/images/<name>.{png,exr} and
 tests/golden/images/decoded.npz (per fixture: "<name>" texels, "<name>_info" = w, h, c, is_hdr).
+
+The EXR writer below is this script's own (single-part scanline files, NONE / RLE / ZIPS / ZIP,
+HALF / FLOAT channels, OpenEXR's byte reordering + delta predictor).
 
 The PNG writer below is this script's own: it chooses the scanline filter per row (all five
 filter types appear in every fixture), so the loader's unfiltering is exercised whatever zlib
 makes of the data.  Colour types: grey (1/2/4/8/16 bit), grey + alpha, RGB (8/16 bit), RGBA,
-palette with and without tRNS.  JPEG and OpenEXR are outside the loader (refused
-with RTG_ERR_UNSUPPORTED).
+palette with and without tRNS.  JPEG is outside the loader (refused with RTG_ERR_UNSUPPORTED).
 
     python tests/golden/make_images.py        (needs oracle/_ref/refdriver: make -C oracle)
 """
@@ -23,6 +26,105 @@ import numpy as np
 HERE = os.path.dirname(os.path.abspath(__file__))
 OUT = os.path.join(HERE, "images")
 REFDRIVER = os.path.join(os.path.dirname(os.path.dirname(HERE)), "oracle", "_ref", "refdriver")
+
+
+def _attr(name, typ, data):
+    return name.encode() + b"\0" + typ.encode() + b"\0" + struct.pack("<i", len(data)) + data
+
+
+def _predict(raw):
+    """OpenEXR's ZIP / RLE pre-pass: split even / odd bytes, then byte deltas (+128)."""
+    b = np.frombuffer(raw, np.uint8)
+    t = np.concatenate([b[0::2], b[1::2]]).astype(np.int32)
+    d = t.copy()
+    d[1:] = (t[1:] - t[:-1] + 128 + 256) & 255
+    return d.astype(np.uint8).tobytes()
+
+
+def _rle(data):
+    out = bytearray()
+    i, n = 0, len(data)
+    while i < n:
+        j = i
+        while j + 1 < n and data[j + 1] == data[i] and j - i < 127:
+            j += 1
+        run = j - i + 1
+        if run >= 3:
+            out += struct.pack("<b", run - 1) + bytes([data[i]])
+            i = j + 1
+            continue
+        k = i
+        while k < n and k - i < 127:
+            if k + 2 < n and data[k] == data[k + 1] == data[k + 2]:
+                break
+            k += 1
+        out += struct.pack("<b", -(k - i)) + bytes(data[i:k])
+        i = k
+    return bytes(out)
+
+
+def write_exr(path, channels, comp=3, line_order=0):
+    """channels: {name: (HxW float array, 1 = HALF / 2 = FLOAT)}; comp 0 NONE, 1 RLE, 2 ZIPS, 3 ZIP."""
+    names = sorted(channels)
+    h, w = next(iter(channels.values()))[0].shape
+    chl = b"".join(n.encode() + b"\0" + struct.pack("<iB3xii", channels[n][1], 0, 1, 1) for n in names) + b"\0"
+    hdr = (_attr("channels", "chlist", chl) + _attr("compression", "compression", bytes([comp])) +
+           _attr("dataWindow", "box2i", struct.pack("<4i", 0, 0, w - 1, h - 1)) +
+           _attr("displayWindow", "box2i", struct.pack("<4i", 0, 0, w - 1, h - 1)) +
+           _attr("lineOrder", "lineOrder", bytes([line_order])) +
+           _attr("pixelAspectRatio", "float", struct.pack("<f", 1.0)) +
+           _attr("screenWindowCenter", "v2f", struct.pack("<2f", 0.0, 0.0)) +
+           _attr("screenWindowWidth", "float", struct.pack("<f", 1.0)) + b"\0")
+    lines = 16 if comp == 3 else 1
+    chunks = []
+    for y0 in range(0, h, lines):
+        raw = b""
+        for y in range(y0, min(h, y0 + lines)):
+            for n in names:
+                a, t = channels[n]
+                raw += a[y].astype(np.float16 if t == 1 else np.float32).astype("<f2" if t == 1 else "<f4").tobytes()
+        if comp in (2, 3):
+            data = zlib.compress(_predict(raw), 9)
+        elif comp == 1:
+            data = _rle(_predict(raw))
+        else:
+            data = raw
+        if len(data) >= len(raw):        # stored when it does not compress (OpenEXR / tinyexr)
+            data = raw
+        chunks.append(struct.pack("<ii", y0, len(data)) + data)
+    head = struct.pack("<Ii", 20000630, 2) + hdr
+    off = len(head) + 8 * len(chunks)
+    table = b""
+    for c in chunks:
+        table += struct.pack("<Q", off)
+        off += len(c)
+    with open(path, "wb") as f:
+        f.write(head + table + b"".join(chunks))
+
+
+def exr_fixtures():
+    rng = np.random.default_rng(7)
+    H, W = 37, 29
+    yy, xx = np.mgrid[0:H, 0:W].astype(np.float32)
+    smooth = {c: (np.sin(xx * (0.2 + 0.1 * k)) * np.cos(yy * 0.15) * 4.0 + 2.0 * k).astype(np.float32)
+              for k, c in enumerate("RGB")}
+    noise = {c: (rng.standard_normal((H, W)) * 10 ** rng.uniform(-6, 4, (H, W))).astype(np.float32) for c in "RGBA"}
+    # half specials: subnormals, zero, -0, large, inf
+    spec = noise["R"].copy()
+    spec[0, :6] = [6.0e-8, -6.0e-8, 0.0, -0.0, 65504.0, np.inf]
+    fx = {
+        "exr_half_zip": ({c: (smooth[c], 1) for c in "RGB"}, 3, 0),
+        "exr_float_none_rgba_decreasing": ({c: (noise[c], 2) for c in "RGBA"}, 0, 1),
+        "exr_half_zips": ({"R": (spec, 1), "G": (smooth["G"], 1), "B": (noise["B"], 1)}, 2, 0),
+        "exr_half_rle": ({c: (np.round(smooth[c]), 1) for c in "RGB"}, 1, 0),
+        "exr_float_zip_noise": ({c: (noise[c], 2) for c in "RGB"}, 3, 0),     # incompressible: stored chunks
+        "exr_y_float_zip": ({"Y": (smooth["G"], 2)}, 3, 0),                   # one channel -> grey
+        "exr_mixed_extra": ({"R": (smooth["R"], 1), "G": (smooth["G"], 2), "B": (smooth["B"], 1),
+                             "A": (noise["A"], 1), "Z": (noise["R"], 2)}, 3, 0),
+    }
+    for name, (ch, comp, lo) in fx.items():
+        write_exr(os.path.join(OUT, name + ".exr"), ch, comp, lo)
+    return [n + ".exr" for n in fx]
 
 
 def _chunk(typ, body):
@@ -126,7 +228,7 @@ def main():
     for f in os.listdir(OUT):
         if f.endswith((".png", ".jpg", ".exr")):
             os.remove(os.path.join(OUT, f))
-    files = png_fixtures()
+    files = png_fixtures() + exr_fixtures()
     np.savez_compressed(os.path.join(OUT, "decoded.npz"), **decode_with_reference(files))
     print("wrote", len(files), "fixtures to", OUT)
 

@@ -1,11 +1,13 @@
-"""Image decoders of the host loader against the reference's own image class.
+"""Image decoders of the host loader against the reference's own image classes.
 
 Fixtures (tests/golden/make_images.py): small PNGs written by that script's own encoder (grey at
 1/2/4/8/16 bits, grey + alpha, RGB 8/16, RGBA, palette with and without tRNS; every row filter
-type, split IDAT).  Goldens: the texels LDRImage (stbi_load, LDRImage.h:37-44) reads from them,
-dumped by `oracle/_ref/refdriver imgdump` (the reference compiled here).  The loader must
-reproduce them bit for bit, seen through the scene description a parsed <Images> entry
-produces.  JPEG and OpenEXR are outside the loader: refused with
+type, split IDAT) and OpenEXR files from its own writer (HALF / FLOAT, NONE / RLE / ZIPS / ZIP,
+increasing / decreasing line order, one channel, extra channels, half specials).  Goldens: the
+texels LDRImage (stbi_load, LDRImage.h:37-44) and HDRImage (tinyexr LoadEXR, HDRImage.h:45-72)
+read from them, dumped by `oracle/_ref/refdriver imgdump` (the reference compiled here).  The
+loader must reproduce them bit for bit, seen through the scene description a parsed <Images>
+entry produces.  JPEG is outside the loader (a parity gap): refused with
 RTG_ERR_UNSUPPORTED."""
 import ctypes
 import os
@@ -19,7 +21,7 @@ import rtgpu
 
 IMAGES = os.path.join(ob.GOLDEN, "images")
 GOLD = np.load(os.path.join(IMAGES, "decoded.npz"))
-PNG = sorted(f for f in os.listdir(IMAGES) if f.endswith(".png"))
+PNG = sorted(f for f in os.listdir(IMAGES) if f.endswith((".png", ".exr")))
 
 SCENE = """<Scene>
     <Cameras><Camera id="1"><Position>0 0 0</Position><Gaze>0 0 -1</Gaze><Up>0 1 0</Up>
@@ -69,8 +71,8 @@ def test_decoder_matches_reference(tmp_path, name):
 
 
 @pytest.mark.parametrize("name,data", [("a.jpg", b"\xff\xd8\xff\xe0" + bytes(64)),
-                                       ("a.exr", b"\x76\x2f\x31\x01" + bytes(64))])
-def test_jpeg_exr_refused(tmp_path, name, data):
+                                       ("b.exr", b"\x76\x2f\x31\x01" + b"\x02\x02\x00\x00" + bytes(64))])
+def test_jpeg_and_tiled_exr_refused(tmp_path, name, data):
     os.makedirs(tmp_path / "inputs", exist_ok=True)
     (tmp_path / "inputs" / name).write_bytes(data)
     (tmp_path / "s.xml").write_text(SCENE.replace("IMG", name))
