@@ -1279,10 +1279,12 @@ int rtg_copy_part_to_host(rtg_scene* s, const rtg_render_opts* o, const float* d
 // chunk starting at round m are the bands of part (p - m) mod part_count of that chunk (the
 // rotation of part_band), so the chunks together cover exactly part p's rows.  Pixels are
 // keyed by their image position (RNG included): the image is the one-launch image bit for bit.
+// Measured slower than one launch + one copy at every chunk count (2-16 chunks: 0.63-1.15 ms
+// against 0.58 ms per 1080p frame, profiles/r04d_hostpath.jsonl: each chunk's host-side launch
+// work and small grids cost more than the copy they hide), so it runs only on request:
+// RTG_HOST_CHUNKS=<chunks> (A/B).
 constexpr long long kChunkMinPixels = 1ll << 20;
-static bool chunk_disabled() { return std::getenv("RTG_HOST_CHUNKS_OFF") != nullptr; }
-// chunks per frame part (RTG_HOST_CHUNKS: A/B) and whether each chunk's copy goes on the copy
-// stream (default) or on the chunk's own render stream (RTG_HOST_CHUNK_COPY=own: A/B)
+static bool chunk_disabled() { return std::getenv("RTG_HOST_CHUNKS") == nullptr; }
 static int host_chunks() {
     const char* v = std::getenv("RTG_HOST_CHUNKS");
     return v ? std::max(1, std::atoi(v)) : 8;
@@ -1346,6 +1348,20 @@ static int render_chunked(rtg_scene* s, const rtg_render_opts* o, const rtg::Ren
     return RTG_OK;
 }
 
+// The device's view of a page-locked host buffer (rtg_host_alloc / rtg_host_register), or null.
+static void* device_view(void* p) {
+    if (!p) return nullptr;
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return nullptr;
+    }
+    return a.type == hipMemoryTypeHost ? a.devicePointer : nullptr;
+}
+// RTG_HOST_DIRECT=1 (A/B): the kernels write the pixels straight into the caller's page-locked
+// frame over the bus (no device frame, no copy after the render)
+static bool host_direct() { return std::getenv("RTG_HOST_DIRECT") != nullptr; }
+
 // Replaces main.cpp:164-185.  With replicas (rtg_scene_create_multi) replica i renders part
 // i of n on its own stream and copies its rows into the caller's buffers; the renders of all
 // replicas are enqueued before any copy (a copy to pageable memory may block the host), then
@@ -1363,6 +1379,23 @@ int rtg_render(rtg_scene* s, const rtg_render_opts* o, float* hdr_rgb, uint8_t* 
     const rtg_camera& cam = s->cameras[o->camera];
     std::vector<rtg_render_opts> ro(n, *o);
     bool whole = false;
+    if (n == 1 && host_direct() && !cam.has_tonemapper && (hdr_rgb || ldr_rgb)) {
+        float* dh = (float*)device_view(hdr_rgb);
+        uint8_t* dl = (uint8_t*)device_view(ldr_rgb);
+        if ((!hdr_rgb || dh) && (!ldr_rgb || dl)) {
+            rtg::DevCamera C;
+            rtg::RenderParams P;
+            int rc = prepare(s, o, C, P);
+            if (rc) return rc;
+            if (P.num_tiles == 0) return RTG_OK;
+            HIP_TRY(hipSetDevice(s->device));
+            rc = launch(s, o, C, P, dh, dl, nullptr, s->stream);
+            if (rc) return rc;
+            HIP_TRY(hipEventRecord(s->done, s->stream));
+            HIP_TRY(hipStreamSynchronize(s->stream));
+            return RTG_OK;
+        }
+    }
     if (n == 1 && !chunk_disabled() && !(o->flags & (RTG_RENDER_TIMING | RTG_RENDER_COUNT_STATS)) &&
         (long long)cam.width * cam.height >= kChunkMinPixels && !(cam.has_tonemapper)) {
         rtg::DevCamera C;

@@ -145,7 +145,9 @@ DEV f3 resolve_sum(f3 base, int flags, f3 sum) {
 //               summed in light order as k_resolve sums them (a separate instantiation: the
 //               loop costs the one-light kernel 15 %)
 enum { SH_GENERAL = 0, SH_ONE = 1, SH_FUSED = 2, SH_FUSED_N = 3 };
-template <bool STATS, int SK, int MODE, int FEAT = 0, bool FAST = false>
+// FRAME (SH_FUSED / SH_FUSED_N only; RTG_FRAME_KERNEL): the lane also traces its camera ray
+// (k_primary's walk) instead of reading the hit buffers -- the whole sample pass in one launch
+template <bool STATS, int SK, int MODE, int FEAT = 0, bool FAST = false, bool FRAME = false>
 __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(FEAT))
                                                    : RTG_SHADE_WAVES) void k_shade(const DevScene S, const DevCamera C,
                                                                                    const RenderParams P,
@@ -164,7 +166,19 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
     const int pixel = valid ? px + py * C.width : 0;
     const int i = valid ? crow * C.width + px : 0;
     const uint64_t key = root_key(P.seed, pixel, sample);
-    const int obj = valid ? W.hit_obj[i] : -1;
+    static_assert(!FRAME || MODE >= SH_FUSED, "the frame kernel is the fused layout's");
+    Hit fh;                          // FRAME: the camera ray's hit
+    fh.obj = -1;
+    if constexpr (FRAME) {
+        if (valid) {
+            float mbt;
+            Ray cr = camera_ray(C, px, py, key, mbt);
+            cn.cam();
+            trace<false, STATS, FEAT, RTG_PRIMARY_PACKET != 0 && !(FEAT & FEAT_BIGLEAF)>(S, cr, mbt, INFINITY, INFINITY,
+                                                                                           fh, cn);
+        }
+    }
+    const int obj = FRAME ? fh.obj : (valid ? W.hit_obj[i] : -1);
     // lanes that need the light loop
     bool lit = false;
     ShadeCtx c;
@@ -186,9 +200,9 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
         } else {
             const DevObject& ob = S.objects[obj];
             Hit h;
-            h.t = W.hit_t[i];
+            h.t = FRAME ? fh.t : W.hit_t[i];
             h.obj = obj;
-            h.face = W.hit_face[i];
+            h.face = FRAME ? fh.face : W.hit_face[i];
             h.o = ray.o;
             c.ob = &ob;
             c.mat = &S.materials[ob.material];
@@ -425,6 +439,7 @@ hipError_t wave_shade(bool stats, int sk, bool one, const DevScene& S, const Dev
 void wave_resolve(const DevCamera& C, const RenderParams& P, int sample, const WaveBufs& W, const PassOut& O,
                   hipStream_t st);
 bool no_fused_shade();
+bool frame_kernel();
 bool wide_bigleaf();
 
 // One traversal variant's pass sequence (instantiated in rtg_wave_a.hip / rtg_wave_b.hip).
@@ -464,10 +479,22 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
                 ordered = true;
             }
         }
-        if (!ordered)
+        // RTG_FRAME_KERNEL (fused layout, no motion blur): one launch per sample pass
+        const bool frame = fused && frame_kernel() && !ordered;
+        if (!ordered && !frame)
             hipLaunchKernelGGL((k_primary<STATS, FEAT>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
         if (e5) (void)hipEventRecord(e5[1], st);
-        if (fused) {
+        if (frame) {
+            if constexpr (!(FEAT & FEAT_BIGLEAF)) {
+                if (one)
+                    hipLaunchKernelGGL((k_shade<STATS, 0, SH_FUSED, FEAT, true, true>), dim3(P.num_tiles), dim3(256), 0,
+                                       st, S, C, P, s, W, O, cnt);
+                else
+                    hipLaunchKernelGGL((k_shade<STATS, 0, SH_FUSED_N, FEAT, true, true>), dim3(P.num_tiles), dim3(256),
+                                       0, st, S, C, P, s, W, O, cnt);
+            }
+            if (e5) (void)hipEventRecord(e5[2], st);
+        } else if (fused) {
             if constexpr (!(FEAT & FEAT_BIGLEAF)) {
                 if (one)
                     hipLaunchKernelGGL((k_shade<STATS, 0, SH_FUSED, FEAT, true>), dim3(P.num_tiles), dim3(256), 0, st, S,

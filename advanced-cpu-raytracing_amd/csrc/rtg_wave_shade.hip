@@ -30,6 +30,12 @@ __global__ __launch_bounds__(256) void k_resolve(const DevCamera C, const Render
 // (experiment; by default they take the cooperative reference walk)
 bool wide_bigleaf() { return std::getenv("RTG_WIDE_BIGLEAF") != nullptr; }
 
+// RTG_FRAME_KERNEL=1: the fused layout's two kernels as one (k_shade<..., FRAME>: A/B)
+bool frame_kernel() {
+    static const bool v = std::getenv("RTG_FRAME_KERNEL") != nullptr;
+    return v;
+}
+
 bool no_fused_shade() {
     static const bool v = std::getenv("RTG_NO_FUSED_SHADE") != nullptr;
     return v;

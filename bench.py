@@ -198,8 +198,12 @@ def measure(render, torch, steps, warmup, barrier, serial=None):
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
+    last = t0
     for k in range(steps):
         render(k)
+        if k % 8 == 7 and time.perf_counter() - last > 20.0:    # long steps (C5): keep the run visibly alive
+            last = time.perf_counter()
+            log(f"step {k + 1}/{steps}")
     measure.issue_s = time.perf_counter() - t0    # host time to issue the steps (launch-bound if ~elapsed)
     torch.cuda.synchronize()
     barrier()

@@ -211,11 +211,12 @@ def test_cli_devices(tmp_path):
 
 @pytest.mark.parametrize("part,rows", [((0, 1), (0, 0)), ((1, 2), (0, 0)), ((2, 3), (0, 0)), ((5, 8), (0, 0)),
                                        ((0, 1), (100, 1000)), ((3, 4), (37, 1080))])
-def test_overlapped_host_path_equals_one_launch(part, rows, tmp_path, monkeypatch):
-    """rtg_render's overlapped host path (frames of >= 1 M pixels: row chunks of whole band
-    rounds on two streams, each chunk's rows copied while the next render) writes exactly the
-    rows and bits of the one-launch path (RTG_HOST_CHUNKS_OFF), for whole frames, parts of a
-    partition and row ranges."""
+def test_host_path_variants_equal_one_launch(part, rows, tmp_path, monkeypatch):
+    """rtg_render's host-path variants write exactly the rows and bits of the default one-launch
+    path (render + copy), for whole frames, parts of a partition and row ranges: the chunked
+    path (RTG_HOST_CHUNKS: row chunks of whole band rounds on two streams, each chunk's rows
+    copied while the next renders) and direct writes into a page-locked frame
+    (RTG_HOST_DIRECT)."""
     import scenes
     xml = scenes.synthetic_heightfield(str(tmp_path), K=10082, width=1920, height=1080)
     old = os.getcwd()
@@ -224,10 +225,20 @@ def test_overlapped_host_path_equals_one_launch(part, rows, tmp_path, monkeypatc
         hs = rtgpu.HostScene(xml)
         ds = rtgpu.DeviceScene(hs, 0)
         init = lambda: (np.full((1080, 1920, 3), -1.0, np.float32), np.full((1080, 1920, 3), 7, np.uint8))  # noqa: E731
-        a = ds.render(0, rows=rows, part=part, seed=3, out=init())
-        monkeypatch.setenv("RTG_HOST_CHUNKS_OFF", "1")
         b = ds.render(0, rows=rows, part=part, seed=3, out=init())
+        monkeypatch.setenv("RTG_HOST_CHUNKS", "8")
+        a = ds.render(0, rows=rows, part=part, seed=3, out=init())
+        monkeypatch.delenv("RTG_HOST_CHUNKS")
+        monkeypatch.setenv("RTG_HOST_DIRECT", "1")
+        ph, pl = rtgpu.PinnedArray((1080, 1920, 3), "float32"), rtgpu.PinnedArray((1080, 1920, 3), "uint8")
+        ph.array[...] = -1.0
+        pl.array[...] = 7
+        c = ds.render(0, rows=rows, part=part, seed=3, out=(ph.array, pl.array))
+        c = (c[0].copy(), c[1].copy())
+        ph.close()
+        pl.close()
     finally:
         os.chdir(old)
     assert _same(a[0], b[0]) and _same(a[1], b[1])
-    assert (a[1] != 7).any()
+    assert _same(c[0], b[0]) and _same(c[1], b[1])
+    assert (b[1] != 7).any()

@@ -1,7 +1,7 @@
 """rtg_render's host-buffer path (the CLI's, main.cpp:164-195) on the headline frame: one frame at
-a time into page-locked frames, with the overlapped chunked path (rtg_api.cpp render_chunked) at
-several chunk counts, with each chunk's copy on its render stream, and with chunking off -- beside
-the device-resident frame (rtg_render_device + synchronize) it is compared with.
+a time into page-locked frames: render + copy (the default), the kernels writing into the frame
+directly (RTG_HOST_DIRECT), and the chunked path (RTG_HOST_CHUNKS, rtg_api.cpp render_chunked) --
+beside the device-resident frame (rtg_render_device + synchronize) it is compared with.
 Usage: python tools/diag_hostpath.py [frames]"""
 import json
 import os
@@ -38,14 +38,13 @@ def main():
     def host():
         ds.render(0, out=(None, pl.array))
 
-    cases = [("device", {}, dev), ("host_off", {"RTG_HOST_CHUNKS_OFF": "1"}, host)]
-    for c in (2, 4, 8, 16):
+    cases = [("device", {}, dev), ("host", {}, host), ("host_direct", {"RTG_HOST_DIRECT": "1"}, host)]
+    for c in (2, 4):
         cases.append((f"host_chunks{c}", {"RTG_HOST_CHUNKS": str(c)}, host))
-        cases.append((f"host_chunks{c}_own", {"RTG_HOST_CHUNKS": str(c), "RTG_HOST_CHUNK_COPY": "own"}, host))
     ref = None
     for rep in range(2):
         for name, env, fn in cases:
-            for k in ("RTG_HOST_CHUNKS_OFF", "RTG_HOST_CHUNKS", "RTG_HOST_CHUNK_COPY"):
+            for k in ("RTG_HOST_CHUNKS", "RTG_HOST_CHUNK_COPY", "RTG_HOST_DIRECT"):
                 os.environ.pop(k, None)
             os.environ.update(env)
             for _ in range(3):

@@ -51,11 +51,21 @@ for s in "${steps[@]}"; do
         if [ $rc -ne 0 ]; then exit $rc; fi
       done ;;
     configs)
-      for c in c2 c3 c3ton c4 c5; do
+      for c in c2 c3 c3ton c4; do
         run cfg_$c 300 python bench.py --config $c --no-cpu-baseline $extra
-      done ;;
+      done
+      run cfg_c5 400 python bench.py --config c5 --steps 5 --warmup 1 --no-cpu-baseline $extra ;;
     ab)
       run ab 1500 bash tools/gpu_ab_head.sh $tag/ab $AB_LIBS ;;
+    envbench)
+      # the headline bench (with gather / host-frame / parts / ordered extras) once per setting in
+      # $ENV_AB ("base" or NAME=VALUE[,NAME=VALUE])
+      for setting in $ENV_AB; do
+        name=${setting//[=,]/_}
+        envs=()
+        [ "$setting" != base ] && IFS=, read -ra envs <<< "$setting"
+        run envbench_$name 300 env "${envs[@]}" python bench.py --no-sweep --no-cpu-baseline $extra
+      done ;;
     py:*)
       t=${s#py:}
       run $t 600 python -u tools/$t.py ;;
