@@ -1237,7 +1237,10 @@ int rtg_render_device(rtg_scene* s, const rtg_render_opts* o, float* d_hdr, uint
     HIP_TRY(hipSetDevice(s->device));
     rc = launch(s, o, C, P, d_hdr, d_ldr, d_accum, (hipStream_t)stream);
     if (rc) return rc;
-    HIP_TRY(hipEventRecord(s->done, (hipStream_t)stream));
+    // (RTG_NO_DONE_EVENT=1, A/B: no completion marker; rtg_scene_stats then sees only renders
+    // whose stream was synchronised)
+    static const bool no_done = std::getenv("RTG_NO_DONE_EVENT") != nullptr;
+    if (!no_done || (o->flags & RTG_RENDER_COUNT_STATS)) HIP_TRY(hipEventRecord(s->done, (hipStream_t)stream));
     return RTG_OK;
 }
 
@@ -1358,9 +1361,15 @@ static void* device_view(void* p) {
     }
     return a.type == hipMemoryTypeHost ? a.devicePointer : nullptr;
 }
-// RTG_HOST_DIRECT=1 (A/B): the kernels write the pixels straight into the caller's page-locked
-// frame over the bus (no device frame, no copy after the render)
-static bool host_direct() { return std::getenv("RTG_HOST_DIRECT") != nullptr; }
+// Page-locked caller frames (rtg_host_alloc / rtg_host_register, as the CLIs and the shared
+// frame of multigpu.py allocate them): the kernels write the pixels straight into the frame over
+// the bus -- no device frame and no copy after the render, the writes overlap the rendering
+// (headline 1080p frame: 0.53 -> 0.46 ms per frame, profiles/r04e_hostpath.jsonl).  Pageable
+// frames take the render + copy path.  RTG_HOST_DIRECT=0: render + copy always (A/B).
+static bool host_direct() {
+    const char* v = std::getenv("RTG_HOST_DIRECT");
+    return !v || std::strcmp(v, "0") != 0;
+}
 
 // Replaces main.cpp:164-185.  With replicas (rtg_scene_create_multi) replica i renders part
 // i of n on its own stream and copies its rows into the caller's buffers; the renders of all

@@ -11,7 +11,7 @@ A step = one full 1920x1080 frame (one sample pass) traced and shaded, inputs (s
 resident in HBM.  With N ranks every frame is partitioned (multigpu.py): rank r renders the
 8-row bands dealt round-robin (rotated one slot per round) into its own HBM -- no collective on the data path (the
 barriers around the timed region and the max-over-ranks of the elapsed time are the only
-collectives).  The steps rotate over 8 scene replicas, each on its own stream ("frames in
+collectives).  The steps rotate over 16 scene replicas, each on its own stream ("frames in
 flight"), so a frame's kernels overlap the next frames' -- a part of 1/N of one frame alone
 is too small a grid to keep a GPU busy; `config.serial` times the same steps
 on one stream, one frame after the other.  `value` = rays of the frames x steps /
@@ -35,9 +35,11 @@ import time
 # part of 1/N of a frame is too small a grid to fill the GPU on its own: DESIGN.md §6).  Each
 # stream needs its own hardware queue (HIP's default is 4 per process, and streams beyond the
 # queues share them and serialise: part (0, 8) 0.14 ms with 4 queues, 0.070 with 9;
-# profiles/r03o_parts_queues.txt); raised to 9 -- the replicas' 8 streams + torch's own; 9
-# measured faster than 12 or 16 -- before the HIP runtime starts.
-HW_QUEUES = int(os.environ.get("RTG_BENCH_HW_QUEUES", "9"))
+# profiles/r03o_parts_queues.txt); raised to 17 -- the replicas' 16 streams + torch's own --
+# before the HIP runtime starts.  Round 4: 16 frames in flight instead of 8 (a part of 1/8 of the
+# frame 0.0522 -> 0.0501 ms, the full frame unchanged: profiles/r04f_parts_ab.jsonl).
+FRAMES_IN_FLIGHT = 16
+HW_QUEUES = int(os.environ.get("RTG_BENCH_HW_QUEUES", str(FRAMES_IN_FLIGHT + 1)))
 if "--help" not in sys.argv and "-h" not in sys.argv:
     # (RTG_BENCH_QUEUES_AS_GIVEN=1: keep the environment's value, for the A/B)
     if int(os.environ.get("GPU_MAX_HW_QUEUES", "0") or 0) < HW_QUEUES and not os.environ.get("RTG_BENCH_QUEUES_AS_GIVEN"):
@@ -68,7 +70,7 @@ def parse():
     p.add_argument("--config", default="headline", choices=["headline", "c2", "c3", "c3ton", "c4", "c5"],
                    help="BASELINE.json configuration (c2-c5: one frame = all camera samples)")
     p.add_argument("--inflight", type=int, default=0,
-                   help="frames in flight (scene replicas / streams the steps rotate over); 0 = 8, "
+                   help="frames in flight (scene replicas / streams the steps rotate over); 0 = 16, "
                         "1 for c5")
     return p.parse_args()
 
@@ -483,7 +485,7 @@ def main():
         # (C5's 4K x 64 spp frames fill the GPU on their own and its ray-tree levels take ~10 GB
         # per replica: one; the others 8 -- C3 1 892 -> 4 153 Mrays/s, C4 1 653 -> 2 102, C2
         # 7 792 -> 14 083: a frame's slowest waves no longer idle the GPU, profiles/r03v)
-        F = args.inflight or (1 if args.config == "c5" else 8)
+        F = args.inflight or (1 if args.config == "c5" else FRAMES_IN_FLIGHT)
         streams = [torch.cuda.Stream() for _ in range(F if F > 1 else 0)]
         reps = [(ds, hdr, ldr, streams[0].cuda_stream if F > 1 else sptr)]
         for k in range(1, F):

@@ -229,7 +229,7 @@ def test_host_path_variants_equal_one_launch(part, rows, tmp_path, monkeypatch):
         monkeypatch.setenv("RTG_HOST_CHUNKS", "8")
         a = ds.render(0, rows=rows, part=part, seed=3, out=init())
         monkeypatch.delenv("RTG_HOST_CHUNKS")
-        monkeypatch.setenv("RTG_HOST_DIRECT", "1")
+        monkeypatch.delenv("RTG_HOST_DIRECT", raising=False)        # the default for page-locked frames
         ph, pl = rtgpu.PinnedArray((1080, 1920, 3), "float32"), rtgpu.PinnedArray((1080, 1920, 3), "uint8")
         ph.array[...] = -1.0
         pl.array[...] = 7

@@ -1,6 +1,6 @@
 """rtg_render's host-buffer path (the CLI's, main.cpp:164-195) on the headline frame: one frame at
-a time into page-locked frames: render + copy (the default), the kernels writing into the frame
-directly (RTG_HOST_DIRECT), and the chunked path (RTG_HOST_CHUNKS, rtg_api.cpp render_chunked) --
+a time into page-locked frames: the kernels writing into the frame directly (the default for
+page-locked frames), render + copy (RTG_HOST_DIRECT=0), and the chunked path (RTG_HOST_CHUNKS, rtg_api.cpp render_chunked) --
 beside the device-resident frame (rtg_render_device + synchronize) it is compared with.
 Usage: python tools/diag_hostpath.py [frames]"""
 import json
@@ -38,7 +38,7 @@ def main():
     def host():
         ds.render(0, out=(None, pl.array))
 
-    cases = [("device", {}, dev), ("host", {}, host), ("host_direct", {"RTG_HOST_DIRECT": "1"}, host)]
+    cases = [("device", {}, dev), ("host_copy", {"RTG_HOST_DIRECT": "0"}, host), ("host_direct", {}, host)]
     for c in (2, 4):
         cases.append((f"host_chunks{c}", {"RTG_HOST_CHUNKS": str(c)}, host))
     ref = None

@@ -3,7 +3,8 @@
 # steps: tests (pytest -m gpu + smoke), slivers (tools/diag_slivers.py), bench, prof (kernel
 # trace of serial frames), pmc (limiter + HBM counter passes, one rocprofv3 --pmc run each),
 # configs (bench --config c2..c5), ab (tools/gpu_ab_head.sh over the libraries in $AB_LIBS,
-# e.g. AB_LIBS="base libpk2.so"), py:<name> (tools/<name>.py).  Every step has its own
+# e.g. AB_LIBS="base libpk2.so"), py:<name> (tools/<name>.py), envbench / envpy:<name> (bench.py /
+# tools/<name>.py once per setting of $ENV_AB).  Every step has its own
 # time limit; the first failing step ends the script.
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
@@ -65,6 +66,15 @@ for s in "${steps[@]}"; do
         envs=()
         [ "$setting" != base ] && IFS=, read -ra envs <<< "$setting"
         run envbench_$name 300 env "${envs[@]}" python bench.py --no-sweep --no-cpu-baseline $extra
+      done ;;
+    envpy:*)
+      # tools/<name>.py once per setting in $ENV_AB
+      t=${s#envpy:}
+      for setting in $ENV_AB; do
+        name=${setting//[=,]/_}
+        envs=()
+        [ "$setting" != base ] && IFS=, read -ra envs <<< "$setting"
+        run ${t}_$name 300 env "${envs[@]}" python -u tools/$t.py
       done ;;
     py:*)
       t=${s#py:}
