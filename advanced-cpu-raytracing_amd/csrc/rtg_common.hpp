@@ -1570,6 +1570,120 @@ DEV bool trace_closest_pk(const DevScene& S, const Ray& r, Hit& h, Cnt<STATS>& c
     return sure;
 }
 
+// The same closest-hit walk per lane (incoherent rays: the ray trees' secondary levels): each
+// lane walks the any-hit tree nearest child first with its own LDS stack of node indices (a
+// popped node is culled child by child at the lane's best t then), vector loads of the 128-B
+// node and 48-B face records.  Same certificate as walk_closest_pk; false: reference walk.
+#ifndef RTG_CL_STACK
+#define RTG_CL_STACK 16
+#endif
+template <bool STATS>
+DEV bool walk_closest_lane(const DevScene& S, int node, const int k, const Ray& lr, const RayRcp& q, const SlabRay& sr,
+                           ClosestState& B, Cnt<STATS>& c) {
+    __shared__ int cl_stack[RTG_CL_STACK][256];
+    const int tid = threadIdx.x;
+    int sp = 0;
+    int steps = 0;
+    while (true) {
+        if (++steps > RTG_PK_MAX_STEPS) return false;
+        const WNode* N = S.anodes + node;
+        const float4 lox = N->lox, hix = N->hix, loy = N->loy, hiy = N->hiy, loz = N->loz, hiz = N->hiz;
+        const int4 ch = N->child, lf = N->leaf;
+        c.ewnode();
+        const float minTc = cull_limit(B.bestT);
+        float tn[4];
+        bool h[4], hi[4];
+        h[0] = slab_cons2(lox.x, loy.x, loz.x, hix.x, hiy.x, hiz.x, sr, minTc, tn[0], hi[0]);
+        h[1] = slab_cons2(lox.y, loy.y, loz.y, hix.y, hiy.y, hiz.y, sr, minTc, tn[1], hi[1]);
+        h[2] = slab_cons2(lox.z, loy.z, loz.z, hix.z, hiy.z, hiz.z, sr, minTc, tn[2], hi[2]);
+        h[3] = slab_cons2(lox.w, loy.w, loz.w, hix.w, hiy.w, hiz.w, sr, minTc, tn[3], hi[3]);
+        const int cidx[4] = {ch.x, ch.y, ch.z, ch.w};
+        const int lidx[4] = {lf.x, lf.y, lf.z, lf.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (cidx[j] == WCHILD_EMPTY || cidx[j] >= 0) continue;
+            if (hi[j] & !h[j]) B.cullMin = fminf(B.cullMin, tn[j]);
+            if (!h[j]) continue;
+            const int first = lidx[j] >> 8, cnt = lidx[j] & 255;
+            for (int e = first; e < first + cnt; ++e) {
+                const float4* R = S.ahtris + 3 * (size_t)e;
+                c.template tri<false>();
+                float t;
+                if (!tri_test_fast_rec(R, lr, INFINITY, t)) continue;
+                const float4 r0 = R[0], r1 = R[1];
+                const int f = __float_as_int(r1.w);
+                if (!hit_less(t, k, f, B.bestT, B.bestK, B.bestF)) continue;
+                const int ref = __float_as_int(r0.w);
+                const float4 a = S.nodes[2 * ref], b = S.nodes[2 * ref + 1];
+                if (box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, next_up(t))) {
+                    B.bestT = t; B.bestK = k; B.bestF = f;
+                } else if (box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, INFINITY) &&
+                           hit_less(t, k, f, B.hidT, B.hidK, B.hidF)) {
+                    B.hidT = t; B.hidK = k; B.hidF = f;
+                }
+            }
+        }
+        const float minTc2 = cull_limit(B.bestT);
+        int next = -1;
+        float nextT = INFINITY;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (cidx[j] < 0) continue;
+            if (!(h[j] & (tn[j] < minTc2))) {
+                if (hi[j]) B.cullMin = fminf(B.cullMin, tn[j]);
+                continue;
+            }
+            int spill = cidx[j];
+            if (tn[j] < nextT) {
+                spill = next;
+                next = cidx[j];
+                nextT = tn[j];
+            }
+            if (spill >= 0) {
+                if (sp >= RTG_CL_STACK) return false;
+                cl_stack[sp++][tid] = spill;
+            }
+        }
+        if (next >= 0) {
+            node = next;
+            continue;
+        }
+        if (sp == 0) break;
+        node = cl_stack[--sp][tid];
+    }
+    return true;
+}
+
+template <bool STATS, int FEAT>
+DEV bool trace_closest_lane(const DevScene& S, const Ray& r, Hit& h, Cnt<STATS>& c) {
+    static_assert((FEAT & ~FEAT_SPHERE) == 0, "meshes with identity transforms and spheres only");
+    const RayRcp q = ray_rcp(r);
+    if (!q.fast) return false;
+    const SlabRay sr = slab_ray(r, q);
+    ClosestState B;
+    B.bestT = B.hidT = B.cullMin = INFINITY;
+    B.bestK = B.bestF = B.hidK = B.hidF = 0x7FFFFFFF;
+    for (int k = 0; k < S.num_objects; ++k) {
+        const DevObject& ob = S.objects[k];
+        c.obj();
+        if ((FEAT & FEAT_SPHERE) && ob.kind == OBJ_SPHERE) {
+            c.sph();
+            float t;
+            if (sphere_t(ob, r, B.bestT, t)) { B.bestT = t; B.bestK = k; B.bestF = -1; }
+            continue;
+        }
+        if (ob.aroot < 0) return false;
+        if (!walk_closest_lane<STATS>(S, ob.aroot, k, r, q, sr, B, c)) return false;
+    }
+    if (hit_less(B.hidT, B.hidK, B.hidF, B.bestT, B.bestK, B.bestF)) return false;
+    if (B.bestT < INFINITY && B.cullMin <= B.bestT * (1.0f + 0x1p-16f)) return false;
+    h.t = B.bestT;
+    h.obj = B.bestT < INFINITY ? B.bestK : -1;
+    h.face = B.bestT < INFINITY ? B.bestF : -1;
+    h.o = r.o;
+    return true;
+}
+
 // The same decision on the reference BVH itself, walked from the shadow ray's origin
 // upwards.  A shadow ray starts on the surface it leaves (hit point + eps n), so top-down
 // every ancestor of the origin's leaf is hit and both children are tested at every level;

@@ -52,8 +52,14 @@ __global__ __launch_bounds__(256) void k_tree_gen(const DevCamera C, const Rende
     L0.key[i] = key;
 }
 
-template <bool STATS, int FEAT>
-__global__ __launch_bounds__(256, RTG_TRACE_WAVES(FEAT)) void k_tree_trace(const DevScene S, const TreeLevel L, const int level,
+// PK: the wave-packet form of the reference walk (k_primary's; coherent rays -- level 0, whose
+// rays are consecutive pixels of a row).  CL: the checked closest-hit walk of the any-hit tree
+// per lane (trace_closest_lane; plain meshes and spheres), the reference walk where it checks out
+#ifndef RTG_CL_WAVES
+#define RTG_CL_WAVES 4
+#endif
+template <bool STATS, int FEAT, bool PK = false, bool CL = false>
+__global__ __launch_bounds__(256, CL ? RTG_CL_WAVES : RTG_TRACE_WAVES(FEAT)) void k_tree_trace(const DevScene S, const TreeLevel L, const int level,
                                                     DevCounters* counters) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     Cnt<STATS> cn;
@@ -65,7 +71,12 @@ __global__ __launch_bounds__(256, RTG_TRACE_WAVES(FEAT)) void k_tree_trace(const
         if (level == 0) cn.cam();
         else cn.sec();
         Hit h;
-        trace<false, STATS, FEAT>(S, r, 0.f, INFINITY, INFINITY, h, cn);
+        bool done = false;
+        if constexpr (CL && (FEAT & ~FEAT_SPHERE) == 0) {
+            done = trace_closest_lane<STATS, FEAT>(S, r, h, cn);
+            if (!done) cn.efallback();
+        }
+        if (!done) trace<false, STATS, FEAT, PK && !(FEAT & FEAT_BIGLEAF)>(S, r, 0.f, INFINITY, INFINITY, h, cn);
         L.t[i] = h.t;
         L.obj[i] = h.obj;
         L.face[i] = h.face;
@@ -548,12 +559,30 @@ static hipError_t ensure_segs(TreeState& T, size_t blocks, int ns) {
 void tree_destroy(TreeState* t) { delete t; }
 
 // One level's trace / shade / shadow / scan launches (rays: L's count, on the host or device).
+// Levels whose closest hits take the packet walk (RTG_TREE_PK_LEVELS, A/B; default 0: every
+// level per lane)
+static int tree_packet_levels() {
+    const char* v = std::getenv("RTG_TREE_PK_LEVELS");
+    return v ? std::atoi(v) : 0;
+}
+
+// RTG_TREE_CLOSEST=1 (A/B): the levels not on the packet walk take the checked closest-hit walk
+// of the any-hit tree per lane
+static bool tree_closest() { return std::getenv("RTG_TREE_CLOSEST") != nullptr; }
+
 template <bool STATS, int FEAT>
 static void level_launches(TreeState& T, const DevScene& S, const DevCamera& C, const RenderParams& P, int s,
                            int level, TreeLevel& L, int blocks, int ns, int* next_n, int cap_next, DevCounters* cnt,
                            hipStream_t st) {
     if (level == 0) hipLaunchKernelGGL(k_tree_gen, dim3(blocks), dim3(256), 0, st, C, P, s, L);
-    hipLaunchKernelGGL((k_tree_trace<STATS, FEAT>), dim3(blocks), dim3(256), 0, st, S, L, level, cnt);
+    const int pkl = tree_packet_levels();
+    const bool cl = tree_closest() && (FEAT & ~FEAT_SPHERE) == 0 && S.anodes && !S.ahb_split;
+    if (level < pkl)
+        hipLaunchKernelGGL((k_tree_trace<STATS, FEAT, true>), dim3(blocks), dim3(256), 0, st, S, L, level, cnt);
+    else if (cl)
+        hipLaunchKernelGGL((k_tree_trace<STATS, FEAT, false, true>), dim3(blocks), dim3(256), 0, st, S, L, level, cnt);
+    else
+        hipLaunchKernelGGL((k_tree_trace<STATS, FEAT>), dim3(blocks), dim3(256), 0, st, S, L, level, cnt);
     if ((T.sk & ~SK_TEX) == 0)
         hipLaunchKernelGGL((k_tree_shade<STATS, SK_TEX>), dim3(blocks), dim3(256), 0, st, S, C, L, level, P, T.G, cnt);
     else
