@@ -85,6 +85,7 @@ struct WaveWork {
     size_t pixels = 0, tiles = 0;
     int slots = 0;
     void* mem = nullptr;
+    void* dq = nullptr;               // deferred-leaf queue + per-pixel hit keys (ensure_defer)
     rtg::WaveBufs W{};
 };
 constexpr int kWorkCtx = 3;
@@ -173,8 +174,10 @@ struct rtg_scene {
             if (e) (void)hipEventDestroy(e);
         if (d_hdr) (void)hipFree(d_hdr);
         if (d_ldr) (void)hipFree(d_ldr);
-        for (auto& w : work)
+        for (auto& w : work) {
             if (w.mem) (void)hipFree(w.mem);
+            if (w.dq) (void)hipFree(w.dq);
+        }
         for (auto& c : chunk_stream)
             if (c) (void)hipStreamDestroy(c);
         if (copy_stream) (void)hipStreamDestroy(copy_stream);
@@ -1095,6 +1098,7 @@ static int prepare(rtg_scene* s, const rtg_render_opts* o, rtg::DevCamera& C, rt
 // shade blocks (queue segments of 256 * slots entries), one allocation.
 static int ensure_wave(WaveWork& ww, size_t pixels, int slots, size_t tiles) {
     if (ww.mem && ww.pixels >= pixels && ww.slots >= slots && ww.tiles >= tiles) return RTG_OK;
+    if (ww.dq) { (void)hipFree(ww.dq); ww.dq = nullptr; }
     if (ww.mem) { (void)hipFree(ww.mem); ww.mem = nullptr; }
     pixels = std::max(pixels, ww.pixels);
     tiles = std::max(tiles, ww.tiles);
@@ -1116,6 +1120,26 @@ static int ensure_wave(WaveWork& ww, size_t pixels, int slots, size_t tiles) {
     ww.pixels = pixels;
     ww.slots = slots;
     ww.tiles = tiles;
+    W.dq_e = nullptr;
+    W.dq_count = nullptr;
+    W.hit_key = nullptr;
+    W.dq_cap = 0;
+    return RTG_OK;
+}
+
+// The deferred-leaf queue of a large-leaf scene's camera walk (WaveBufs dq_*, hit_key): one
+// entry per pixel of capacity (an entry that does not fit is tested in the walk).
+static int ensure_defer(WaveWork& ww, size_t pixels) {
+    if (ww.dq && ww.W.dq_cap >= (int)pixels) return RTG_OK;
+    if (ww.dq) { (void)hipFree(ww.dq); ww.dq = nullptr; }
+    const size_t cap = std::max<size_t>(pixels, 1024);
+    const size_t bytes = 256 + pixels * 8 + cap * 48;
+    HIP_TRY(hipMalloc(&ww.dq, bytes));
+    char* b = (char*)ww.dq;
+    ww.W.dq_count = (int*)b;
+    ww.W.hit_key = (unsigned long long*)(b + 256);
+    ww.W.dq_e = (float4*)(b + 256 + pixels * 8);
+    ww.W.dq_cap = (int)cap;
     return RTG_OK;
 }
 
@@ -1203,6 +1227,7 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
         const size_t rows = (size_t)P.part_rows;
         int rc = ensure_wave(ww, rows * C.width, s->num_slots, (size_t)P.num_tiles);
         if (rc) return rc;
+
         rtg::WaveBufs W = ww.W;
         W.num_slots = s->num_slots;
         if (P.accum_only) W.accum = (float4*)d_accum;
@@ -1214,6 +1239,14 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
                 W = ww.W;
                 W.num_slots = s->num_slots;
             }
+        }
+        if ((s->feat & rtg::FEAT_BIGLEAF) && !stats && rtg::defer_leaves()) {
+            rc = ensure_defer(ww, rows * C.width);
+            if (rc) return rc;
+            W.dq_e = ww.W.dq_e;
+            W.dq_count = ww.W.dq_count;
+            W.hit_key = ww.W.hit_key;
+            W.dq_cap = ww.W.dq_cap;
         }
         int layout = rtg::LAYOUT_WAVE;
         HIP_TRY(rtg::launch_wave(ds, C, P, W, d_hdr, d_ldr, s->counters.p, stats, s->feat, s->shade_sk, stream, ev,

@@ -673,9 +673,34 @@ DEV int wave_min_int(int v) {
 // fallback as wave-uniform branches) and the slab test's exact fallback as a wave-uniform
 // branch; lanes outside their own walk take no part in either fallback.  SC = false: round 2's
 // form (vector loads of the uniform address, per-lane face tests).
-template <bool ANY, bool STATS, bool SC = false>
+// Deferred large leaves (FEAT_BIGLEAF scenes, camera walk of production renders; k_bigleaf /
+// k_hitfix in rtg_wave.hpp).  A lane that reaches a leaf of more than kDeferLeaf faces appends
+// (its local ray, minT at entry, the leaf, its object, its pixel) to a queue and walks on
+// without lowering minT.  Exact: the walk then visits a superset of the reference's boxes (its
+// minT never drops below the reference's: only the deferred leaves' acceptances are missing
+// from it, and every face the reference accepts elsewhere it accepts too), so the minimum in
+// (t, object, face) order over its accepted faces and the deferred leaves' faces with t below
+// their entry minT is at or below the reference's answer h; a candidate below h was never
+// reached by the reference, i.e. it was culled at a minT above its t, so its own leaf box
+// enters after t (hit before its box: rounding only).  Hence a winner whose leaf box passes at
+// next_up(t) IS h; k_hitfix checks exactly that and runs the reference walk otherwise.
+constexpr int kDeferLeaf = 16;
+struct DeferCtx {
+    float4* e;
+    int* count;
+    int cap;
+    int ray;                          // the pixel's work-buffer index
+    bool deferred;                    // this lane appended an entry
+};
+// (t, object, face) as one 64-bit key: t > 0 orders like its bits; objects < 2^12, faces < 2^20
+// (defer_ok); a sphere's face field is all ones
+DEV uint64_t obj_key(float t, int k, int f) {
+    return ((uint64_t)__float_as_uint(t) << 32) | ((uint64_t)(uint32_t)k << 20) | (uint64_t)((uint32_t)f & 0xFFFFFu);
+}
+
+template <bool ANY, bool STATS, bool SC = false, bool DEFER = false>
 DEV bool walk_bvh_packet(const DevScene& S, const int begin, const int end, const Ray& r, float& minT, int& hitFace,
-                         float limit, Cnt<STATS>& c) {
+                         float limit, Cnt<STATS>& c, DeferCtx* dc = nullptr, int k = 0) {
     bool hit = false;
     const RayRcp q = ray_rcp(r);
     const int kDone = 0x7FFFFFFF;
@@ -732,6 +757,26 @@ DEV bool walk_bvh_packet(const DevScene& S, const int begin, const int end, cons
                     const int2 e = S.node_ext[i];
                     first = __builtin_amdgcn_readfirstlane(e.x);
                     cnt = __builtin_amdgcn_readfirstlane(e.y);
+                }
+                if constexpr (DEFER) {
+                    if (cnt > kDeferLeaf) {
+                        // one atomic per wave for the lanes that reached the leaf
+                        const uint64_t m = __ballot(pass);
+                        const int lane = threadIdx.x & 63, lead = __ffsll((long long)m) - 1;
+                        int base = 0;
+                        if (lane == lead) base = atomicAdd(dc->count, __popcll(m));
+                        base = __shfl(base, lead);
+                        const int slot = base + __popcll(m & ((1ull << lane) - 1ull));
+                        if (pass && slot < dc->cap) {
+                            float4* q = dc->e + 3 * (size_t)slot;
+                            q[0] = make_float4(r.o.x, r.o.y, r.o.z, minT);
+                            q[1] = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(dc->ray));
+                            q[2] = make_float4(__int_as_float(first), __int_as_float(cnt), __int_as_float(k), 0.f);
+                            dc->deferred = true;
+                            pass = false;                // queued: no test here, minT unchanged
+                        }
+                        // (a lane whose entry did not fit tests the leaf below)
+                    }
                 }
                 for (int f = first; f < first + cnt; ++f) {
                     if constexpr (SC) {
@@ -825,8 +870,9 @@ struct Hit {
 // bbox test fails leaves its offset on the ray origin (instancedMesh.cpp:18-60).
 // FEAT (scene features the caller guarantees absent when the bit is clear) lets the
 // traversal kernels drop whole code paths -- and their registers -- for plain scenes.
-template <bool ANY, bool STATS, int FEAT = FEAT_ALL, bool PK = false>
-DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit, Hit& h, Cnt<STATS>& c) {
+template <bool ANY, bool STATS, int FEAT = FEAT_ALL, bool PK = false, bool DEFER = false>
+DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit, Hit& h, Cnt<STATS>& c,
+               DeferCtx* dc = nullptr) {
     h.t = minT;
     h.obj = -1;
     h.face = -1;
@@ -884,8 +930,8 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
         float t = h.t;
         bool found;
         if constexpr (PK)
-            found = walk_bvh_packet<ANY, STATS, RTG_PRIMARY_PACKET == 2>(S, ob.node_begin, ob.node_end, lr, t, face,
-                                                                           limit, c);
+            found = walk_bvh_packet<ANY, STATS, RTG_PRIMARY_PACKET == 2, DEFER>(S, ob.node_begin, ob.node_end, lr, t,
+                                                                                  face, limit, c, dc, k);
         else found = walk_bvh<ANY, STATS, (FEAT & FEAT_BIGLEAF) != 0>(S, ob.node_begin, ob.node_end, lr, t, face, limit, c);
         if (found) {
             h.t = t; h.obj = k; h.face = face; h.o = r.o;

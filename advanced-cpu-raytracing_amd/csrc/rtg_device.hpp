@@ -226,6 +226,13 @@ struct WaveBufs {
     // and its light term + pixel index, so k_shadow finishes the pixel itself (no k_resolve)
     float4* __restrict__ q_pay;
     int num_slots;                      // lights per pixel
+    // large-leaf scenes (FEAT_BIGLEAF), production renders: the camera walk defers each large
+    // leaf it reaches to a queue of (ray, leaf, minT at entry) entries, 3 float4 each, tested by
+    // k_bigleaf; per pixel the 64-bit (t, object, face) key of the best hit so far
+    float4* __restrict__ dq_e;
+    int* __restrict__ dq_count;
+    unsigned long long* __restrict__ hit_key;
+    int dq_cap;
 };
 
 // One level of the wavefront ray tree (rtg_tree.hip): rays, their hits, the shading node

@@ -31,7 +31,7 @@ enum { BASE_FINAL = 1, BASE_ADD_ZERO = 2 };
 #ifndef RTG_ORD_WAVES
 #define RTG_ORD_WAVES RTG_WIDE_WAVES_PLAIN
 #endif
-template <bool STATS, int FEAT, int ORD = 0>
+template <bool STATS, int FEAT, int ORD = 0, bool DEFER = false>
 __global__ __launch_bounds__(256, ORD ? RTG_ORD_WAVES : RTG_TRACE_WAVES(FEAT)) void k_primary(
     const DevScene S, const DevCamera C, const RenderParams P, const int sample, const WaveBufs W,
     DevCounters* counters) {
@@ -53,6 +53,17 @@ __global__ __launch_bounds__(256, ORD ? RTG_ORD_WAVES : RTG_TRACE_WAVES(FEAT)) v
                 cn.efallback();
                 trace<false, STATS, FEAT>(S, ray, mbTime, INFINITY, INFINITY, h, cn);
             }
+        } else if constexpr (DEFER) {
+            // large leaves deferred to k_bigleaf; k_hitfix settles the pixel (rtg_common.hpp DeferCtx)
+            DeferCtx dc{W.dq_e, W.dq_count, W.dq_cap, crow * C.width + px, false};
+            trace<false, STATS, FEAT, true, true>(S, ray, mbTime, INFINITY, INFINITY, h, cn, &dc);
+            if (dc.deferred) {
+                const int i = crow * C.width + px;
+                W.hit_key[i] = h.obj >= 0 ? obj_key(h.t, h.obj, h.face) : ~0ull;
+                W.hit_obj[i] = -2;                         // pending
+                flush_counters<STATS>(cn, counters);
+                return;
+            }
         } else {
             trace<false, STATS, FEAT, RTG_PRIMARY_PACKET != 0 && !(FEAT & FEAT_BIGLEAF)>(S, ray, mbTime, INFINITY,
                                                                                        INFINITY, h, cn);
@@ -63,6 +74,82 @@ __global__ __launch_bounds__(256, ORD ? RTG_ORD_WAVES : RTG_TRACE_WAVES(FEAT)) v
         W.hit_face[i] = h.face;
     }
     flush_counters<STATS>(cn, counters);
+}
+
+// The deferred large leaves: one wave per queue entry (grid-stride), its lanes testing the leaf's
+// faces against the entry's local ray at the minT the walk had at the leaf (IntersectFace's
+// acceptance t < minT: the faces the reference's sequential loop could keep), the (t, object,
+// face) minimum folded into the pixel's key with one 64-bit atomic min.
+template <int FEAT>
+__global__ __launch_bounds__(256) void k_bigleaf(const DevScene S, const WaveBufs W) {
+    const int n = min(*W.dq_count, W.dq_cap);
+    const int lane = threadIdx.x & 63;
+    for (int e = (int)((blockIdx.x * 256u + threadIdx.x) >> 6); e < n; e += gridDim.x * 4) {
+        const float4 a = W.dq_e[3 * (size_t)e], b = W.dq_e[3 * (size_t)e + 1], q = W.dq_e[3 * (size_t)e + 2];
+        Ray lr;
+        lr.o = mk(a.x, a.y, a.z);
+        lr.d = mk(b.x, b.y, b.z);
+        const float minT = a.w;
+        const int ray = __float_as_int(b.w), first = __float_as_int(q.x), cnt = __float_as_int(q.y);
+        const int k = __float_as_int(q.z);
+        uint64_t best = ~0ull;
+        for (int f = first + lane; f < first + cnt; f += 64) {
+            float t;
+            if (tri_test_fast(S, f, lr, minT, t)) {
+                const uint64_t key = obj_key(t, k, f);
+                best = key < best ? key : best;
+            }
+        }
+        best = wave_min_key(best, __ballot(1));
+        if (lane == 0 && best != ~0ull) atomicMin(&W.hit_key[ray], (unsigned long long)best);
+    }
+}
+
+// A pending pixel's hit from its key, checked: the winner's reference leaf box (and an
+// instance's world box) must pass the exact slab test at next_up(t) -- else the reference walk
+// decides (rtg_common.hpp DeferCtx).
+template <int FEAT>
+__global__ __launch_bounds__(256) void k_hitfix(const DevScene S, const DevCamera C, const RenderParams P,
+                                                const int sample, const WaveBufs W) {
+    int px, py, crow;
+    tile_pixel(P, px, py, crow);
+    if (px >= C.width || py >= P.row_end) return;
+    const int i = crow * C.width + px;
+    if (W.hit_obj[i] != -2) return;
+    const uint64_t key = W.hit_key[i];
+    const int pixel = px + py * C.width;
+    float mbTime;
+    Ray ray = camera_ray(C, px, py, root_key(P.seed, pixel, sample), mbTime);
+    Hit h;
+    h.t = INFINITY;
+    h.obj = -1;
+    h.face = -1;
+    bool sure = true;
+    if (key != ~0ull) {
+        h.t = __uint_as_float((uint32_t)(key >> 32));
+        h.obj = (int)((key >> 20) & 0xFFFu);
+        const int f = (int)(key & 0xFFFFFu);
+        const DevObject& ob = S.objects[h.obj];
+        if (ob.kind == OBJ_SPHERE) {
+            h.face = -1;
+        } else {
+            h.face = f;
+            const float up = next_up(h.t);
+            if (ob.kind == OBJ_INSTANCE)
+                sure &= box_hit(ob.bmin[0], ob.bmin[1], ob.bmin[2], ob.bmax[0], ob.bmax[1], ob.bmax[2], ray, up);
+            const Ray lr = (FEAT & FEAT_XFORM) ? trav_ray(ob, ray, mbTime) : ray;
+            const int leaf = S.face_leaf[f];
+            const float4 a = S.nodes[2 * leaf], b = S.nodes[2 * leaf + 1];
+            sure &= box_hit(a.x, a.y, a.z, a.w, b.x, b.y, lr, up);
+        }
+    }
+    if (!sure) {
+        Cnt<false> cn;
+        trace<false, false, FEAT>(S, ray, mbTime, INFINITY, INFINITY, h, cn);
+    }
+    W.hit_t[i] = h.t;
+    W.hit_obj[i] = h.obj;
+    W.hit_face[i] = h.face;
 }
 
 // wave-aggregated append to the block's queue segment: ballot + mbcnt rank, one LDS
@@ -440,6 +527,7 @@ void wave_resolve(const DevCamera& C, const RenderParams& P, int sample, const W
                   hipStream_t st);
 bool no_fused_shade();
 bool frame_kernel();
+bool defer_leaves();
 bool wide_bigleaf();
 
 // One traversal variant's pass sequence (instantiated in rtg_wave_a.hip / rtg_wave_b.hip).
@@ -481,7 +569,20 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
         }
         // RTG_FRAME_KERNEL (fused layout, no motion blur): one launch per sample pass
         const bool frame = fused && frame_kernel() && !ordered;
-        if (!ordered && !frame)
+        // large-leaf scenes: the camera walk defers large leaves (k_bigleaf, k_hitfix; production
+        // renders only -- counting renders keep the cooperative walk and the reference's counts)
+        bool deferred = false;
+        if constexpr (!STATS && (FEAT & FEAT_BIGLEAF) != 0) {
+            if (!ordered && !frame && W.dq_e && S.face_leaf && S.num_objects < 4096 && S.num_faces < (1 << 20)) {
+                (void)hipMemsetAsync(W.dq_count, 0, sizeof(int), st);
+                hipLaunchKernelGGL((k_primary<STATS, FEAT, 0, true>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s,
+                                   W, cnt);
+                hipLaunchKernelGGL((k_bigleaf<FEAT>), dim3(2048), dim3(256), 0, st, S, W);
+                hipLaunchKernelGGL((k_hitfix<FEAT>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W);
+                deferred = true;
+            }
+        }
+        if (!ordered && !frame && !deferred)
             hipLaunchKernelGGL((k_primary<STATS, FEAT>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
         if (e5) (void)hipEventRecord(e5[1], st);
         if (frame) {

@@ -1,4 +1,6 @@
 // Wavefront shading kernels (k_shade variants, k_resolve) and the pipeline dispatcher.
+#include <cstring>
+
 #include "rtg_wave.hpp"
 
 namespace rtg {
@@ -29,6 +31,13 @@ __global__ __launch_bounds__(256) void k_resolve(const DevCamera C, const Render
 // RTG_WIDE_BIGLEAF=1: shadow rays of large-leaf scenes also take the any-hit wide walk
 // (experiment; by default they take the cooperative reference walk)
 bool wide_bigleaf() { return std::getenv("RTG_WIDE_BIGLEAF") != nullptr; }
+
+// Large leaves of the camera walk deferred to k_bigleaf (production renders of large-leaf scenes;
+// RTG_DEFER=0: the cooperative walk, A/B)
+bool defer_leaves() {
+    const char* v = std::getenv("RTG_DEFER");
+    return !v || std::strcmp(v, "0") != 0;
+}
 
 // RTG_FRAME_KERNEL=1: the fused layout's two kernels as one (k_shade<..., FRAME>: A/B)
 bool frame_kernel() {

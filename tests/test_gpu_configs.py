@@ -153,3 +153,29 @@ def test_large_leaf_cooperative_walk_small(cfg, in_tmp):
     a, _ = ds0.render(0, seed=3)
     b, _ = ds0.render(0, seed=3, flags=rtgpu.RTG_RENDER_FUSED)
     assert np.array_equal(a.view(np.uint32), b.view(np.uint32))
+
+
+@pytest.mark.parametrize("name", ["c3_small", "c4_small", "c3_blob", "berserker", "windmill", "tower", "car_smooth"])
+def test_deferred_large_leaves(name, in_tmp, monkeypatch):
+    """Large-leaf scenes: the camera walk defers its large leaves to k_bigleaf and settles each
+    pixel in k_hitfix (the winner's leaf box checked at next_up(t), rtg_common.hpp DeferCtx) --
+    bit for bit the image of the cooperative reference walk (RTG_DEFER=0) and of the counting
+    render (which never defers)."""
+    if name == "c3_small":
+        xml = scenes.config_c3(in_tmp, K=20000, width=320, height=180, spp=1)
+    elif name == "c4_small":
+        xml = scenes.config_c4(in_tmp, n_side=3, K_tree=4000, width=320, height=180, spp=2)
+    else:
+        xml = os.path.join(SCENES, name + ".xml")
+        os.chdir(SCENES)
+    hs, ds = _scene(xml)
+    xml0 = scenes.with_depth(xml, os.path.join(in_tmp, "d0.xml"), 0)   # wavefront pipeline (no ray trees)
+    hs0, ds0 = _scene(xml0)
+    a, la = ds0.render(0, seed=9)
+    c, lc = ds0.render(0, seed=9, flags=rtgpu.RTG_RENDER_COUNT_STATS)
+    monkeypatch.setenv("RTG_DEFER", "0")
+    b, lb = ds0.render(0, seed=9)
+    n = int((a.view(np.uint32) != b.view(np.uint32)).any(axis=2).sum())
+    print(name, "differing pixels", n)
+    assert n == 0 and np.array_equal(la, lb)
+    assert np.array_equal(a.view(np.uint32), c.view(np.uint32))
