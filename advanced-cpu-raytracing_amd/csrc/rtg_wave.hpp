@@ -108,14 +108,19 @@ __global__ __launch_bounds__(256) void k_bigleaf(const DevScene S, const WaveBuf
 // A pending pixel's hit from its key, checked: the winner's reference leaf box (and an
 // instance's world box) must pass the exact slab test at next_up(t) -- else the reference walk
 // decides (rtg_common.hpp DeferCtx).
+// (the production render's counters are otherwise untouched: extend_wide_visits counts the
+// pending pixels and extend_fallbacks those the check sent to the reference walk -- diagnostics)
 template <int FEAT>
 __global__ __launch_bounds__(256) void k_hitfix(const DevScene S, const DevCamera C, const RenderParams P,
-                                                const int sample, const WaveBufs W) {
+                                                const int sample, const WaveBufs W, DevCounters* counters) {
     int px, py, crow;
     tile_pixel(P, px, py, crow);
-    if (px >= C.width || py >= P.row_end) return;
     const int i = crow * C.width + px;
-    if (W.hit_obj[i] != -2) return;
+    const bool pending = px < C.width && py < P.row_end && W.hit_obj[i] == -2;
+    const uint64_t pm = __ballot(pending);
+    if (counters && pm && (threadIdx.x & 63) == __ffsll((long long)pm) - 1)
+        atomicAdd(&counters->extend_wide_visits, (unsigned long long)__popcll(pm));
+    if (!pending) return;
     const uint64_t key = W.hit_key[i];
     const int pixel = px + py * C.width;
     float mbTime;
@@ -143,13 +148,117 @@ __global__ __launch_bounds__(256) void k_hitfix(const DevScene S, const DevCamer
             sure &= box_hit(a.x, a.y, a.z, a.w, b.x, b.y, lr, up);
         }
     }
-    if (!sure) {
-        Cnt<false> cn;
-        trace<false, false, FEAT>(S, ray, mbTime, INFINITY, INFINITY, h, cn);
+    // a winner that fails the check: the pixel goes to k_refwalk (the reference walk, one ray per
+    // wave); its slot in the (now consumed) entry memory, the count in dq_count[1]
+    const uint64_t fm = __ballot(!sure);
+    if (fm) {
+        const int lane = threadIdx.x & 63, lead = __ffsll((long long)fm) - 1;
+        int base = 0;
+        if (lane == lead) {
+            base = atomicAdd(W.dq_count + 1, __popcll(fm));
+            if (counters) atomicAdd(&counters->extend_fallbacks, (unsigned long long)__popcll(fm));
+        }
+        base = __shfl(base, lead);
+        if (!sure) {
+            reinterpret_cast<int*>(W.dq_e)[base + __popcll(fm & ((1ull << lane) - 1ull))] = i;
+            return;
+        }
     }
     W.hit_t[i] = h.t;
     W.hit_obj[i] = h.obj;
     W.hit_face[i] = h.face;
+}
+
+// IntersectObjects for one ray per wave (the pixels k_hitfix could not settle): every lane holds
+// the same ray and takes the same decisions, and a leaf's faces are dealt over the lanes, 64 at a
+// time -- the minimum (t, face) with t below minT of each chunk is exactly what the reference's
+// sequential loop keeps from it (acceptance t < minT, minT shrinking), so the walk is the
+// reference walk with its leaf loops run 64 wide.
+template <int FEAT>
+DEV bool trace_wave(const DevScene& S, Ray& r, float mbTime, Hit& h) {
+    const int lane = threadIdx.x & 63;
+    h.t = INFINITY;
+    h.obj = -1;
+    h.face = -1;
+    const RayRcp rq = ray_rcp(r);
+    for (int k = 0; k < S.num_objects; ++k) {
+        const DevObject& ob = S.objects[k];
+        if ((FEAT & FEAT_INSTANCE) && ob.group_end > k) {
+            const float4 ga = S.group_box[2 * k], gb = S.group_box[2 * k + 1];
+            if (!box_hit_fast(ga.x, ga.y, ga.z, gb.x, gb.y, gb.z, r, rq, h.t)) {
+                k = ob.group_end - 1;
+                continue;
+            }
+        }
+        if ((FEAT & FEAT_SPHERE) && ob.kind == OBJ_SPHERE) {
+            const Ray lr = trav_ray(ob, r, mbTime);
+            float t;
+            if (sphere_t(ob, lr, h.t, t)) { h.t = t; h.obj = k; h.face = -1; h.o = r.o; }
+            continue;
+        }
+        if ((FEAT & FEAT_INSTANCE) && ob.kind == OBJ_INSTANCE) {
+            Ray wr = r;
+            if (ob.flags & OBJF_MOTION_BLUR) wr.o = add(wr.o, muls(ld3(ob.mbv), mbTime));
+            if (!box_hit_fast(ob.bmin[0], ob.bmin[1], ob.bmin[2], ob.bmax[0], ob.bmax[1], ob.bmax[2], wr, rq, h.t)) {
+                r.o = wr.o;
+                continue;
+            }
+        }
+        const Ray lr = (FEAT & FEAT_XFORM) ? trav_ray(ob, r, mbTime) : r;
+        const RayRcp q = ray_rcp(lr);
+        float minT = h.t;
+        int face = -1;
+        for (int i = ob.node_begin; i < ob.node_end;) {
+            const float4 a = S.nodes[2 * i], b = S.nodes[2 * i + 1];
+            const int skip = __float_as_int(b.z), leaf = __float_as_int(b.w);
+            if (!box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, minT)) {
+                i = skip;
+                continue;
+            }
+            if (leaf < 0) {
+                ++i;
+                continue;
+            }
+            int first = leaf >> 8, cnt = leaf & 255;
+            if (leaf == LEAF_EXT) {
+                const int2 e = S.node_ext[i];
+                first = e.x;
+                cnt = e.y;
+            }
+            for (int c0 = first; c0 < first + cnt; c0 += 64) {
+                const int f = c0 + lane;
+                float t;
+                const bool ok = f < first + cnt && tri_test_fast(S, f, lr, minT, t);
+                const uint64_t best = wave_min_key(ok ? hit_key(t, f) : ~0ull, __ballot(1));
+                if (best != ~0ull) {
+                    minT = __uint_as_float((uint32_t)(best >> 32));
+                    face = (int)(uint32_t)best;
+                }
+            }
+            i = skip;
+        }
+        if (face >= 0) { h.t = minT; h.obj = k; h.face = face; h.o = r.o; }
+    }
+    return h.obj >= 0;
+}
+
+template <int FEAT>
+__global__ __launch_bounds__(256) void k_refwalk(const DevScene S, const DevCamera C, const RenderParams P,
+                                                 const int sample, const WaveBufs W) {
+    const int n = W.dq_count[1];
+    for (int e = (int)((blockIdx.x * 256u + threadIdx.x) >> 6); e < n; e += gridDim.x * 4) {
+        const int i = reinterpret_cast<const int*>(W.dq_e)[e];
+        const int crow = i / C.width, px = i - crow * C.width, py = part_row(P, crow);
+        float mbTime;
+        Ray ray = camera_ray(C, px, py, root_key(P.seed, px + py * C.width, sample), mbTime);
+        Hit h;
+        trace_wave<FEAT>(S, ray, mbTime, h);
+        if ((threadIdx.x & 63) == 0) {
+            W.hit_t[i] = h.t;
+            W.hit_obj[i] = h.obj;
+            W.hit_face[i] = h.face;
+        }
+    }
 }
 
 // wave-aggregated append to the block's queue segment: ballot + mbcnt rank, one LDS
@@ -574,11 +683,12 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
         bool deferred = false;
         if constexpr (!STATS && (FEAT & FEAT_BIGLEAF) != 0) {
             if (!ordered && !frame && W.dq_e && S.face_leaf && S.num_objects < 4096 && S.num_faces < (1 << 20)) {
-                (void)hipMemsetAsync(W.dq_count, 0, sizeof(int), st);
+                (void)hipMemsetAsync(W.dq_count, 0, 2 * sizeof(int), st);
                 hipLaunchKernelGGL((k_primary<STATS, FEAT, 0, true>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s,
                                    W, cnt);
                 hipLaunchKernelGGL((k_bigleaf<FEAT>), dim3(2048), dim3(256), 0, st, S, W);
-                hipLaunchKernelGGL((k_hitfix<FEAT>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W);
+                hipLaunchKernelGGL((k_hitfix<FEAT>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
+                hipLaunchKernelGGL((k_refwalk<FEAT>), dim3(256), dim3(256), 0, st, S, C, P, s, W);
                 deferred = true;
             }
         }
