@@ -1127,12 +1127,12 @@ static int ensure_wave(WaveWork& ww, size_t pixels, int slots, size_t tiles) {
     return RTG_OK;
 }
 
-// The deferred-leaf queue of a large-leaf scene's camera walk (WaveBufs dq_*, hit_key): one
-// entry per pixel of capacity (an entry that does not fit is tested in the walk).
+// The deferred-leaf queue of a large-leaf scene's camera walk (WaveBufs dq_*, hit_key): two
+// entries per pixel of capacity (an entry that does not fit is tested in the walk).
 static int ensure_defer(WaveWork& ww, size_t pixels) {
-    if (ww.dq && ww.W.dq_cap >= (int)pixels) return RTG_OK;
+    const size_t cap = std::max<size_t>(2 * pixels, 1024);
+    if (ww.dq && ww.W.dq_cap >= (int)cap) return RTG_OK;
     if (ww.dq) { (void)hipFree(ww.dq); ww.dq = nullptr; }
-    const size_t cap = std::max<size_t>(pixels, 1024);
     const size_t bytes = 256 + pixels * 8 + cap * 48;
     HIP_TRY(hipMalloc(&ww.dq, bytes));
     char* b = (char*)ww.dq;

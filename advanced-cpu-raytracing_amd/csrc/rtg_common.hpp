@@ -685,6 +685,11 @@ DEV int wave_min_int(int v) {
 // enters after t (hit before its box: rounding only).  Hence a winner whose leaf box passes at
 // next_up(t) IS h; k_hitfix checks exactly that and runs the reference walk otherwise.
 constexpr int kDeferLeaf = 16;
+// A leaf is deferred only for the lanes of a wave that reach it when they are few; when many
+// reach it together the wave tests it in the walk, every lane busy (RTG_DEFER_LANES: A/B)
+#ifndef RTG_DEFER_LANES
+#define RTG_DEFER_LANES 16
+#endif
 struct DeferCtx {
     float4* e;
     int* count;
@@ -759,9 +764,9 @@ DEV bool walk_bvh_packet(const DevScene& S, const int begin, const int end, cons
                     cnt = __builtin_amdgcn_readfirstlane(e.y);
                 }
                 if constexpr (DEFER) {
-                    if (cnt > kDeferLeaf) {
+                    const uint64_t m = __ballot(pass);
+                    if (cnt > kDeferLeaf && __popcll(m) <= RTG_DEFER_LANES) {
                         // one atomic per wave for the lanes that reached the leaf
-                        const uint64_t m = __ballot(pass);
                         const int lane = threadIdx.x & 63, lead = __ffsll((long long)m) - 1;
                         int base = 0;
                         if (lane == lead) base = atomicAdd(dc->count, __popcll(m));
