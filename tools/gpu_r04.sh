@@ -58,6 +58,9 @@ for s in "${steps[@]}"; do
       run cfg_c5 400 python bench.py --config c5 --steps 5 --warmup 1 --no-cpu-baseline $extra ;;
     ab)
       run ab 1500 bash tools/gpu_ab_head.sh $tag/ab $AB_LIBS ;;
+    multirank)
+      # the driver's N-rank launch rehearsed on one GPU (gloo; ranks share GPU 0)
+      run multirank_n2 400 env RTG_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29512 bench.py --gpus 2 --steps 20 --warmup 2 ;;
     envbench)
       # the headline bench (with gather / host-frame / parts / ordered extras) once per setting in
       # $ENV_AB ("base" or NAME=VALUE[,NAME=VALUE])
