@@ -86,6 +86,7 @@ struct WaveWork {
     int slots = 0;
     void* mem = nullptr;
     void* dq = nullptr;               // deferred-leaf queue + per-pixel hit keys (ensure_defer)
+    size_t dq_nq = 0;                 // its shadow-state entries
     rtg::WaveBufs W{};
 };
 constexpr int kWorkCtx = 3;
@@ -1123,23 +1124,28 @@ static int ensure_wave(WaveWork& ww, size_t pixels, int slots, size_t tiles) {
     W.dq_e = nullptr;
     W.dq_count = nullptr;
     W.hit_key = nullptr;
+    W.shadow_state = nullptr;
     W.dq_cap = 0;
+    ww.dq_nq = 0;
     return RTG_OK;
 }
 
 // The deferred-leaf queue of a large-leaf scene's camera walk (WaveBufs dq_*, hit_key): two
 // entries per pixel of capacity (an entry that does not fit is tested in the walk).
-static int ensure_defer(WaveWork& ww, size_t pixels) {
+static int ensure_defer(WaveWork& ww, size_t pixels, size_t nq) {
     const size_t cap = std::max<size_t>(2 * pixels, 1024);
-    if (ww.dq && ww.W.dq_cap >= (int)cap) return RTG_OK;
+    if (ww.dq && ww.W.dq_cap >= (int)cap && ww.dq_nq >= nq) return RTG_OK;
     if (ww.dq) { (void)hipFree(ww.dq); ww.dq = nullptr; }
-    const size_t bytes = 256 + pixels * 8 + cap * 48;
+    nq = std::max(nq, ww.dq_nq);
+    const size_t bytes = 256 + pixels * 8 + cap * 48 + nq * 4;
     HIP_TRY(hipMalloc(&ww.dq, bytes));
     char* b = (char*)ww.dq;
     ww.W.dq_count = (int*)b;
     ww.W.hit_key = (unsigned long long*)(b + 256);
     ww.W.dq_e = (float4*)(b + 256 + pixels * 8);
+    ww.W.shadow_state = (int*)(b + 256 + pixels * 8 + cap * 48);
     ww.W.dq_cap = (int)cap;
+    ww.dq_nq = nq;
     return RTG_OK;
 }
 
@@ -1241,12 +1247,14 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
             }
         }
         if ((s->feat & rtg::FEAT_BIGLEAF) && !stats && rtg::defer_leaves()) {
-            rc = ensure_defer(ww, rows * C.width);
+            rc = ensure_defer(ww, rows * C.width, (size_t)P.num_tiles * 256 * std::max(s->num_slots, 1));
             if (rc) return rc;
             W.dq_e = ww.W.dq_e;
             W.dq_count = ww.W.dq_count;
             W.hit_key = ww.W.hit_key;
+            W.shadow_state = ww.W.shadow_state;
             W.dq_cap = ww.W.dq_cap;
+            W.defer_any_min = (int)std::max<int64_t>(1, (int64_t)rows * C.width / rtg::defer_any_gate());
         }
         int layout = rtg::LAYOUT_WAVE;
         HIP_TRY(rtg::launch_wave(ds, C, P, W, d_hdr, d_ldr, s->counters.p, stats, s->feat, s->shade_sk, stream, ev,

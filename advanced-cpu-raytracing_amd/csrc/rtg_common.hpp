@@ -696,6 +696,7 @@ struct DeferCtx {
     int cap;
     int ray;                          // the pixel's work-buffer index
     bool deferred;                    // this lane appended an entry
+    int big;                          // wave-uniform: lanes that tested a large leaf in the walk
 };
 // (t, object, face) as one 64-bit key: t > 0 orders like its bits; objects < 2^12, faces < 2^20
 // (defer_ok); a sphere's face field is all ones
@@ -781,6 +782,8 @@ DEV bool walk_bvh_packet(const DevScene& S, const int begin, const int end, cons
                             pass = false;                // queued: no test here, minT unchanged
                         }
                         // (a lane whose entry did not fit tests the leaf below)
+                    } else if (cnt > kDeferLeaf) {
+                        dc->big += __popcll(m);          // the shadow walk's choice reads these (GATE)
                     }
                 }
                 for (int f = first; f < first + cnt; ++f) {
@@ -1013,6 +1016,24 @@ DEV bool slab_cons(float lx, float ly, float lz, float hx, float hy, float hz, c
     return (tmax > -1e-30f) & (tmax >= tmin * (1.0f - 0x1p-21f) - 1e-30f) & (tmin < minTc);
 }
 
+// DEFER (large-leaf scenes, the packet walk): a leaf slot of more than RTG_DEFER_ANY_LEAF entries
+// that at most RTG_DEFER_ANY_LANES lanes reach is queued for those lanes (k_bigleaf_any) instead
+// of tested; the decisions are the same per face wherever they are taken, so the answer is
+// unchanged.  (Per lane, walk_wide_any, measured slower: C3 4 735, C3-ton 2 844, C4 2 150
+// Mrays/s against 4 400 / 5 333 / 2 494 for the packet, profiles/r04p_any_walk_ab.txt.)
+#ifndef RTG_DEFER_ANY_LANES
+#define RTG_DEFER_ANY_LANES 16
+#endif
+#ifndef RTG_DEFER_ANY_LEAF
+#define RTG_DEFER_ANY_LEAF 16
+#endif
+struct AnyDefer {
+    float4* e;
+    int* count;
+    int cap;
+    int q;                            // the shadow ray's queue entry
+    bool deferred;
+};
 // One mesh's any-hit tree (rtg_ahb.cpp; local ray lr).  inst_conf: the instance's world box
 // passes at limit (true for plain meshes).  Returns 1 / 0 / -1 as above.  A node's leaf
 // children are tested in place (all lanes stay in step: a separate iteration per leaf measured
@@ -1103,9 +1124,9 @@ DEV int walk_wide_any(const DevScene& S, int node, const Ray& lr, float minT0, f
 #ifndef RTG_PK_MAX_STEPS
 #define RTG_PK_MAX_STEPS 4096
 #endif
-template <bool STATS>
+template <bool STATS, bool DEFER = false>
 DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0, float limit, bool inst_conf,
-                         Cnt<STATS>& c) {
+                         Cnt<STATS>& c, AnyDefer* ad = nullptr) {
     const RayRcp q = ray_rcp(lr);
     const float minTc = minT0 * (1.0f + 0x1p-21f);
     const SlabRay sr = slab_ray(lr, q);
@@ -1164,6 +1185,25 @@ DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0
                 continue;
             }
             const int first = lidx[k] >> 8, cnt = lidx[k] & 255;
+            if constexpr (DEFER) {
+                const uint64_t m = __ballot(h[k]);
+                if (cnt > RTG_DEFER_ANY_LEAF && __popcll(m) <= RTG_DEFER_ANY_LANES) {
+                    const int lane = threadIdx.x & 63, lead = __ffsll((long long)m) - 1;
+                    int base = 0;
+                    if (lane == lead) base = atomicAdd(ad->count, __popcll(m));
+                    base = __shfl(base, lead);
+                    const int slot = base + __popcll(m & ((1ull << lane) - 1ull));
+                    if (h[k] && slot < ad->cap) {
+                        float4* qe = ad->e + 3 * (size_t)slot;
+                        qe[0] = make_float4(lr.o.x, lr.o.y, lr.o.z, minT0);
+                        qe[1] = make_float4(lr.d.x, lr.d.y, lr.d.z, limit);
+                        qe[2] = make_float4(__int_as_float(first), __int_as_float(cnt), __int_as_float(ad->q),
+                                            __int_as_float((int)inst_conf));
+                        ad->deferred = true;
+                        h[k] = false;
+                    }
+                }
+            }
             for (int e = first; e < first + cnt; ++e) {
                 rtg_s8 ra;
                 rtg_s4 rb;
@@ -1221,8 +1261,9 @@ DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0
 // CastShadowRay on the wide BVH: objects in any order (the answer is a boolean), spheres
 // exactly (a sphere hit with t < limit is accepted at any minT_cur >= limit, one with
 // t >= limit never decides).  Returns 1 / 0 / -1 (undecided: run trace<true>).
-template <bool STATS, int FEAT>
-DEV int trace_any_wide(const DevScene& S, const Ray& r, float minT0, float limit, Cnt<STATS>& c) {
+template <bool STATS, int FEAT, bool DEFER = false, bool PK = RTG_ANY_PACKET || DEFER>
+DEV int trace_any_wide(const DevScene& S, const Ray& r, float minT0, float limit, Cnt<STATS>& c,
+                       AnyDefer* ad = nullptr) {
     const RayRcp rq = (FEAT & FEAT_INSTANCE) ? ray_rcp(r) : RayRcp{};
     if ((FEAT & FEAT_INSTANCE) && !rq.fast) return -1;
     bool undecided = false;
@@ -1231,7 +1272,7 @@ DEV int trace_any_wide(const DevScene& S, const Ray& r, float minT0, float limit
         const DevObject& ob = S.objects[k];
         if ((FEAT & FEAT_INSTANCE) && ob.group_end > k) {
             const float4 ga = S.group_box[2 * k], gb = S.group_box[2 * k + 1];
-            if (RTG_ANY_PACKET) {
+            if (PK) {
                 // the packet walk needs one object (one root) per wave: a lane whose group box
                 // fails sits the group out, and the wave jumps over it when every lane does
                 if (k >= gskip && !box_hit_fast(ga.x, ga.y, ga.z, gb.x, gb.y, gb.z, r, rq, minT0))
@@ -1245,7 +1286,7 @@ DEV int trace_any_wide(const DevScene& S, const Ray& r, float minT0, float limit
                 continue;
             }
         }
-        if (RTG_ANY_PACKET && k < gskip) continue;
+        if (PK && k < gskip) continue;
         c.obj();
         if ((FEAT & FEAT_SPHERE) && ob.kind == OBJ_SPHERE) {
             c.sph();
@@ -1263,8 +1304,8 @@ DEV int trace_any_wide(const DevScene& S, const Ray& r, float minT0, float limit
         }
         const Ray lr = (FEAT & FEAT_XFORM) ? trav_ray(ob, r, 0.f) : r;
         if (ob.aroot < 0) return -1;                 // no any-hit tree for this mesh: reference walk
-        const int res = RTG_ANY_PACKET ? walk_wide_any_pk<STATS>(S, ob.aroot, lr, minT0, limit, conf, c)
-                                       : walk_wide_any<STATS>(S, ob.aroot, lr, minT0, limit, conf, c);
+        const int res = PK ? walk_wide_any_pk<STATS, DEFER>(S, ob.aroot, lr, minT0, limit, conf, c, ad)
+                           : walk_wide_any<STATS>(S, ob.aroot, lr, minT0, limit, conf, c);
         if (res > 0) return 1;
         undecided |= res < 0;
     }
@@ -2536,6 +2577,25 @@ DEV void flush_counters(Cnt<STATS>& cn, DevCounters* counters) {
 // early-exit any-hit.
 // grid (shade blocks, slots): block (b, c) takes entries [256c, 256c+256) of segment b
 // CastShadowRay's answer for queue entry q (origin + initial minT o, direction + limit d).
+// DEFER (large-leaf scenes, fast walk): the any-hit walk may queue large leaves; a ray with no
+// answer of its own but queued leaves is pending (k_bigleaf_any, k_shadow_fin decide it)
+enum : int { SS_PENDING = 1, SS_OCC = 2, SS_UNDECIDED = 4 };
+template <bool STATS, int FEAT>
+DEV int shadow_state_defer(const DevScene& S, const WaveBufs& W, size_t q, float4 o, float4 d, Cnt<STATS>& cn) {
+    Ray r;
+    r.o = mk(o.x, o.y, o.z);
+    r.d = mk(d.x, d.y, d.z);
+    AnyDefer ad{W.dq_e, W.dq_count + 2, W.dq_cap, (int)q, false};
+    int res = trace_any_wide<STATS, FEAT, true>(S, r, o.w, d.w, cn, &ad);
+    if (res < 0) {                                   // undecided: the reference walk (queued leaves moot)
+        cn.fallback();
+        Hit h;
+        res = trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
+    } else if (res == 0 && ad.deferred) {
+        return SS_PENDING;
+    }
+    return res > 0 ? SS_OCC : 0;
+}
 template <bool STATS, int FEAT, bool FAST>
 DEV bool shadow_occluded(const DevScene& S, const WaveBufs& W, size_t q, float4 o, float4 d, Cnt<STATS>& cn) {
     Ray r;
@@ -2570,16 +2630,72 @@ DEV bool shadow_occluded(const DevScene& S, const WaveBufs& W, size_t q, float4 
     return res > 0;
 }
 
-template <bool STATS, int FEAT, bool FAST>
-__global__ __launch_bounds__(256, FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(FEAT)) void k_shadow(const DevScene S, const WaveBufs W,
-                                                                                            DevCounters* counters) {
+// Large-leaf scenes pick the shadow walk per pass on the device (GATE): the deferring any-hit
+// walk (GATE 1) when the pass's camera walk reached large leaves with at least defer_any_min
+// lanes (queued, dq_count[0], or tested in the walk, dq_count[3]), else the cooperative
+// reference walk (GATE -1); the other kernel's blocks return at once.  Measured: C3-ton
+// 3 900 -> 5 333 Mrays/s and C4 2 377 -> 2 494 with the deferring walk, C3 5 035 -> 4 400: its
+// cooperative walk stays (profiles/r04p_any_walk_ab.txt).
+DEV bool any_defer_on(const WaveBufs& W) { return W.dq_count[0] + W.dq_count[3] >= W.defer_any_min; }
+template <int GATE>
+DEV bool gate_skip(const WaveBufs& W) {
+    if constexpr (GATE == 0) return false;
+    else return any_defer_on(W) != (GATE > 0);
+}
+
+template <bool STATS, int FEAT, bool FAST, bool DEFER = false, int GATE = 0>
+__global__ __launch_bounds__(256, FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(FEAT)) void k_shadow(
+    const DevScene S, const WaveBufs W, DevCounters* counters) {
+    if (gate_skip<GATE>(W)) return;
     const int k = blockIdx.y * 256 + threadIdx.x;
     const size_t q = ((size_t)blockIdx.x * W.num_slots) * 256 + k;
     Cnt<STATS> cn;
     if (k < W.q_count[blockIdx.x]) {
-        if (shadow_occluded<STATS, FEAT, FAST>(S, W, q, W.q_o[q], W.q_d[q], cn)) W.occ[W.q_slot[q]] = 1;
+        if constexpr (DEFER) {
+            const int st = shadow_state_defer<STATS, FEAT>(S, W, q, W.q_o[q], W.q_d[q], cn);
+            W.shadow_state[q] = st;
+            if (st == SS_OCC) W.occ[W.q_slot[q]] = 1;
+        } else if (shadow_occluded<STATS, FEAT, FAST>(S, W, q, W.q_o[q], W.q_d[q], cn)) {
+            W.occ[W.q_slot[q]] = 1;
+        }
     }
     flush_counters<STATS>(cn, counters);
 }
+
+// The shadow rays' queued large leaves: one wave per entry, each lane taking entries (face
+// records of the any-hit tree) 64 apart and the exact decisions of walk_wide_any on each --
+// a sufficient face (the leaf box passes at limit) occludes, a face reaching only at minT0
+// leaves the ray undecided -- OR-ed into the ray's state.
+template <int FEAT>
+__global__ __launch_bounds__(256) void k_bigleaf_any(const DevScene S, const WaveBufs W) {
+    const int n = min(W.dq_count[2], W.dq_cap);
+    const int lane = threadIdx.x & 63;
+    for (int e = (int)((blockIdx.x * 256u + threadIdx.x) >> 6); e < n; e += gridDim.x * 4) {
+        const float4 a = W.dq_e[3 * (size_t)e], b = W.dq_e[3 * (size_t)e + 1], c4 = W.dq_e[3 * (size_t)e + 2];
+        Ray lr;
+        lr.o = mk(a.x, a.y, a.z);
+        lr.d = mk(b.x, b.y, b.z);
+        const float minT0 = a.w, limit = b.w;
+        const int first = __float_as_int(c4.x), cnt = __float_as_int(c4.y), q = __float_as_int(c4.z);
+        const bool conf = __float_as_int(c4.w) != 0;
+        const RayRcp rq = ray_rcp(lr);
+        int bits = 0;
+        for (int x = first + lane; x < first + cnt; x += 64) {
+            const float4* R = S.ahtris + 3 * (size_t)x;
+            float t;
+            if (!tri_test_fast_rec(R, lr, limit, t)) continue;
+            const int ref = __float_as_int(R[0].w);
+            const float4 na = S.nodes[2 * ref], nb = S.nodes[2 * ref + 1];
+            if (!box_hit_fast(na.x, na.y, na.z, na.w, nb.x, nb.y, lr, rq, minT0)) continue;
+            bits |= (conf && box_hit_fast(na.x, na.y, na.z, na.w, nb.x, nb.y, lr, rq, limit)) ? SS_OCC : SS_UNDECIDED;
+        }
+        const uint64_t occ = __ballot(bits & SS_OCC), und = __ballot(bits & SS_UNDECIDED);
+        if (lane == 0 && (occ | und)) atomicOr(W.shadow_state + q, (occ ? SS_OCC : 0) | (und ? SS_UNDECIDED : 0));
+    }
+}
+
+// A pending shadow ray's answer: occluded by a queued leaf, undecided (the reference walk), or
+// not occluded; the general layout records it in occ, the one-light layout finishes the pixel.
+DEV bool pending_occluded(int st) { return (st & SS_OCC) != 0; }
 
 }  // namespace rtg

@@ -230,8 +230,11 @@ struct WaveBufs {
     // leaf it reaches to a queue of (ray, leaf, minT at entry) entries, 3 float4 each, tested by
     // k_bigleaf; per pixel the 64-bit (t, object, face) key of the best hit so far
     float4* __restrict__ dq_e;
-    int* __restrict__ dq_count;
+    int* __restrict__ dq_count;         // [0] camera entries, [1] unsettled pixels, [2] shadow entries,
+                                        // [3] camera lanes testing large leaves in the walk
+    int defer_any_min;                  // shadow walk choice (GATE): large-leaf lanes of the camera pass
     unsigned long long* __restrict__ hit_key;
+    int* __restrict__ shadow_state;     // per shadow queue entry: SS_* bits (deferred any-hit)
     int dq_cap;
 };
 

@@ -55,8 +55,10 @@ __global__ __launch_bounds__(256, ORD ? RTG_ORD_WAVES : RTG_TRACE_WAVES(FEAT)) v
             }
         } else if constexpr (DEFER) {
             // large leaves deferred to k_bigleaf; k_hitfix settles the pixel (rtg_common.hpp DeferCtx)
-            DeferCtx dc{W.dq_e, W.dq_count, W.dq_cap, crow * C.width + px, false};
+            DeferCtx dc{W.dq_e, W.dq_count, W.dq_cap, crow * C.width + px, false, 0};
             trace<false, STATS, FEAT, true, true>(S, ray, mbTime, INFINITY, INFINITY, h, cn, &dc);
+            const int big = __builtin_amdgcn_readfirstlane(dc.big);
+            if (big && (int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) atomicAdd(W.dq_count + 3, big);
             if (dc.deferred) {
                 const int i = crow * C.width + px;
                 W.hit_key[i] = h.obj >= 0 ? obj_key(h.t, h.obj, h.face) : ~0ull;
@@ -610,20 +612,81 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
 
 // One-light scenes: CastShadowRay for a queued pixel, then its PerformShading sum and the end
 // of the sample pass (what k_resolve does for the general case).
-template <bool STATS, int FEAT, bool FAST>
+template <bool STATS, int FEAT, bool FAST, bool DEFER = false, int GATE = 0>
 __global__ __launch_bounds__(256, FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(FEAT)) void k_shadow_one(
     const DevScene S, const DevCamera C, const RenderParams P, const int sample, const WaveBufs W, const PassOut O,
     DevCounters* counters) {
+    if (gate_skip<GATE>(W)) return;
     const int k = threadIdx.x;
     const size_t q = (size_t)blockIdx.x * 256 + k;
     Cnt<STATS> cn;
     if (k < W.q_count[blockIdx.x]) {
-        const bool occluded = shadow_occluded<STATS, FEAT, FAST>(S, W, q, W.q_o[q], W.q_d[q], cn);
+        bool occluded;
+        if constexpr (DEFER) {
+            // large leaves queued (k_bigleaf_any): a pending ray is finished by k_shadow_fin_one
+            const int st = shadow_state_defer<STATS, FEAT>(S, W, q, W.q_o[q], W.q_d[q], cn);
+            W.shadow_state[q] = st;
+            occluded = st == SS_OCC;
+            if (st == SS_PENDING) {
+                flush_counters<STATS>(cn, counters);
+                return;
+            }
+        } else {
+            occluded = shadow_occluded<STATS, FEAT, FAST>(S, W, q, W.q_o[q], W.q_d[q], cn);
+        }
         const float4 b = W.q_pay[2 * q], t = W.q_pay[2 * q + 1];
         const f3 color = resolve_one(mk(b.x, b.y, b.z), __float_as_int(b.w), true, mk(t.x, t.y, t.z), occluded);
         finish_pixel(C, P, sample, O, __float_as_int(t.w), color);
     }
     flush_counters<STATS>(cn, counters);
+}
+
+// Pending shadow rays after k_bigleaf_any: occluded by a queued leaf, undecided (the reference
+// walk decides), else unoccluded -- then the pixel is finished as k_shadow_one would have.
+template <int FEAT, int GATE>
+__global__ __launch_bounds__(256) void k_shadow_fin_one(const DevScene S, const DevCamera C, const RenderParams P,
+                                                        const int sample, const WaveBufs W, const PassOut O) {
+    if (gate_skip<GATE>(W)) return;              // (shadow_state holds an older pass's states)
+    const int k = threadIdx.x;
+    const size_t q = (size_t)blockIdx.x * 256 + k;
+    if (k >= W.q_count[blockIdx.x]) return;
+    const int st = W.shadow_state[q];
+    if (!(st & SS_PENDING)) return;
+    bool occluded = (st & SS_OCC) != 0;
+    if (!occluded && (st & SS_UNDECIDED)) {
+        const float4 o = W.q_o[q], d = W.q_d[q];
+        Ray r;
+        r.o = mk(o.x, o.y, o.z);
+        r.d = mk(d.x, d.y, d.z);
+        Cnt<false> cn;
+        Hit h;
+        occluded = trace<true, false, FEAT>(S, r, 0.f, o.w, d.w, h, cn);
+    }
+    const float4 b = W.q_pay[2 * q], t = W.q_pay[2 * q + 1];
+    const f3 color = resolve_one(mk(b.x, b.y, b.z), __float_as_int(b.w), true, mk(t.x, t.y, t.z), occluded);
+    finish_pixel(C, P, sample, O, __float_as_int(t.w), color);
+}
+
+// The same for the general layout: the answer goes to the light slot's occlusion byte.
+template <int FEAT, int GATE>
+__global__ __launch_bounds__(256) void k_shadow_fin(const DevScene S, const WaveBufs W) {
+    if (gate_skip<GATE>(W)) return;
+    const int k = blockIdx.y * 256 + threadIdx.x;
+    const size_t q = ((size_t)blockIdx.x * W.num_slots) * 256 + k;
+    if (k >= W.q_count[blockIdx.x]) return;
+    const int st = W.shadow_state[q];
+    if (!(st & SS_PENDING)) return;
+    bool occluded = (st & SS_OCC) != 0;
+    if (!occluded && (st & SS_UNDECIDED)) {
+        const float4 o = W.q_o[q], d = W.q_d[q];
+        Ray r;
+        r.o = mk(o.x, o.y, o.z);
+        r.d = mk(d.x, d.y, d.z);
+        Cnt<false> cn;
+        Hit h;
+        occluded = trace<true, false, FEAT>(S, r, 0.f, o.w, d.w, h, cn);
+    }
+    if (occluded) W.occ[W.q_slot[q]] = 1;
 }
 
 
@@ -637,6 +700,7 @@ void wave_resolve(const DevCamera& C, const RenderParams& P, int sample, const W
 bool no_fused_shade();
 bool frame_kernel();
 bool defer_leaves();
+int defer_any_leaves();
 bool wide_bigleaf();
 
 // One traversal variant's pass sequence (instantiated in rtg_wave_a.hip / rtg_wave_b.hip).
@@ -653,9 +717,16 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
     // reference walk
     // (large-leaf scenes: the split any-hit tree cuts their pole fans into small leaves; with
     // RTG_AHB=ref / exact they keep the cooperative reference walk unless RTG_WIDE_BIGLEAF)
+    // large-leaf scenes (production renders): the any-hit walk with their large leaves queued
+    // (k_bigleaf_any; RTG_DEFER=0: the cooperative reference walk)
+    // (0 off; 1 always; 2 chosen per pass on the device -- GATE, rtg_common.hpp)
+    const int defer_any = !STATS && (FEAT & FEAT_BIGLEAF) && RTG_SHADOW_MODE == 3 && W.dq_e && W.shadow_state &&
+                                  S.anodes && !S.ahb_split && !S.exact_shadow
+                              ? defer_any_leaves()
+                              : 0;
     const bool fast = (RTG_SHADOW_MODE == 3 ? S.anodes != nullptr
                                             : RTG_SHADOW_MODE == 2 ? S.node_up != nullptr : S.nodes != nullptr) &&
-                      (!(FEAT & FEAT_BIGLEAF) || S.ahb_split || wide_bigleaf()) && !S.exact_shadow;
+                      (!(FEAT & FEAT_BIGLEAF) || S.ahb_split || wide_bigleaf() || defer_any == 1) && !S.exact_shadow;
     // shading fused with the shadow ray: plain shading, the fast any-hit walk (RTG_NO_FUSED_SHADE=1
     // keeps the queue: experiments)
     const bool fused = scene_sk == 0 && fast && !(FEAT & FEAT_BIGLEAF) && nshadow > 0 && !no_fused_shade();
@@ -681,9 +752,9 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
         // large-leaf scenes: the camera walk defers large leaves (k_bigleaf, k_hitfix; production
         // renders only -- counting renders keep the cooperative walk and the reference's counts)
         bool deferred = false;
+        if (W.dq_e) (void)hipMemsetAsync(W.dq_count, 0, 4 * sizeof(int), st);
         if constexpr (!STATS && (FEAT & FEAT_BIGLEAF) != 0) {
             if (!ordered && !frame && W.dq_e && S.face_leaf && S.num_objects < 4096 && S.num_faces < (1 << 20)) {
-                (void)hipMemsetAsync(W.dq_count, 0, 2 * sizeof(int), st);
                 hipLaunchKernelGGL((k_primary<STATS, FEAT, 0, true>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s,
                                    W, cnt);
                 hipLaunchKernelGGL((k_bigleaf<FEAT>), dim3(2048), dim3(256), 0, st, S, W);
@@ -720,7 +791,25 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
             if (e != hipSuccess) return e;
             if (e5) (void)hipEventRecord(e5[2], st);
             if (nshadow > 0) {
-                if (fast)
+                if (defer_any) {
+                    if constexpr (!STATS && (FEAT & FEAT_BIGLEAF)) {
+                        if (defer_any == 1) {            // RTG_DEFER_ANY=1: always the deferring walk
+                            hipLaunchKernelGGL((k_shadow_one<STATS, FEAT, true, true>), dim3(P.num_tiles), dim3(256), 0,
+                                               st, S, C, P, s, W, O, cnt);
+                            hipLaunchKernelGGL((k_bigleaf_any<FEAT>), dim3(2048), dim3(256), 0, st, S, W);
+                            hipLaunchKernelGGL((k_shadow_fin_one<FEAT, 0>), dim3(P.num_tiles), dim3(256), 0, st, S, C,
+                                               P, s, W, O);
+                        } else {                         // chosen on the device (GATE)
+                            hipLaunchKernelGGL((k_shadow_one<STATS, FEAT, false, false, -1>), dim3(P.num_tiles),
+                                               dim3(256), 0, st, S, C, P, s, W, O, cnt);
+                            hipLaunchKernelGGL((k_shadow_one<STATS, FEAT, true, true, 1>), dim3(P.num_tiles), dim3(256),
+                                               0, st, S, C, P, s, W, O, cnt);
+                            hipLaunchKernelGGL((k_bigleaf_any<FEAT>), dim3(2048), dim3(256), 0, st, S, W);
+                            hipLaunchKernelGGL((k_shadow_fin_one<FEAT, 1>), dim3(P.num_tiles), dim3(256), 0, st, S, C,
+                                               P, s, W, O);
+                        }
+                    }
+                } else if (fast)
                     hipLaunchKernelGGL((k_shadow_one<STATS, FEAT, true>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P,
                                        s, W, O, cnt);
                 else
@@ -733,7 +822,21 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
             if (e != hipSuccess) return e;
             if (e5) (void)hipEventRecord(e5[2], st);
             if (nshadow > 0) {
-                if (fast) {
+                if (defer_any) {
+                    if constexpr (!STATS && (FEAT & FEAT_BIGLEAF)) {
+                        const dim3 g(P.num_tiles, nshadow);
+                        if (defer_any == 1) {
+                            hipLaunchKernelGGL((k_shadow<STATS, FEAT, true, true>), g, dim3(256), 0, st, S, W, cnt);
+                            hipLaunchKernelGGL((k_bigleaf_any<FEAT>), dim3(2048), dim3(256), 0, st, S, W);
+                            hipLaunchKernelGGL((k_shadow_fin<FEAT, 0>), g, dim3(256), 0, st, S, W);
+                        } else {
+                            hipLaunchKernelGGL((k_shadow<STATS, FEAT, false, false, -1>), g, dim3(256), 0, st, S, W, cnt);
+                            hipLaunchKernelGGL((k_shadow<STATS, FEAT, true, true, 1>), g, dim3(256), 0, st, S, W, cnt);
+                            hipLaunchKernelGGL((k_bigleaf_any<FEAT>), dim3(2048), dim3(256), 0, st, S, W);
+                            hipLaunchKernelGGL((k_shadow_fin<FEAT, 1>), g, dim3(256), 0, st, S, W);
+                        }
+                    }
+                } else if (fast) {
                     hipLaunchKernelGGL((k_shadow<STATS, FEAT, true>), dim3(P.num_tiles, nshadow), dim3(256), 0, st, S,
                                        W, cnt);
                 } else {

@@ -39,6 +39,20 @@ bool defer_leaves() {
     return !v || std::strcmp(v, "0") != 0;
 }
 
+// RTG_DEFER_ANY: shadow rays of large-leaf scenes -- 0 the cooperative reference walk, 1 the
+// deferring any-hit walk, unset: chosen per pass on the device (GATE, rtg_common.hpp)
+// RTG_DEFER_ANY_GATE=g: the deferring walk when the camera pass reached large leaves with at
+// least pixels / g lanes (default 50: 2 %)
+int defer_any_gate() {
+    const char* v = std::getenv("RTG_DEFER_ANY_GATE");
+    return v && std::atoi(v) > 0 ? std::atoi(v) : 50;
+}
+
+int defer_any_leaves() {
+    const char* v = std::getenv("RTG_DEFER_ANY");
+    return !v ? 2 : std::strcmp(v, "0") == 0 ? 0 : 1;
+}
+
 // RTG_FRAME_KERNEL=1: the fused layout's two kernels as one (k_shade<..., FRAME>: A/B)
 bool frame_kernel() {
     static const bool v = std::getenv("RTG_FRAME_KERNEL") != nullptr;

@@ -158,8 +158,10 @@ def test_large_leaf_cooperative_walk_small(cfg, in_tmp):
 @pytest.mark.parametrize("name", ["c3_small", "c4_small", "c3_blob", "berserker", "windmill", "tower", "car_smooth"])
 def test_deferred_large_leaves(name, in_tmp, monkeypatch):
     """Large-leaf scenes: the camera walk defers its large leaves to k_bigleaf and settles each
-    pixel in k_hitfix (the winner's leaf box checked at next_up(t), rtg_common.hpp DeferCtx) --
-    bit for bit the image of the cooperative reference walk (RTG_DEFER=0) and of the counting
+    pixel in k_hitfix (the winner's leaf box checked at next_up(t), rtg_common.hpp DeferCtx), the
+    shadow walk queues its large leaves to k_bigleaf_any (AnyDefer; by default when the camera pass
+    queued enough of them, RTG_DEFER_ANY=1 always) -- bit for bit the image of the cooperative
+    reference walk (RTG_DEFER=0), of camera deferral alone (RTG_DEFER_ANY=0) and of the counting
     render (which never defers)."""
     if name == "c3_small":
         xml = scenes.config_c3(in_tmp, K=20000, width=320, height=180, spp=1)
@@ -173,9 +175,15 @@ def test_deferred_large_leaves(name, in_tmp, monkeypatch):
     hs0, ds0 = _scene(xml0)
     a, la = ds0.render(0, seed=9)
     c, lc = ds0.render(0, seed=9, flags=rtgpu.RTG_RENDER_COUNT_STATS)
+    monkeypatch.setenv("RTG_DEFER_ANY", "1")   # shadow rays: always the deferring walk
+    e, le = ds0.render(0, seed=9)
+    assert np.array_equal(a.view(np.uint32), e.view(np.uint32)) and np.array_equal(la, le)
+    monkeypatch.setenv("RTG_DEFER_ANY", "0")   # shadow rays: the cooperative walk
+    d, ld = ds0.render(0, seed=9)
     monkeypatch.setenv("RTG_DEFER", "0")
     b, lb = ds0.render(0, seed=9)
     n = int((a.view(np.uint32) != b.view(np.uint32)).any(axis=2).sum())
-    print(name, "differing pixels", n)
-    assert n == 0 and np.array_equal(la, lb)
+    m = int((a.view(np.uint32) != d.view(np.uint32)).any(axis=2).sum())
+    print(name, "differing pixels", n, "(shadow deferral alone:", m, ")")
+    assert n == 0 and m == 0 and np.array_equal(la, lb) and np.array_equal(la, ld)
     assert np.array_equal(a.view(np.uint32), c.view(np.uint32))
