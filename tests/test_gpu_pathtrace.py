@@ -122,12 +122,16 @@ def _bits(a):
     return a.view(np.uint32)
 
 
+@pytest.mark.parametrize("split", ["1", "0"])
 @pytest.mark.parametrize("name", PT_ONLY)
 @pytest.mark.parametrize("spp", [1, 4])
-def test_path_wavefront_equals_fused(name, spp, tmp_path):
+def test_path_wavefront_equals_fused(name, spp, split, tmp_path, monkeypatch):
     """The wavefront path tracer (rtg_path.hip, forced with RTG_RENDER_TREE) gives the fused
-    kernel's image bit for bit: the same node steps (rtg_node.hpp) on the same RNG keys.  The
-    first render plans its later passes from its first; the second runs planned throughout."""
+    kernel's image bit for bit: the same node steps (rtg_node.hpp) on the same RNG keys -- with
+    the step as one kernel (the default) and split by node kind (RTG_PATH_SPLIT=1: k_path_hit /
+    k_path_rest / k_path_unwind).  The first render plans its later passes from its first; the
+    second runs planned throughout."""
+    monkeypatch.setenv("RTG_PATH_SPLIT", split)
     hs = _scene(tmp_path, name, spp)
     ds = rtgpu.DeviceScene(hs, 0)
     b, lb = ds.render(0, seed=11, flags=rtgpu.RTG_RENDER_FUSED)
@@ -139,12 +143,14 @@ def test_path_wavefront_equals_fused(name, spp, tmp_path):
     assert "path_iterations" in ds.timings()
 
 
+@pytest.mark.parametrize("split", ["1", "0"])
 @pytest.mark.parametrize("env", ["RTG_PATH_SYNC", "RTG_PATH_PLAN_TIGHT"])
-def test_path_wavefront_host_driven_and_overflow(env, tmp_path, monkeypatch):
+def test_path_wavefront_host_driven_and_overflow(env, split, tmp_path, monkeypatch):
     """Every pass host-driven (RTG_PATH_SYNC), and plans one iteration short
     (RTG_PATH_PLAN_TIGHT: every planned pass leaves paths, the render is redone host-driven):
     the same image as the fused kernel."""
     monkeypatch.setenv(env, "1")
+    monkeypatch.setenv("RTG_PATH_SPLIT", split)
     hs = _scene(tmp_path, "pt_nee", 4)
     ds = rtgpu.DeviceScene(hs, 0)
     b, _ = ds.render(0, seed=5, flags=rtgpu.RTG_RENDER_FUSED)
@@ -153,10 +159,13 @@ def test_path_wavefront_host_driven_and_overflow(env, tmp_path, monkeypatch):
         assert np.array_equal(_bits(a), _bits(b)), ob.compare(a, b)
 
 
-def test_path_wavefront_stats_and_bands(tmp_path):
+@pytest.mark.parametrize("name", ["pt_cornell", "pt_nee"])
+@pytest.mark.parametrize("split", ["1", "0"])
+def test_path_wavefront_stats_and_bands(name, split, tmp_path, monkeypatch):
     """Ray counts of the wavefront path tracer equal the fused kernel's; row bands rendered
     separately give the whole frame (part_pixel mapping of the path queues)."""
-    hs = _scene(tmp_path, "pt_cornell", 2)
+    monkeypatch.setenv("RTG_PATH_SPLIT", split)
+    hs = _scene(tmp_path, name, 2)
     ds = rtgpu.DeviceScene(hs, 0)
     ds.reset_stats()
     ds.render(0, seed=17, flags=rtgpu.RTG_RENDER_FUSED | rtgpu.RTG_RENDER_COUNT_STATS)
