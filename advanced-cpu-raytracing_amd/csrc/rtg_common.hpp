@@ -223,14 +223,14 @@ DEV bool box_hit_fast(float mnx, float mny, float mnz, float mxx, float mxy, flo
     const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
     const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
     const float atmin = fabsf(tmin), atmax = fabsf(tmax);
-    const float slack = 0x1p-20f * (atmin + atmax) + 1e-30f;
+    const float slack = fmaf(0x1p-20f, atmin + atmax, 1e-30f);   // (fma: one rounding, tighter)
     // all three decisions clear of their boundaries.  NaN fails every comparison and an
     // infinite tmin or tmax makes the slack infinite, so both take the exact test; with both
     // finite, minT = inf passes the last test (tmax >= tmin decided, tmin < inf exact)
     // (round 4: dropping the separate range and minT = inf terms took the headline k_primary
     // 0.2052 -> 0.1915 ms, profiles/r04y_slab_lean_ab.txt)
     const bool sure = (int)q.fast & (atmax >= 1e-30f) & (fabsf(tmax - tmin) > slack) &
-                      (fabsf(tmin - minT) > 0x1p-20f * atmin + 1e-30f);
+                      (fabsf(tmin - minT) > fmaf(0x1p-20f, atmin, 1e-30f));
     bool hit = (tmax > 0) & (tmax >= tmin) & (tmin < minT);
     if constexpr (UNI) {
         if (__builtin_expect(__ballot(on & !sure) != 0, 0)) {
@@ -308,7 +308,7 @@ DEV bool tri_test_fast(const DevScene& S, int f, const Ray& r, float minT, float
             if (gsure) {
                 if (gama < 0) return false;
                 const float sum = gama + beta;
-                if (fabsf(sum - 1.0f) > 0x1p-19f * sum + 0x1p-22f) {
+                if (fabsf(sum - 1.0f) > fmaf(0x1p-19f, sum, 0x1p-22f)) {
                     if (sum > 1) return false;
                     float t = det3(E1.x, E2.x, sx, E1.y, E2.y, sy, E1.z, E2.z, sz) / detA;
                     tout = t;
@@ -340,7 +340,7 @@ DEV bool tri_test_fast_rec(const float4* R, const Ray& r, float minT, float& tou
             if (gsure) {
                 if (gama < 0) return false;
                 const float sum = gama + beta;
-                if (fabsf(sum - 1.0f) > 0x1p-19f * sum + 0x1p-22f) {
+                if (fabsf(sum - 1.0f) > fmaf(0x1p-19f, sum, 0x1p-22f)) {
                     if (sum > 1) return false;
                     float t = det3(E1.x, E2.x, sx, E1.y, E2.y, sy, E1.z, E2.z, sz) / detA;
                     tout = t;
@@ -371,7 +371,7 @@ DEV bool tri_test_sel(const float4* R, const Ray& r, float limit, float& tout, b
     const bool range = (ad >= 0x1p-100f) & (ad <= 0x1p100f);
     const bool bsure = (nb == 0.0f) | (fabsf(beta) > 1e-30f);
     const bool gsure = (ng == 0.0f) | (fabsf(gama) > 1e-30f);
-    const bool ssure = fabsf(sum - 1.0f) > 0x1p-19f * sum + 0x1p-22f;
+    const bool ssure = fabsf(sum - 1.0f) > fmaf(0x1p-19f, sum, 0x1p-22f);
     // tri_test_fast_rec's decision tree: false / t test / exact fallback
     const bool b_out = range & bsure & (beta < 0);
     const bool g_out = range & bsure & !(beta < 0) & gsure & (gama < 0);
@@ -1016,7 +1016,7 @@ DEV bool slab_cons(float lx, float ly, float lz, float hx, float hy, float hz, c
     const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
     const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
     tnear = tmin;
-    return (tmax > -1e-30f) & (tmax >= tmin * (1.0f - 0x1p-21f) - 1e-30f) & (tmin < minTc);
+    return (tmax > -1e-30f) & (tmax >= fmaf(tmin, 1.0f - 0x1p-21f, -1e-30f)) & (tmin < minTc);
 }
 
 // DEFER (large-leaf scenes, the packet walk): a leaf slot of more than RTG_DEFER_ANY_LEAF entries
@@ -1493,7 +1493,7 @@ DEV bool slab_cons2(float lx, float ly, float lz, float hx, float hy, float hz, 
     const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
     const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
     tnear = tmin;
-    hinf = (tmax > -1e-30f) & (tmax >= tmin * (1.0f - 0x1p-21f) - 1e-30f);
+    hinf = (tmax > -1e-30f) & (tmax >= fmaf(tmin, 1.0f - 0x1p-21f, -1e-30f));
     return hinf & (tmin < minTc);
 }
 // wave minimum of a non-negative float (the lanes that do not take part hold +inf)
