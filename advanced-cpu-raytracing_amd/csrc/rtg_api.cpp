@@ -501,6 +501,9 @@ static int build_wide(const std::vector<float4>& nodes, int root, std::vector<rt
 int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     if (!d || !out) return set_err(RTG_ERR_INVALID, "null argument");
     *out = nullptr;
+    // the packet walks address records by 32-bit byte offsets (rtg_common.hpp rec_at)
+    if (d->num_faces > ((int64_t)1 << 25))
+        return set_err(RTG_ERR_INVALID, "%lld faces: at most 2^25 per scene", (long long)d->num_faces);
     for (int i = 0; i < d->num_mesh_lights; ++i) {
         const int o = d->mesh_lights ? d->mesh_lights[i].object : -1;
         if (o < 0 || o >= d->num_objects || d->objects[o].kind != RTG_OBJ_MESH ||

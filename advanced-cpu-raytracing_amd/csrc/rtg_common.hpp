@@ -690,6 +690,21 @@ DEV int wave_min_int(int v) {
 constexpr int kDeferLeaf = 16;
 // A leaf is deferred only for the lanes of a wave that reach it when they are few; when many
 // reach it together the wave tests it in the walk, every lane busy (RTG_DEFER_LANES: A/B)
+// packet walks address their scalar records by 32-bit byte offsets: two scalar ops fewer per
+// record than a 64-bit index; scenes are limited to 2^25 faces (rtg_scene_create), which keeps
+// every node, wide node and face-record array below 4 GiB (k_primary 0.1881 -> 0.1828 ms,
+// profiles/r04aa_addr_on_ab.txt)
+#ifndef RTG_NODE_ADDR32
+#define RTG_NODE_ADDR32 1
+#endif
+template <int BYTES, typename T>
+DEV const T* rec_at(const T* base, int i) {
+#if RTG_NODE_ADDR32
+    return (const T*)((const char*)base + (uint32_t)i * (uint32_t)BYTES);
+#else
+    return (const T*)((const char*)base + (size_t)i * BYTES);
+#endif
+}
 #ifndef RTG_DEFER_LANES
 #define RTG_DEFER_LANES 16
 #endif
@@ -736,7 +751,7 @@ DEV bool walk_bvh_packet(const DevScene& S, const int begin, const int end, cons
         float4 a, b;
         if constexpr (SC) {
             rtg_s8 nd;
-            sload_node(S.nodes + 2 * i, nd);
+            sload_node(rec_at<32>(S.nodes, i), nd);
             a = f4(nd[0], nd[1], nd[2], nd[3]);
             b = f4(nd[4], nd[5], nd[6], nd[7]);
         } else {
@@ -793,7 +808,7 @@ DEV bool walk_bvh_packet(const DevScene& S, const int begin, const int end, cons
                     if constexpr (SC) {
                         rtg_s8 ra;
                         rtg_s4 rb;
-                        sload_rec(S.tris + 3 * (size_t)f, ra, rb);
+                        sload_rec(rec_at<48>(S.tris, f), ra, rb);
                         const float4 R[3] = {f4(ra[0], ra[1], ra[2], ra[3]), f4(ra[4], ra[5], ra[6], ra[7]),
                                              f4(rb[0], rb[1], rb[2], rb[3])};
                         if (pass) c.template tri<ANY>();
@@ -1148,7 +1163,7 @@ DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0
         }
         node = __builtin_amdgcn_readfirstlane(node);
         rtg_s16 na, nb;
-        sload_wnode(S.anodes + node, na, nb);
+        sload_wnode(rec_at<128>(S.anodes, node), na, nb);
         const float4 lox = f4(na[0], na[1], na[2], na[3]), hix = f4(na[4], na[5], na[6], na[7]);
         const float4 loy = f4(na[8], na[9], na[10], na[11]), hiy = f4(na[12], na[13], na[14], na[15]);
         const float4 loz = f4(nb[0], nb[1], nb[2], nb[3]), hiz = f4(nb[4], nb[5], nb[6], nb[7]);
@@ -1210,7 +1225,7 @@ DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0
             for (int e = first; e < first + cnt; ++e) {
                 rtg_s8 ra;
                 rtg_s4 rb;
-                sload_rec(S.ahtris + 3 * (size_t)e, ra, rb);
+                sload_rec(rec_at<48>(S.ahtris, e), ra, rb);
 #if RTG_PK_SELECT
                 if (h[k]) c.template tri<true>();
                 const float4 R[3] = {f4(ra[0], ra[1], ra[2], ra[3]), f4(ra[4], ra[5], ra[6], ra[7]), f4(rb[0], rb[1], rb[2], rb[3])};
@@ -1218,7 +1233,7 @@ DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0
                 const bool ok = tri_test_sel(R, lr, limit, t) & h[k];
                 if (!__ballot(ok)) continue;
                 rtg_s8 rn;
-                sload_node(S.nodes + 2 * ra[3], rn);
+                sload_node(rec_at<32>(S.nodes, ra[3]), rn);
                 const bool reach = ok & box_hit_fast<true>(__int_as_float(rn[0]), __int_as_float(rn[1]), __int_as_float(rn[2]),
                                                            __int_as_float(rn[3]), __int_as_float(rn[4]), __int_as_float(rn[5]),
                                                            lr, q, minT0);
@@ -1237,7 +1252,7 @@ DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0
                 float t;
                 if (!tri_test_fast_rec(R, lr, limit, t)) continue;
                 rtg_s8 rn;
-                sload_node(S.nodes + 2 * ra[3], rn);
+                sload_node(rec_at<32>(S.nodes, ra[3]), rn);
                 const float4 a = f4(rn[0], rn[1], rn[2], rn[3]), b = f4(rn[4], rn[5], rn[6], rn[7]);
                 if (!box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, minT0)) continue;   // leaf unreachable
                 if (inst_conf && box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, limit)) {
@@ -1528,7 +1543,7 @@ DEV bool walk_closest_pk(const DevScene& S, int node, const int k, const Ray& lr
         if (++steps > RTG_PK_MAX_STEPS) return false;
         node = __builtin_amdgcn_readfirstlane(node);
         rtg_s16 na, nb;
-        sload_wnode(S.anodes + node, na, nb);
+        sload_wnode(rec_at<128>(S.anodes, node), na, nb);
         const float4 lox = f4(na[0], na[1], na[2], na[3]), hix = f4(na[4], na[5], na[6], na[7]);
         const float4 loy = f4(na[8], na[9], na[10], na[11]), hiy = f4(na[12], na[13], na[14], na[15]);
         const float4 loz = f4(nb[0], nb[1], nb[2], nb[3]), hiz = f4(nb[4], nb[5], nb[6], nb[7]);
@@ -1552,7 +1567,7 @@ DEV bool walk_closest_pk(const DevScene& S, int node, const int k, const Ray& lr
             for (int e = first; e < first + cnt; ++e) {
                 rtg_s8 ra;
                 rtg_s4 rb;
-                sload_rec(S.ahtris + 3 * (size_t)e, ra, rb);
+                sload_rec(rec_at<48>(S.ahtris, e), ra, rb);
                 const float4 R[3] = {f4(ra[0], ra[1], ra[2], ra[3]), f4(ra[4], ra[5], ra[6], ra[7]),
                                      f4(rb[0], rb[1], rb[2], rb[3])};
                 const int f = ra[7];
@@ -1562,7 +1577,7 @@ DEV bool walk_closest_pk(const DevScene& S, int node, const int k, const Ray& lr
                 const bool better = ok && hit_less(t, k, f, B.bestT, B.bestK, B.bestF);
                 if (!__ballot(better)) continue;
                 rtg_s8 rn;
-                sload_node(S.nodes + 2 * ra[3], rn);
+                sload_node(rec_at<32>(S.nodes, ra[3]), rn);
                 const float bx0 = __int_as_float(rn[0]), by0 = __int_as_float(rn[1]), bz0 = __int_as_float(rn[2]);
                 const float bx1 = __int_as_float(rn[3]), by1 = __int_as_float(rn[4]), bz1 = __int_as_float(rn[5]);
                 // visible: the reference leaf box passes at next_up(t) (its entry is at most t)

@@ -267,7 +267,8 @@ typedef struct rtg_scene rtg_scene;
 
 /* Replaces Raytracer::Raytracer(Scene&) (raytracer.cpp:7-16, which copies the
  * scene): uploads a device-resident replica of `desc` to HIP device `device`.
- * The caller may free `desc` after return. */
+ * The caller may free `desc` after return.  At most 2^25 faces (RTG_ERR_INVALID
+ * beyond: the traversal kernels address records by 32-bit byte offsets). */
 int rtg_scene_create(const rtg_scene_desc* desc, int device, rtg_scene** out);
 /* The device's traversal data, for inspection and tests: the walk's node records (8 floats
  * per node, pre-order layout of the BVH nodes, the trailing pad node included) and the
