@@ -1184,7 +1184,9 @@ DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
             const int cr = cidx[k];
-            if (cr == WCHILD_EMPTY || !__ballot(h[k])) continue;
+            // (a local copy: writes into h[] made the compiler pack the four masks into VGPR bytes)
+            bool hk = h[k];
+            if (cr == WCHILD_EMPTY || !__ballot(hk)) continue;
             if (cr >= 0) {
                 const float t = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tn[k]), lead));
                 int spill = cr;
@@ -1204,21 +1206,21 @@ DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0
             }
             const int first = lidx[k] >> 8, cnt = lidx[k] & 255;
             if constexpr (DEFER) {
-                const uint64_t m = __ballot(h[k]);
+                const uint64_t m = __ballot(hk);
                 if (cnt > RTG_DEFER_ANY_LEAF && __popcll(m) <= RTG_DEFER_ANY_LANES) {
                     const int lane = threadIdx.x & 63, lead = __ffsll((long long)m) - 1;
                     int base = 0;
                     if (lane == lead) base = atomicAdd(ad->count, __popcll(m));
                     base = __shfl(base, lead);
                     const int slot = base + __popcll(m & ((1ull << lane) - 1ull));
-                    if (h[k] && slot < ad->cap) {
+                    if (hk && slot < ad->cap) {
                         float4* qe = ad->e + 3 * (size_t)slot;
                         qe[0] = make_float4(lr.o.x, lr.o.y, lr.o.z, minT0);
                         qe[1] = make_float4(lr.d.x, lr.d.y, lr.d.z, limit);
                         qe[2] = make_float4(__int_as_float(first), __int_as_float(cnt), __int_as_float(ad->q),
                                             __int_as_float((int)inst_conf));
                         ad->deferred = true;
-                        h[k] = false;
+                        hk = false;
                     }
                 }
             }
@@ -1227,10 +1229,10 @@ DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0
                 rtg_s4 rb;
                 sload_rec(rec_at<48>(S.ahtris, e), ra, rb);
 #if RTG_PK_SELECT
-                if (h[k]) c.template tri<true>();
+                if (hk) c.template tri<true>();
                 const float4 R[3] = {f4(ra[0], ra[1], ra[2], ra[3]), f4(ra[4], ra[5], ra[6], ra[7]), f4(rb[0], rb[1], rb[2], rb[3])};
                 float t;
-                const bool ok = tri_test_sel(R, lr, limit, t) & h[k];
+                const bool ok = tri_test_sel(R, lr, limit, t) & hk;
                 if (!__ballot(ok)) continue;
                 rtg_s8 rn;
                 sload_node(rec_at<32>(S.nodes, ra[3]), rn);
@@ -1243,10 +1245,10 @@ DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0
                                                      lr, q, limit);
                 occ |= suff;
                 live &= !suff;
-                h[k] &= !suff;
+                hk &= !suff;
                 undecided |= reach & !suff;
 #else
-                if (!h[k]) continue;
+                if (!hk) continue;
                 c.template tri<true>();
                 const float4 R[3] = {f4(ra[0], ra[1], ra[2], ra[3]), f4(ra[4], ra[5], ra[6], ra[7]), f4(rb[0], rb[1], rb[2], rb[3])};
                 float t;
@@ -1258,7 +1260,7 @@ DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0
                 if (inst_conf && box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, limit)) {
                     live = false;
                     occ = true;
-                    h[k] = false;
+                    hk = false;
                     continue;
                 }
                 undecided = true;
