@@ -1000,9 +1000,11 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
 // compiled for this many waves per SIMD.  Per-lane walk (RTG_ANY_PACKET=0): five (96 VGPRs, no
 // spills) measured 0.228 ms on the headline against 0.291 at six (76 B of spills) and 0.26 at the
 // natural four.  Packet walk (default): 81 VGPRs and no LDS stack at five, six 0.211 ms, seven
-// 0.215, eight 0.216 (profiles/r03pk4_*); instance scenes keep RTG_INST_WAVES
+// 0.215, eight 0.216 (profiles/r03pk4_*); instance scenes keep RTG_INST_WAVES.  Round 4, after
+// the leaner slab test and mask copies: five 0.193, six 0.1804, seven 0.1742, eight 0.270 ms
+// (spills), large-leaf configurations unchanged (profiles/r04ad_wide_waves_ab.txt, r04ae_wide_waves_configs_ab.txt)
 #ifndef RTG_WIDE_WAVES_PLAIN
-#define RTG_WIDE_WAVES_PLAIN (RTG_ANY_PACKET ? 6 : 5)
+#define RTG_WIDE_WAVES_PLAIN (RTG_ANY_PACKET ? 7 : 5)
 #endif
 #define RTG_WIDE_WAVES(FEAT) (((FEAT) & FEAT_INSTANCE) ? RTG_INST_WAVES : RTG_WIDE_WAVES_PLAIN)
 
