@@ -400,17 +400,22 @@ bool load_exr(const std::string& path, int& width, int& height, std::vector<floa
                 q += 16;
             }
         } else if (name == "compression") {
+            if (sz < 1) { err = "bad EXR compression attribute"; return false; }
             comp = v[0];
         } else if (name == "dataWindow") {
+            if (sz < 16) { err = "bad EXR dataWindow attribute"; return false; }
             for (int k = 0; k < 4; ++k) dw[k] = rd<int32_t>(v + 4 * k);
         } else if (name == "lineOrder") {
+            if (sz < 1) { err = "bad EXR lineOrder attribute"; return false; }
             lineOrder = v[0];
         }
         p += sz;
     }
-    width = dw[2] - dw[0] + 1;
-    height = dw[3] - dw[1] + 1;
-    if (chans.empty() || width <= 0 || height <= 0) { err = "EXR without channels / data window"; return false; }
+    const int64_t w64 = int64_t(dw[2]) - dw[0] + 1, h64 = int64_t(dw[3]) - dw[1] + 1;
+    if (chans.empty() || w64 <= 0 || h64 <= 0) { err = "EXR without channels / data window"; return false; }
+    if (w64 > (1 << 16) || h64 > (1 << 16) || w64 * h64 > (int64_t(1) << 28)) { err = "EXR data window too large"; return false; }
+    width = int(w64);
+    height = int(h64);
     int lines;
     switch (comp) {
         case 0: case 1: case 2: lines = 1; break;      // NONE, RLE, ZIPS
@@ -441,11 +446,14 @@ bool load_exr(const std::string& path, int& width, int& height, std::vector<floa
     std::vector<unsigned char> raw, tmp;
     for (int b = 0; b < nblocks; ++b) {
         const uint64_t off = rd<uint64_t>(d + p + 8 * size_t(b));
-        if (off + 8 > n) { err = "bad EXR chunk offset"; return false; }
+        // subtractions, not sums: a 64-bit offset near 2^64 must not wrap past the check
+        if (off > n || n - off < 8) { err = "bad EXR chunk offset"; return false; }
         const int y = rd<int32_t>(d + off);
         const uint32_t len = rd<uint32_t>(d + off + 4);
-        if (off + 8 + len > n) { err = "truncated EXR chunk"; return false; }
-        const int line0 = y - dw[1];
+        if (len > n - off - 8) { err = "truncated EXR chunk"; return false; }
+        const int64_t line0_64 = int64_t(y) - dw[1];
+        if (line0_64 < 0 || line0_64 >= height) { err = "bad EXR chunk line"; return false; }
+        const int line0 = int(line0_64);
         const int nl = std::min(lines, height - line0);
         if (line0 < 0 || nl <= 0) { err = "bad EXR chunk line"; return false; }
         const size_t need = size_t(nl) * width * pixBytes;

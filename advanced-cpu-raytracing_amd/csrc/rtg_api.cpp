@@ -87,6 +87,7 @@ struct WaveWork {
     void* mem = nullptr;
     void* dq = nullptr;               // deferred-leaf queue + per-pixel hit keys (ensure_defer)
     size_t dq_nq = 0;                 // its shadow-state entries
+    size_t dq_pixels = 0;             // the pixel count its hit-key array (and so its layout) was sized for
     rtg::WaveBufs W{};
 };
 constexpr int kWorkCtx = 3;
@@ -1130,16 +1131,22 @@ static int ensure_wave(WaveWork& ww, size_t pixels, int slots, size_t tiles) {
     W.shadow_state = nullptr;
     W.dq_cap = 0;
     ww.dq_nq = 0;
+    ww.dq_pixels = 0;
     return RTG_OK;
 }
 
 // The deferred-leaf queue of a large-leaf scene's camera walk (WaveBufs dq_*, hit_key): two
 // entries per pixel of capacity (an entry that does not fit is tested in the walk).
+// Layout [256 B counts | pixels x 8 B keys | cap x 48 B entries | nq x 4 B states]: the entry
+// and state offsets depend on the pixel count, so a buffer laid out for fewer pixels is never
+// reused (the 1 024-entry floor on cap alone would let keys overrun the entries).
 static int ensure_defer(WaveWork& ww, size_t pixels, size_t nq) {
-    const size_t cap = std::max<size_t>(2 * pixels, 1024);
-    if (ww.dq && ww.W.dq_cap >= (int)cap && ww.dq_nq >= nq) return RTG_OK;
+    if (ww.dq && ww.dq_pixels >= pixels && ww.W.dq_cap >= (int)std::max<size_t>(2 * pixels, 1024) && ww.dq_nq >= nq)
+        return RTG_OK;
     if (ww.dq) { (void)hipFree(ww.dq); ww.dq = nullptr; }
     nq = std::max(nq, ww.dq_nq);
+    pixels = std::max(pixels, ww.dq_pixels);
+    const size_t cap = std::max<size_t>(2 * pixels, 1024);
     const size_t bytes = 256 + pixels * 8 + cap * 48 + nq * 4;
     HIP_TRY(hipMalloc(&ww.dq, bytes));
     char* b = (char*)ww.dq;
@@ -1149,6 +1156,7 @@ static int ensure_defer(WaveWork& ww, size_t pixels, size_t nq) {
     ww.W.shadow_state = (int*)(b + 256 + pixels * 8 + cap * 48);
     ww.W.dq_cap = (int)cap;
     ww.dq_nq = nq;
+    ww.dq_pixels = pixels;
     return RTG_OK;
 }
 

@@ -110,8 +110,8 @@ __global__ __launch_bounds__(256) void k_bigleaf(const DevScene S, const WaveBuf
 // A pending pixel's hit from its key, checked: the winner's reference leaf box (and an
 // instance's world box) must pass the exact slab test at next_up(t) -- else the reference walk
 // decides (rtg_common.hpp DeferCtx).
-// (the production render's counters are otherwise untouched: extend_wide_visits counts the
-// pending pixels and extend_fallbacks those the check sent to the reference walk -- diagnostics)
+// (diagnostics, RTG_DEFER_DIAG=1 only -- counters is null otherwise: extend_wide_visits counts
+// the pending pixels and extend_fallbacks those the check sent to the reference walk)
 template <int FEAT>
 __global__ __launch_bounds__(256) void k_hitfix(const DevScene S, const DevCamera C, const RenderParams P,
                                                 const int sample, const WaveBufs W, DevCounters* counters) {
@@ -702,6 +702,7 @@ bool frame_kernel();
 bool defer_leaves();
 int defer_any_leaves();
 bool wide_bigleaf();
+bool defer_diag();
 
 // One traversal variant's pass sequence (instantiated in rtg_wave_a.hip / rtg_wave_b.hip).
 template <bool STATS, int FEAT>
@@ -758,7 +759,8 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
                 hipLaunchKernelGGL((k_primary<STATS, FEAT, 0, true>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s,
                                    W, cnt);
                 hipLaunchKernelGGL((k_bigleaf<FEAT>), dim3(2048), dim3(256), 0, st, S, W);
-                hipLaunchKernelGGL((k_hitfix<FEAT>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
+                hipLaunchKernelGGL((k_hitfix<FEAT>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W,
+                                   defer_diag() ? cnt : nullptr);
                 hipLaunchKernelGGL((k_refwalk<FEAT>), dim3(256), dim3(256), 0, st, S, C, P, s, W);
                 deferred = true;
             }

@@ -32,6 +32,14 @@ __global__ __launch_bounds__(256) void k_resolve(const DevCamera C, const Render
 // (experiment; by default they take the cooperative reference walk)
 bool wide_bigleaf() { return std::getenv("RTG_WIDE_BIGLEAF") != nullptr; }
 
+// RTG_DEFER_DIAG=1: k_hitfix counts pending / checked-out pixels of production renders into
+// extend_wide_visits / extend_fallbacks (tools/diag_defer.py); otherwise an uncounted render
+// leaves the counters untouched, as every other pipeline does
+bool defer_diag() {
+    const char* v = std::getenv("RTG_DEFER_DIAG");
+    return v && std::strcmp(v, "0") != 0;
+}
+
 // Large leaves of the camera walk deferred to k_bigleaf (production renders of large-leaf scenes;
 // RTG_DEFER=0: the cooperative walk, A/B)
 bool defer_leaves() {

@@ -140,10 +140,11 @@ def render_part(ds, rank: int, world: int, d_hdr: int, d_ldr: int, stream: int, 
     """Rank ``rank``'s share of one frame.
 
     With a ``frame`` and ``overlap`` (the default): rtg_render of part rank/world straight into
-    the shared host framebuffer -- for frames of a million pixels or more the library renders
-    the part in row chunks on two streams and DMAs each chunk's rows while the next chunks
-    render (rtg_api.cpp render_chunked), so only the last chunk's copy adds to the frame time.
-    Synchronous; the device buffers are not written.
+    the shared page-locked host framebuffer -- the kernels write the part's pixels over the bus
+    as they render, so no copy follows.  Synchronous; ``stream``, ``d_hdr`` and
+    ``d_ldr`` are unused.  (RTG_HOST_CHUNKS=1 opts into rendering the part in row chunks on two
+    streams with each chunk's DMA overlapping the next chunk: measured slower, rtg_api.cpp
+    render_chunked.)
     Otherwise: render the part into its device buffers (full-frame sized; only its rows are
     written) and, with a ``frame``, enqueue the DMA of those rows into the shared host
     framebuffer after it.  Asynchronous on ``stream``."""

@@ -337,6 +337,82 @@ def config_c3(out_dir: str, K: int = 70000, width: int = 1920, height: int = 108
     return _write(out_dir, "c3_blob", xml)
 
 
+def config_defer_gate(out_dir: str, pad_objects: int = 0, pad_faces: int = 0, K: int = 20000, width: int = 320,
+                      height: int = 180) -> str:
+    """The reduced C3 blob (large leaves: pole fans) at depth 0, with padding meshes placed
+    BEFORE it in object order, behind the camera: ``pad_objects`` one-face meshes and one mesh of
+    ``pad_faces`` faces (a height field).  They push the blob's object index and its faces'
+    record indices up to the limits of the deferred-leaf key (12 object bits, 20 face bits;
+    rtg_common.hpp obj_key, gate in rtg_wave.hpp) without changing the image."""
+    os.makedirs(out_dir, exist_ok=True)
+    v, f = blob_mesh(K, center=(0, 1.0, 0), radius=1.0, seed=7)
+    write_ply(os.path.join(out_dir, "gate_blob.ply"), v, f)
+    pads = []
+    if pad_faces > 0:
+        n = int(np.ceil(np.sqrt(pad_faces / 2.0)))
+        pv, pf = heightfield_mesh(2 * n * n, (-40.0, 40.0, -40.0, 40.0), seed=3)
+        pv = pv[:, [0, 2, 1]] + np.array([0.0, -1.0, 60.0], np.float32)     # a floor patch behind the camera
+        write_ply(os.path.join(out_dir, "gate_pad.ply"), pv, pf[:pad_faces])
+        pads.append('        <Mesh id="{id}">\n            <Material>2</Material>\n'
+                    '            <Faces plyFile="gate_pad.ply"/>\n        </Mesh>')
+    gv, gf = _ground(6.0)
+    # one-face pads: vertices 5.. (after the ground's 4), small triangles behind the camera
+    pv_lines = []
+    for k in range(pad_objects):
+        x, z = (k % 64) * 0.5 - 16.0, 40.0 + (k // 64) * 0.5
+        pv_lines.append(f"{x} 0 {z}\n        {x + 0.3} 0 {z}\n        {x} 0.3 {z}")
+        b = 5 + 3 * k
+        pads.append(f'        <Mesh id="{{id}}">\n            <Material>2</Material>\n'
+                    f'            <Faces>{b} {b + 1} {b + 2}</Faces>\n        </Mesh>')
+    objs = "\n".join(p.format(id=i + 1) for i, p in enumerate(pads))
+    nid = len(pads)
+    xml = f"""<Scene>
+    <MaxRecursionDepth>0</MaxRecursionDepth>
+    <BackgroundColor>5 5 10</BackgroundColor>
+    <ShadowRayEpsilon>1e-3</ShadowRayEpsilon>
+{_lookat_camera((0, 1.6, 4.2), (0, 0.9, 0), (0, 1, 0), 38, (width, height), 'gate.png', 1)}
+    <Lights>
+        <AmbientLight>8 8 8</AmbientLight>
+        <PointLight id="1">
+            <Position>0.5 4 3</Position>
+            <Intensity>30000 28000 26000</Intensity>
+        </PointLight>
+    </Lights>
+    <Materials>
+        <Material id="1">
+            <AmbientReflectance>0.3 0.3 0.3</AmbientReflectance>
+            <DiffuseReflectance>0.7 0.55 0.4</DiffuseReflectance>
+            <SpecularReflectance>0.4 0.4 0.4</SpecularReflectance>
+            <PhongExponent>30</PhongExponent>
+        </Material>
+        <Material id="2">
+            <AmbientReflectance>0.3 0.3 0.3</AmbientReflectance>
+            <DiffuseReflectance>0.5 0.5 0.55</DiffuseReflectance>
+            <SpecularReflectance>0 0 0</SpecularReflectance>
+        </Material>
+    </Materials>
+    <VertexData>
+        {gv}
+        {chr(10).join(pv_lines)}
+    </VertexData>
+    <Objects>
+{objs}
+        <Mesh id="{nid + 1}">
+            <Material>2</Material>
+            <Faces>
+                {gf}
+            </Faces>
+        </Mesh>
+        <Mesh id="{nid + 2}">
+            <Material>1</Material>
+            <Faces plyFile="gate_blob.ply"/>
+        </Mesh>
+    </Objects>
+</Scene>
+"""
+    return _write(out_dir, "gate", xml)
+
+
 def config_c3_ton(out_dir: str, ply_dir: str, width: int = 1920, height: int = 1080, spp: int = 4) -> str:
     """C3 on a real mesh (SURVEY §8d's stand-in for the missing bunny): the reference's own
     archive/hw1_inputs/akif_uslu/ton_Roosendaal_smooth scene (62 160-triangle mesh_2.ply plus

@@ -16,8 +16,8 @@ flight"), so a frame's kernels overlap the next frames' -- a part of 1/N of one 
 is too small a grid to keep a GPU busy; `config.serial` times the same steps
 on one stream, one frame after the other.  `value` = rays of the frames x steps /
 max-over-ranks time.
-The host framebuffer gather (every rank DMA-ing its rows into one page-locked shared frame)
-is timed separately ("gather"); the one-process host-buffer path of the CLI ("host_frame")
+The host framebuffer gather (every rank rendering its rows straight into one page-locked
+shared frame) is timed separately ("gather"); the one-process host-buffer path of the CLI ("host_frame")
 too -- neither is `value` (the PCIe-inclusive rates).
 """
 import argparse
@@ -565,8 +565,8 @@ def main():
         }
 
         if not args.no_extras:
-            # host framebuffer gather: every rank DMAs its rows into one page-locked shared
-            # frame (LDR = what main.cpp saves; + the float frame for a tonemapped camera)
+            # host framebuffer gather: every rank renders its rows straight into one page-locked
+            # shared frame (LDR = what main.cpp saves; + the float frame for a tonemapped camera)
             name = f"rtg_bench_{os.environ.get('MASTER_PORT', str(os.getpid()))}"
             if rank == 0:
                 frame = multigpu.SharedFrame(name, H, W, hdr=cam["tonemapped"], ldr=True, create=True)
@@ -581,7 +581,9 @@ def main():
             result["gather"] = {"ms_per_frame": round(g_el / args.steps * 1e3, 4),
                                 "mrays_s": round(rays * args.steps / g_el / 1e6, 2),
                                 "bytes_per_frame": int(H * W * 3 * (5 if cam["tonemapped"] else 1)),
-                                "what": "render + DMA of each rank's rows into one page-locked /dev/shm frame"}
+                                "what": "rtg_render of each rank's part straight into one page-locked /dev/shm frame "
+                                        "(the kernels write the pixels over the bus, no copy after the render; "
+                                        "multigpu.render_part)"}
             if world == 1:
                 # the drop-in host path (rtg_render: per-scene stream, page-locked frame, as the CLI)
                 ph = rtgpu.PinnedArray((H, W, 3), "float32") if cam["tonemapped"] else None

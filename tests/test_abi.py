@@ -123,3 +123,42 @@ def test_resolve_accum_matches_reference_clamp():
     assert np.array_equal(ldr, ob.clamp_ldr(hdr))
     assert ldr[1, 1, 0] == 0     # x86 cvttss2si overflow -> INT_MIN -> clamp 0
     assert ldr[1, 2, 0] == 0     # NaN -> 0
+
+
+def _desc_layout(tmp_path):
+    import shutil
+    cc = shutil.which("gcc") or shutil.which("cc")
+    if not cc:
+        pytest.skip("no C compiler")
+    src = tmp_path / "lay.c"
+    src.write_text('#include "rtgpu.h"\n#include <stdio.h>\n#include <stddef.h>\nint main(void){printf("%zu %zu %zu %zu\\n", '
+                   'sizeof(rtg_scene_desc), offsetof(rtg_scene_desc, faces), offsetof(rtg_scene_desc, num_faces), '
+                   'sizeof(rtg_face));return 0;}\n')
+    exe = tmp_path / "lay"
+    subprocess.run([cc, "-I", os.path.join(ROOT, "include"), str(src), "-o", str(exe)], check=True)
+    return map(int, subprocess.run([str(exe)], capture_output=True, text=True).stdout.split())
+
+
+def test_face_limit_refused(tmp_path):
+    """rtg_scene_create refuses descriptions of more than 2^25 faces with RTG_ERR_INVALID
+    before touching a device (rtg_api.cpp: the packet walks address node and face records by
+    32-bit byte offsets, rtg_common.hpp rec_at).  The description is a real one with its face
+    list replaced by 2^25 + 1 zeroed faces (calloc'd: untouched pages cost nothing)."""
+    size, off_faces, off_num, face_size = _desc_layout(tmp_path)
+    assert face_size == 80
+    hs = rtgpu.HostScene(os.path.join(SCENES, "simple.xml"))
+    buf = (ctypes.c_char * size)()
+    ctypes.memmove(buf, hs.desc, size)
+    n = (1 << 25) + 1
+    faces = np.zeros(n * face_size, np.uint8)
+    ctypes.c_void_p.from_buffer(buf, off_faces).value = faces.ctypes.data
+    ctypes.c_int64.from_buffer(buf, off_num).value = n
+    s = ctypes.c_void_p()
+    rc = rtgpu.lib().rtg_scene_create(ctypes.addressof(buf), 0, ctypes.byref(s))
+    assert rc == -1 and not s.value, rc
+    assert b"2^25" in rtgpu.lib().rtg_last_error()
+    # at the limit the count is accepted (what follows needs a device)
+    ctypes.c_int64.from_buffer(buf, off_num).value = n - 1
+    if rtgpu.device_count() == 0:
+        rc = rtgpu.lib().rtg_scene_create(ctypes.addressof(buf), 0, ctypes.byref(s))
+        assert rc == -4, (rc, rtgpu.lib().rtg_last_error())

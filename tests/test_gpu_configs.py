@@ -187,3 +187,50 @@ def test_deferred_large_leaves(name, in_tmp, monkeypatch):
     print(name, "differing pixels", n, "(shadow deferral alone:", m, ")")
     assert n == 0 and m == 0 and np.array_equal(la, lb) and np.array_equal(la, ld)
     assert np.array_equal(a.view(np.uint32), c.view(np.uint32))
+
+
+@pytest.mark.parametrize("case,pad_objects,pad_faces,deferred", [
+    ("objects_under", 4093, 0, True),          # 4 095 objects, the blob is object 4 094
+    ("objects_over", 4095, 0, False),          # 4 097 objects, the blob is object 4 096 (13 bits)
+    ("faces_under", 0, 2 ** 20 - 19802 - 1000, True),
+    ("faces_over", 0, 2 ** 20, False),         # the blob's face records start past 2^20
+])
+def test_deferral_gate(case, pad_objects, pad_faces, deferred, in_tmp, monkeypatch):
+    """The deferred-leaf key packs (t, object, face) into 32 + 12 + 20 bits (rtg_common.hpp
+    obj_key), so the camera walk defers only scenes of fewer than 4 096 objects and 2^20 faces
+    (rtg_wave.hpp launch_wave_t).  Padding meshes before the large-leaf blob put its object index
+    and face records on either side of those limits: below them the deferring walk runs (pending
+    pixels counted with RTG_DEFER_DIAG=1), above them it must not (a key would alias), and either
+    way the image is bit for bit the cooperative walk's (RTG_DEFER=0) and the oracle's."""
+    xml = scenes.config_defer_gate(in_tmp, pad_objects=pad_objects, pad_faces=pad_faces)
+    hs, ds = _scene(xml)
+    n = hs.counts()
+    assert (n["objects"] > 4096) == (pad_objects > 4094) and (n["faces"] >= 2 ** 20) == (pad_faces >= 2 ** 20)
+    monkeypatch.setenv("RTG_DEFER_DIAG", "1")
+    ds.reset_stats()
+    a, la = ds.render(0, seed=4)
+    pending = ds.stats()["extend_wide_visits"]
+    monkeypatch.delenv("RTG_DEFER_DIAG")
+    print(case, n, "pending pixels", pending)
+    assert (pending > 0) == deferred, pending
+    monkeypatch.setenv("RTG_DEFER", "0")
+    b, lb = ds.render(0, seed=4)
+    assert np.array_equal(a.view(np.uint32), b.view(np.uint32)) and np.array_equal(la, lb)
+    ohdr, _, _ = ob.render(hs, seed=4)
+    r = ob.compare(a, ohdr, REL)
+    print(r)
+    assert r["n_fail"] == 0, r
+
+
+def test_defer_buffer_grows_with_the_part(in_tmp):
+    """The deferred-leaf buffer's layout (keys, entries, states) depends on the pixel count it
+    was sized for: after a counted full frame (large wave buffers) and a one-row render (a small
+    queue), a larger row range under the 1 024-entry floor must not reuse it (rtg_api.cpp
+    ensure_defer).  Each row range equals the same rows of a whole-frame render."""
+    xml = scenes.config_defer_gate(in_tmp, width=160, height=90)
+    hs, ds = _scene(xml)
+    full, _ = ds.render(0, seed=6)
+    ds.render(0, seed=6, flags=rtgpu.RTG_RENDER_COUNT_STATS)
+    for rows in ((40, 41), (40, 43), (38, 44)):       # 160, 480, 960 pixels
+        h, _ = ds.render(0, seed=6, rows=rows)
+        assert np.array_equal(h[rows[0]:rows[1]].view(np.uint32), full[rows[0]:rows[1]].view(np.uint32)), rows

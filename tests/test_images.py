@@ -86,6 +86,64 @@ def test_jpeg_and_tiled_exr_refused(tmp_path, name, data):
     assert e.value.code == -6, e.value
 
 
+def _exr(attrs, offsets, tail=b""):
+    """A scanline OpenEXR file from raw (name, type, value bytes, declared size) attributes."""
+    import struct
+    b = b"\x76\x2f\x31\x01" + b"\x02\x00\x00\x00"
+    for name, typ, val, sz in attrs:
+        b += name + b"\0" + typ + b"\0" + struct.pack("<I", len(val) if sz is None else sz) + val
+    b += b"\0"
+    start = len(b) + 8 * len(offsets)          # None: the chunk right after the offset table
+    b += b"".join(struct.pack("<Q", start if o is None else o) for o in offsets)
+    return b + tail
+
+
+def _chans():
+    import struct
+    return b"".join(c + b"\0" + struct.pack("<iBBBBii", 2, 0, 0, 0, 0, 1, 1) for c in (b"B", b"G", b"R")) + b"\0"
+
+
+def _malformed_exrs():
+    import struct
+    dw = struct.pack("<4i", 0, 0, 1, 0)           # 2 x 1 pixels
+    ch = (b"channels", b"chlist", _chans(), None)
+    good_chunk = struct.pack("<iI", 0, 24) + bytes(24)
+    return {
+        # a chunk offset near 2^64: off + 8 wraps to a small value
+        "huge_offset": _exr([ch, (b"compression", b"compression", b"\0", None),
+                             (b"dataWindow", b"box2i", dw, None), (b"lineOrder", b"lineOrder", b"\0", None)],
+                            [2 ** 64 - 4], good_chunk),
+        # a chunk length that runs past the file
+        "long_chunk": _exr([ch, (b"compression", b"compression", b"\0", None),
+                            (b"dataWindow", b"box2i", dw, None)], [None], struct.pack("<iI", 0, 2 ** 32 - 1)),
+        # attributes declared shorter than the values read from them
+        "short_datawindow": _exr([ch, (b"compression", b"compression", b"", 0), (b"dataWindow", b"box2i", b"", 4)],
+                                 [0], bytes(32)),
+        "short_compression": _exr([ch, (b"compression", b"compression", b"", 0)], [0], bytes(32)),
+        # a data window whose size overflows 32 bits
+        "huge_window": _exr([ch, (b"compression", b"compression", b"\0", None),
+                             (b"dataWindow", b"box2i", struct.pack("<4i", -2 ** 31, 0, 2 ** 31 - 1, 0), None)],
+                            [0], bytes(32)),
+    }
+
+
+@pytest.mark.parametrize("case", sorted(_malformed_exrs()))
+def test_malformed_exr_refused(tmp_path, case):
+    """Crafted EXR headers and offset tables are refused with an error, never read out of bounds
+    (host_assets.cpp load_exr: offsets checked by subtraction, attribute sizes checked)."""
+    os.makedirs(tmp_path / "inputs", exist_ok=True)
+    (tmp_path / "inputs" / "m.exr").write_bytes(_malformed_exrs()[case])
+    (tmp_path / "s.xml").write_text(SCENE.replace("IMG", "m.exr"))
+    old = os.getcwd()
+    os.chdir(tmp_path)
+    try:
+        with pytest.raises(rtgpu.RTGError) as e:
+            rtgpu.HostScene(str(tmp_path / "s.xml"))
+    finally:
+        os.chdir(old)
+    assert e.value.code == -2, e.value      # RTG_ERR_IO, as every unreadable image
+
+
 def test_png_fixture_semantics():
     """The goldens carry stb's conventions: 16-bit samples keep the high byte, sub-byte grey
     is scaled to 0..255, a palette with tRNS expands to RGBA."""

@@ -1,6 +1,6 @@
 """Deferred large leaves (k_bigleaf / k_hitfix) on a large-leaf configuration: pending pixels and
-the ones whose winner failed the leaf-box check (counters of a production render: k_hitfix
-counts them in extend_wide_visits / extend_fallbacks).
+the ones whose winner failed the leaf-box check (counters of a production render: with
+RTG_DEFER_DIAG=1, set here, k_hitfix counts them in extend_wide_visits / extend_fallbacks).
 
     python tools/diag_defer.py [c3|c3ton|c4]"""
 import json
@@ -8,6 +8,7 @@ import os
 import sys
 import tempfile
 
+os.environ["RTG_DEFER_DIAG"] = "1"
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "advanced-cpu-raytracing_amd"))
 import torch  # noqa: E402,F401
