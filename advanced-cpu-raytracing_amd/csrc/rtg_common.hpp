@@ -242,6 +242,36 @@ DEV bool box_hit_fast(float mnx, float mny, float mnz, float mxx, float mxy, flo
     return hit;
 }
 
+// box_hit_fast<true> for the camera packet walk with the lane's participation folded in, each
+// predicate one comparison.  act = rel > 0 (rel = i + 1 - resume: the lane's own walk reaches
+// this node).  When sure, the three decisions are clear of their boundaries, so each is the
+// sign of one exactly-signed quantity -- tmax, tmax - tmin (nonzero: |.| > slack) and minT - tmin
+// (a rounded difference has the sign of the exact one) -- and the conjunction is min(...) > 0;
+// `sure` is min(|tmax - tmin| - slack, |tmin - minT| - slack', |tmax| - 1e-30) > 0 (each a rounded
+// difference: exact sign; the last a hair stricter than >=), slack0 = inf when the ray's
+// reciprocals are not exact enough (q.fast).  NaN: only when all six slab distances are NaN,
+// and then nothing is sure.  Unsure lanes inside their walk take the exact test (uniform branch).
+DEV bool box_pass_pk(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, const Ray& r, const RayRcp& q,
+                     float minT, int rel, float slack0) {
+    const float tx1 = (mnx - r.o.x) * q.ix, tx2 = (mxx - r.o.x) * q.ix;
+    const float ty1 = (mny - r.o.y) * q.iy, ty2 = (mxy - r.o.y) * q.iy;
+    const float tz1 = (mnz - r.o.z) * q.iz, tz2 = (mxz - r.o.z) * q.iz;
+    const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+    const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+    const float atmin = fabsf(tmin), atmax = fabsf(tmax);
+    const float d1 = tmax - tmin, d2 = minT - tmin;
+    const float su = fminf(fminf(fabsf(d1) - fmaf(0x1p-20f, atmin + atmax, slack0),
+                                 fabsf(d2) - fmaf(0x1p-20f, atmin, slack0)), atmax - 1e-30f);
+    const float actf = (float)rel;                   // sign exact
+    float pv = fminf(fminf(fminf(tmax, d1), d2), actf);
+    const bool unsure = !(fmaxf(su, 0.5f - actf) > 0.0f);
+    if (__builtin_expect(__ballot(unsure) != 0, 0)) {
+        if (unsure) pv = box_hit(mnx, mny, mnz, mxx, mxy, mxz, r, minT) ? 1.0f : -1.0f;
+    }
+    // (compared after the merge: the caller's ballot of it is then that comparison's mask)
+    return pv > 0.0f;
+}
+
 // determinant (helperMath.cpp:132-138)
 DEV float det3(float m00, float m01, float m02, float m10, float m11, float m12, float m20, float m21, float m22) {
     float first = m00 * (m11 * m22 - m12 * m21);
@@ -708,6 +738,9 @@ DEV const T* rec_at(const T* base, int i) {
 #ifndef RTG_DEFER_LANES
 #define RTG_DEFER_LANES 16
 #endif
+#ifndef RTG_PK_LEAN
+#define RTG_PK_LEAN 1
+#endif
 struct DeferCtx {
     float4* e;
     int* count;
@@ -723,10 +756,21 @@ DEV uint64_t obj_key(float t, int k, int f) {
 }
 
 template <bool ANY, bool STATS, bool SC = false, bool DEFER = false>
-DEV bool walk_bvh_packet(const DevScene& S, const int begin, const int end, const Ray& r, float& minT, int& hitFace,
+DEV bool walk_bvh_packet(const DevScene& S, int begin, int end, const Ray& r, float& minT, int& hitFace,
                          float limit, Cnt<STATS>& c, DeferCtx* dc = nullptr, int k = 0) {
+#if RTG_PK_LEAN
+    // the node range is the object's (wave-uniform): SGPRs, so the loop index and its bound stay
+    // scalar; "a face was accepted" is read off hitFace at the end instead of a lane mask kept
+    // through every iteration
+    begin = __builtin_amdgcn_readfirstlane(begin);
+    end = __builtin_amdgcn_readfirstlane(end);
+    const int face0 = hitFace;
+#endif
     bool hit = false;
     const RayRcp q = ray_rcp(r);
+#if RTG_PK_LEAN
+    const float slack0 = q.fast ? 1e-30f : INFINITY;   // box_pass_pk: a ray off the fast path is never sure
+#endif
     const int kDone = 0x7FFFFFFF;
     int resume = begin;                              // per lane: first node it takes part in again
     int i = begin;                                   // wave-uniform
@@ -763,8 +807,15 @@ DEV bool walk_bvh_packet(const DevScene& S, const int begin, const int end, cons
         bool pass;
         if constexpr (SC) {
             if (act) c.template node<ANY>();
+#if RTG_PK_LEAN
+            pass = box_pass_pk(a.x, a.y, a.z, a.w, b.x, b.y, r, q, minT, i + 1 - resume, slack0);
+            // a lane inside its walk that fails the box resumes at the box's skip; lanes outside it
+            // already wait for a node past this box's subtree (resume >= skip), as do lanes that pass
+            resume = max(resume, pass ? 0 : skip);
+#else
             pass = act & box_hit_fast<true>(a.x, a.y, a.z, a.w, b.x, b.y, r, q, minT, act);
             resume = (act & !pass) ? skip : resume;
+#endif
         } else {
             pass = false;
             if (act) {
@@ -773,12 +824,39 @@ DEV bool walk_bvh_packet(const DevScene& S, const int begin, const int end, cons
                 if (!pass) resume = skip;
             }
         }
+#if !RTG_PK_LEAN
         const bool any = __ballot(pass) != 0;
+#endif
+#if RTG_PK_LEAN
+        // the next node and the leaf to test in five scalar instructions (the compiler kept the
+        // two wave-uniform conditions as 64-bit masks with selects and branches between them):
+        // lf = the leaf word when some lane passed, else 0 (no faces); next = lf < 0 (a passed
+        // inner box) ? its first child : its skip
+        const int cur = i;
+        int lf;
+        {
+            const uint64_t pm = __builtin_amdgcn_ballot_w64(pass);
+            int nx;
+            asm("s_cmp_lg_u64 %[pm], 0\n\t"
+                "s_cselect_b32 %[lf], %[leaf], 0\n\t"
+                "s_add_i32 %[nx], %[i], 1\n\t"
+                "s_cmp_lt_i32 %[lf], 0\n\t"
+                "s_cselect_b32 %[nx], %[nx], %[skip]"
+                : [lf] "=&s"(lf), [nx] "=&s"(nx)
+                : [pm] "s"(pm), [leaf] "s"(leaf), [i] "s"(i), [skip] "s"(skip)
+                : "scc");
+            i = nx;
+        }
+        if (lf > 0) {
+            {
+#else
+        const int cur = i;
         if (leaf >= 0) {
             if (any) {
+#endif
                 int first = leaf >> 8, cnt = leaf & 255;
                 if (leaf == LEAF_EXT) {
-                    const int2 e = S.node_ext[i];
+                    const int2 e = S.node_ext[cur];
                     first = __builtin_amdgcn_readfirstlane(e.x);
                     cnt = __builtin_amdgcn_readfirstlane(e.y);
                 }
@@ -816,7 +894,9 @@ DEV bool walk_bvh_packet(const DevScene& S, const int begin, const int end, cons
                         const bool ok = pass & tri_test_sel(R, r, minT, t, pass);
                         minT = ok ? t : minT;
                         hitFace = ok ? f : hitFace;
+#if !RTG_PK_LEAN
                         hit |= ok;
+#endif
                         if (ANY) {
                             const bool fin = ok & (t < limit);
                             pass &= !fin;
@@ -837,11 +917,16 @@ DEV bool walk_bvh_packet(const DevScene& S, const int begin, const int end, cons
                     }
                 }
             }
+#if !RTG_PK_LEAN
             i = skip;
         } else {
             i = any ? i + 1 : skip;
+#endif
         }
     }
+#if RTG_PK_LEAN
+    if constexpr (SC) return hit | (hitFace != face0);
+#endif
     return hit;
 }
 

@@ -23,6 +23,21 @@
 
 namespace rtg {
 
+// k_shade register-pressure variants (A/B): RTG_SHADE_REFS the hit point / normal by reference
+// and the RNG key recomputed where used (no scratch in the headline's fused kernel),
+// RTG_FUSED_SWITCH one light by branch instead of the light loops (no VGPR spills either, but
+// SGPR spills into the shadow walk: measured slower), RTG_FUSED_STASH the pixel's colour terms
+// in LDS across the shadow walk
+#ifndef RTG_FUSED_STASH
+#define RTG_FUSED_STASH 0
+#endif
+#ifndef RTG_FUSED_SWITCH
+#define RTG_FUSED_SWITCH 0
+#endif
+#ifndef RTG_SHADE_REFS
+#define RTG_SHADE_REFS 1
+#endif
+
 enum { BASE_FINAL = 1, BASE_ADD_ZERO = 2 };
 
 // ORD: RTG_RENDER_ORDERED (plain mesh scenes): the checked closest-hit walk -- on the any-hit
@@ -294,7 +309,13 @@ DEV void finish_pixel(const DevCamera& C, const RenderParams& P, int sample, con
         if (O.ldr) { O.ldr[idx] = ldr(color.x); O.ldr[idx + 1] = ldr(color.y); O.ldr[idx + 2] = ldr(color.z); }
         return;
     }
+#if RTG_SHADE_REFS
+    int pk = pixel;                  // (recomputed, not merged with the caller's key: see area_light)
+    asm volatile("" : "+v"(pk));
+    const float gw = sample_weight(C.spp, sample, root_key(P.seed, pk, sample));
+#else
     const float gw = sample_weight(C.spp, sample, root_key(P.seed, pixel, sample));
+#endif
     float4 a = O.first ? make_float4(0.f, 0.f, 0.f, 0.f) : O.accum[pixel];
     a.x += color.x * gw;
     a.y += color.y * gw;
@@ -422,7 +443,14 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
     }
     // ---- lights, in SampleDirectLighting's order (raytracer.cpp:706-803)
     int slot = i * W.num_slots;
+#if RTG_SHADE_REFS
+    // the hit point and normal by reference: a lane that is not lit never reads them (every use
+    // is behind `lit` / push's `want`), and selected copies kept a second set of six VGPRs live
+    // next to the surface record through the light loops
+    const f3 &p = c.s.p, &n = c.s.n;
+#else
     const f3 p = lit ? c.s.p : mk(0, 0, 0), n = lit ? c.s.n : mk(0, 0, 1);
+#endif
     if constexpr (MODE == SH_FUSED_N) {
         // SK 0: point, area and directional lights only, in that order; one shadow-walk call site
         f3 sum = mk(0, 0, 0);
@@ -516,7 +544,7 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
         if (ONE) { term1 = t; has_term = true; }
         else W.term[slot] = make_float4(t.x, t.y, t.z, 0.f);
     };
-    for (int l = 0; l < S.num_point; ++l, ++slot) {
+    auto point_light = [&](int l) {
         const f3 lp = ld3(S.point_lights[l].pos);
         if (lit) {
             f3 w_i = makeUnit(sub(lp, p));
@@ -524,13 +552,23 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
             put(shade<false, SK>(S, c, w_i, w_o, divs(ld3(S.point_lights[l].intensity), dist * dist)));
         }
         push(lit, lp, false);
-    }
-    for (int l = 0; l < S.num_area; ++l, ++slot) {
+    };
+    auto area_light = [&](int l) {
         f3 sp = mk(0, 0, 0);
         if (lit) {
             const DevAreaLight& L = S.area_lights[l];
-            float offU = rnd(key, RP_AREA, 2 * l) - 0.5f;
-            float offV = rnd(key, RP_AREA, 2 * l + 1) - 0.5f;
+#if RTG_SHADE_REFS
+            // the pixel's RNG key again (a few integer ops) rather than two VGPRs kept through the
+            // point lights' shading; the laundered pixel index stops the compiler from merging it
+            // with the first computation
+            int pk = pixel;
+            asm volatile("" : "+v"(pk));
+            const uint64_t akey = root_key(P.seed, pk, sample);
+#else
+            const uint64_t akey = key;
+#endif
+            float offU = rnd(akey, RP_AREA, 2 * l) - 0.5f;
+            float offV = rnd(akey, RP_AREA, 2 * l + 1) - 0.5f;
             sp = add(add(ld3(L.pos), muls(ld3(L.u), L.extent * offU)), muls(ld3(L.v), L.extent * offV));
             f3 w_i = sub(sp, p);
             float dist = len(w_i);
@@ -541,7 +579,23 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
             put(shade<false, SK>(S, c, w_i, w_o, muls(ld3(L.radiance), L.area * lc / dSqr)));
         }
         push(lit, sp, false);
-    }
+    };
+    auto dir_light = [&](int l) {
+        const f3 ldir = ld3(S.dir_lights[l].dir);
+        if (lit) put(shade<false, SK>(S, c, neg(ldir), w_o, ld3(S.dir_lights[l].radiance)));
+        push(lit, ldir, true);
+    };
+    if constexpr (MODE == SH_FUSED && RTG_FUSED_SWITCH) {
+        // the fused layout's scenes have exactly one light, a point, area or directional one:
+        // one branch instead of three loops, so nothing of one light kind stays live across
+        // another's code (the loops kept the RNG key and the hit point live through the point
+        // light's shading and spilled them to scratch at seven waves per SIMD)
+        if (S.num_point) point_light(0);
+        else if (S.num_area) area_light(0);
+        else dir_light(0);
+    } else {
+    for (int l = 0; l < S.num_point; ++l, ++slot) point_light(l);
+    for (int l = 0; l < S.num_area; ++l, ++slot) area_light(l);
     if constexpr ((SK & SK_XLIGHT) != 0) {
         for (int l = 0; l < S.num_env; ++l, ++slot) {
             if (lit) {                                               // no shadow ray (:741-755)
@@ -551,11 +605,7 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
             }
         }
     }
-    for (int l = 0; l < S.num_dir; ++l, ++slot) {
-        const f3 ldir = ld3(S.dir_lights[l].dir);
-        if (lit) put(shade<false, SK>(S, c, neg(ldir), w_o, ld3(S.dir_lights[l].radiance)));
-        push(lit, ldir, true);
-    }
+    for (int l = 0; l < S.num_dir; ++l, ++slot) dir_light(l);
     if constexpr ((SK & SK_XLIGHT) != 0) {
         for (int l = 0; l < S.num_spot; ++l, ++slot) {
             const DevSpotLight& L = S.spot_lights[l];
@@ -595,10 +645,26 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
             push(lit, sp, false);
         }
     }
+    }
     if constexpr (MODE == SH_FUSED) {
         if (pushed) {
+#if RTG_FUSED_STASH
+            // the pixel's base colour, flags, light term and index wait in LDS while the shadow
+            // walk runs: eight VGPRs fewer across the walk, which at seven waves per SIMD (72
+            // VGPRs) had spilled to scratch
+            __shared__ float4 stash[2][256];
+            stash[0][threadIdx.x] = make_float4(base.x, base.y, base.z, __int_as_float(bflags));
+            stash[1][threadIdx.x] = make_float4(term1.x, term1.y, term1.z, __int_as_float(pixel));
+            asm volatile("" ::: "memory");
+            const bool occluded = shadow_occluded<STATS, FEAT, FAST>(S, W, 0, ro, rd, cn);
+            asm volatile("" ::: "memory");
+            const float4 sb = stash[0][threadIdx.x], st = stash[1][threadIdx.x];
+            finish_pixel(C, P, sample, O, __float_as_int(st.w),
+                         resolve_one(mk(sb.x, sb.y, sb.z), __float_as_int(sb.w), true, mk(st.x, st.y, st.z), occluded));
+#else
             const bool occluded = shadow_occluded<STATS, FEAT, FAST>(S, W, 0, ro, rd, cn);
             finish_pixel(C, P, sample, O, pixel, resolve_one(base, bflags, true, term1, occluded));
+#endif
         } else if (valid) {
             finish_pixel(C, P, sample, O, pixel, resolve_one(base, bflags, has_term, term1, false));
         }
