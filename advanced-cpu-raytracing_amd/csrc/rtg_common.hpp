@@ -242,6 +242,12 @@ DEV bool box_hit_fast(float mnx, float mny, float mnz, float mxx, float mxy, flo
     return hit;
 }
 
+// NaN-propagating minimum of three (IEEE 754-2019 minimum; v_minimum3_f32 on gfx950):
+// vmin3(a, b, c) > 0 is exactly (a > 0) & (b > 0) & (c > 0), NaN included
+DEV float vmin3(float a, float b, float c) {
+    return __builtin_elementwise_minimum(__builtin_elementwise_minimum(a, b), c);
+}
+
 // box_hit_fast<true> for the camera packet walk with the lane's participation folded in, each
 // predicate one comparison.  act = rel > 0 (rel = i + 1 - resume: the lane's own walk reaches
 // this node).  When sure, the three decisions are clear of their boundaries, so each is the
@@ -249,10 +255,14 @@ DEV bool box_hit_fast(float mnx, float mny, float mnz, float mxx, float mxy, flo
 // (a rounded difference has the sign of the exact one) -- and the conjunction is min(...) > 0;
 // `sure` is min(|tmax - tmin| - slack, |tmin - minT| - slack', |tmax| - 1e-30) > 0 (each a rounded
 // difference: exact sign; the last a hair stricter than >=), slack0 = inf when the ray's
-// reciprocals are not exact enough (q.fast).  NaN: only when all six slab distances are NaN,
-// and then nothing is sure.  Unsure lanes inside their walk take the exact test (uniform branch).
-DEV bool box_pass_pk(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, const Ray& r, const RayRcp& q,
-                     float minT, int rel, float slack0) {
+// reciprocals are not exact enough (q.fast).  A NaN term leaves the lane unsure; a sure lane has
+// no NaN among tmax, d1, d2.  Unsure lanes inside their walk take the exact test (uniform branch).
+// Returns a value whose sign is the answer (> 0: the lane takes part and the box passes), so a
+// caller's ballot of `> 0` is one comparison; actf > 0: the lane takes part.
+// INT: actf is an integer (rel), so `act & !sure` is one comparison, !(max(su, 0.5 - actf) > 0)
+template <bool INT = false>
+DEV float box_pass_v(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, const Ray& r, const RayRcp& q,
+                     float minT, float actf, float slack0) {
     const float tx1 = (mnx - r.o.x) * q.ix, tx2 = (mxx - r.o.x) * q.ix;
     const float ty1 = (mny - r.o.y) * q.iy, ty2 = (mxy - r.o.y) * q.iy;
     const float tz1 = (mnz - r.o.z) * q.iz, tz2 = (mxz - r.o.z) * q.iz;
@@ -260,16 +270,22 @@ DEV bool box_pass_pk(float mnx, float mny, float mnz, float mxx, float mxy, floa
     const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
     const float atmin = fabsf(tmin), atmax = fabsf(tmax);
     const float d1 = tmax - tmin, d2 = minT - tmin;
-    const float su = fminf(fminf(fabsf(d1) - fmaf(0x1p-20f, atmin + atmax, slack0),
-                                 fabsf(d2) - fmaf(0x1p-20f, atmin, slack0)), atmax - 1e-30f);
-    const float actf = (float)rel;                   // sign exact
-    float pv = fminf(fminf(fminf(tmax, d1), d2), actf);
-    const bool unsure = !(fmaxf(su, 0.5f - actf) > 0.0f);
+    // (NaN-propagating minimum, v_minimum3_f32: any NaN term -- an infinite box face, inf - inf
+    // -- leaves the lane unsure)
+    const float su = vmin3(fabsf(d1) - fmaf(0x1p-20f, atmin + atmax, slack0), fabsf(d2) - fmaf(0x1p-20f, atmin, slack0),
+                           atmax - 1e-30f);
+    float pv = __builtin_elementwise_minimum(fminf(fminf(tmax, d1), d2), actf);   // (a NaN actf: not taking part)
+    const bool unsure = INT ? !(fmaxf(su, 0.5f - actf) > 0.0f) : (actf > 0.0f) & !(su > 0.0f);
     if (__builtin_expect(__ballot(unsure) != 0, 0)) {
         if (unsure) pv = box_hit(mnx, mny, mnz, mxx, mxy, mxz, r, minT) ? 1.0f : -1.0f;
     }
+    return pv;
+}
+DEV bool box_pass_pk(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, const Ray& r, const RayRcp& q,
+                     float minT, int rel, float slack0) {
+    // rel = i + 1 - resume > 0: the lane's walk reaches the node (as a float: sign exact)
     // (compared after the merge: the caller's ballot of it is then that comparison's mask)
-    return pv > 0.0f;
+    return box_pass_v<true>(mnx, mny, mnz, mxx, mxy, mxz, r, q, minT, (float)rel, slack0) > 0.0f;
 }
 
 // determinant (helperMath.cpp:132-138)
@@ -419,6 +435,44 @@ DEV bool tri_test_sel(const float4* R, const Ray& r, float limit, float& tout, b
         if (unsure) hit = tri_test_rec(R, r, limit, tout);
     }
     return hit;
+}
+
+// tri_test_sel with every decision a single comparison of a value (the packet walks' face
+// tests; lanes with onf > 0 take part).  Returns a value > 0 exactly when IntersectFace
+// accepts the face with 0 < t < limit (t in tout).  Sure candidates: |detA| in range (strict),
+// beta and gama above 1e-30 and 1 - sum above the bound of tri_test_fast_rec (each a rounded
+// difference, so its sign is the comparison's); sure rejections: detA == 0, or in range and
+// beta or gama below -1e-30 or sum - 1 above the bound (any one decides, in whatever order the
+// reference tests them: each makes IntersectFace return false).  Everything else -- also the
+// exact zeros nb == 0 / ng == 0 that tri_test_fast_rec takes as sure -- takes the exact test
+// (uniform branch).  AND is the NaN-propagating minimum, OR the NaN-dropping max.
+DEV float tri_test_pk(const float4* R, const Ray& r, float limit, float& tout, float onf) {
+    const float4 A = R[0], E1 = R[1], E2 = R[2];
+    const float dx = r.d.x, dy = r.d.y, dz = r.d.z;
+    const float detA = det3(E1.x, E2.x, dx, E1.y, E2.y, dy, E1.z, E2.z, dz);
+    const float ad = fabsf(detA);
+    const float rd = __builtin_amdgcn_rcpf(detA);
+    const float sx = A.x - r.o.x, sy = A.y - r.o.y, sz = A.z - r.o.z;
+    const float nb = det3(sx, E2.x, dx, sy, E2.y, dy, sz, E2.z, dz);
+    const float ng = det3(E1.x, sx, dx, E1.y, sy, dy, E1.z, sz, dz);
+    const float beta = nb * rd, gama = ng * rd, sum = gama + beta;
+    const float sslack = fmaf(0x1p-19f, sum, 0x1p-22f);
+    const float rng = __builtin_elementwise_minimum(ad - 0x1p-100f, 0x1p100f - ad);
+    const float ttv = __builtin_elementwise_minimum(vmin3(beta - 1e-30f, gama - 1e-30f, (1.0f - sum) - sslack),
+                                                    __builtin_elementwise_minimum(rng, onf));
+    const float rjv = __builtin_elementwise_minimum(fmaxf(fmaxf(-1e-30f - beta, -1e-30f - gama), (sum - 1.0f) - sslack),
+                                                    rng);
+    float hv = -1.0f;
+    if (__ballot(ttv > 0.0f)) {
+        const float t = det3(E1.x, E2.x, sx, E1.y, E2.y, sy, E1.z, E2.z, sz) / detA;
+        tout = t;
+        hv = vmin3(ttv, t, limit - t);               // 0 < t < limit (rounded difference: exact sign)
+    }
+    const bool unsure = (onf > 0.0f) & !(ttv > 0.0f) & !(rjv > 0.0f) & (detA != 0.0f);
+    if (__builtin_expect(__ballot(unsure) != 0, 0)) {
+        if (unsure) hv = tri_test_rec(R, r, limit, tout) ? 1.0f : -1.0f;
+    }
+    return hv;
 }
 
 // Wave-uniform records through the scalar cache (the compiler keeps vector loads here: the
@@ -741,6 +795,13 @@ DEV const T* rec_at(const T* base, int i) {
 #ifndef RTG_PK_LEAN
 #define RTG_PK_LEAN 1
 #endif
+// (A/B parts of the lean packet walks: the any-hit walk, the closest-hit walk's face test)
+#ifndef RTG_PK_LEAN_ANY
+#define RTG_PK_LEAN_ANY RTG_PK_LEAN
+#endif
+#ifndef RTG_PK_LEAN_TRI
+#define RTG_PK_LEAN_TRI RTG_PK_LEAN
+#endif
 struct DeferCtx {
     float4* e;
     int* count;
@@ -891,7 +952,11 @@ DEV bool walk_bvh_packet(const DevScene& S, int begin, int end, const Ray& r, fl
                                              f4(rb[0], rb[1], rb[2], rb[3])};
                         if (pass) c.template tri<ANY>();
                         float t;
+#if RTG_PK_LEAN_TRI
+                        const bool ok = tri_test_pk(R, r, minT, t, pass ? 1.0f : -1.0f) > 0.0f;
+#else
                         const bool ok = pass & tri_test_sel(R, r, minT, t, pass);
+#endif
                         minT = ok ? t : minT;
                         hitFace = ok ? f : hitFace;
 #if !RTG_PK_LEAN
@@ -1229,9 +1294,142 @@ DEV int walk_wide_any(const DevScene& S, int node, const Ray& lr, float minT0, f
 #ifndef RTG_PK_MAX_STEPS
 #define RTG_PK_MAX_STEPS 4096
 #endif
+#if RTG_PK_LEAN_ANY
+// slab_cons as a value (> 0: the conservative test passes and the lane walks, livef > 0): tmax >
+// -1e-30 is tmax + 1e-30 > 0 and tmin < minTc is minTc - tmin > 0 (exact: rounded sums and
+// differences keep their signs); tmax >= tmin (1 - 2^-21) - 1e-30 is loosened by another 1e-30
+// so that it becomes a strict comparison too -- the test only has to keep every box the exact
+// test keeps (walk_wide_any_pk: extra boxes change no answer).
+DEV float slab_cons_v(float lx, float ly, float lz, float hx, float hy, float hz, const SlabRay& s, float minTc,
+                      float& tnear, float livef) {
+    const float tx1 = (lx - s.o.x) * s.ix, tx2 = (hx - s.o.x) * s.ix;
+    const float ty1 = (ly - s.o.y) * s.iy, ty2 = (hy - s.o.y) * s.iy;
+    const float tz1 = (lz - s.o.z) * s.iz, tz2 = (hz - s.o.z) * s.iz;
+    const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+    const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+    tnear = tmin;
+    return __builtin_elementwise_minimum(
+        vmin3(tmax + 1e-30f, (tmax - fmaf(tmin, 1.0f - 0x1p-21f, -1e-30f)) + 1e-30f, minTc - tmin), livef);
+}
+#endif
+
 template <bool STATS, bool DEFER = false>
 DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0, float limit, bool inst_conf,
                          Cnt<STATS>& c, AnyDefer* ad = nullptr) {
+#if RTG_PK_LEAN_ANY
+    // The lane state as values, every wave-level test one comparison (the mask version kept
+    // live / occluded / undecided and the four child masks as SGPR pairs merged at every block
+    // and spilled to VGPR lanes): livef > 0 walking, occ / und flags, a child's hk > 0 taking it.
+    const RayRcp q = ray_rcp(lr);
+    const float minTc = minT0 * (1.0f + 0x1p-21f);
+    const SlabRay sr = slab_ray(lr, q);
+    const float slack0 = q.fast ? 1e-30f : INFINITY;
+    const float icf = inst_conf ? 1.0f : -1.0f;
+    float livef = q.fast ? 1.0f : -1.0f;
+    int occ = 0;
+    int und = q.fast ? 0 : 1;                        // zero / tiny direction component: reference walk
+    __shared__ int pk_stack[4][RTG_PK_STACK];        // the wave's stack (256-thread blocks)
+    int* const stk = pk_stack[(threadIdx.x >> 6) & 3];
+    int sp = 0;                                      // wave-uniform
+    node = __builtin_amdgcn_readfirstlane(node);
+    int steps = 0;                                   // bound: a walk visits each node once
+    while (__ballot(livef > 0.0f)) {
+        if (++steps > RTG_PK_MAX_STEPS) {
+            und |= livef > 0.0f;
+            break;
+        }
+        node = __builtin_amdgcn_readfirstlane(node);
+        rtg_s16 na, nb;
+        sload_wnode(rec_at<128>(S.anodes, node), na, nb);
+        if (livef > 0.0f) c.wnode();
+        float tn[4], hv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+            hv[k] = slab_cons_v(__int_as_float(na[k]), __int_as_float(na[8 + k]), __int_as_float(nb[k]),
+                                __int_as_float(na[4 + k]), __int_as_float(na[12 + k]), __int_as_float(nb[4 + k]), sr,
+                                minTc, tn[k], livef);
+        const int lead = __ffsll((long long)__ballot(livef > 0.0f)) - 1;
+        int next = -1;
+        float nextT = INFINITY;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int cr = nb[8 + k], lfw = nb[12 + k];
+            float hk = hv[k];
+            if (cr == WCHILD_EMPTY || !__ballot(hk > 0.0f)) continue;
+            if (cr >= 0) {
+                const float t = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tn[k]), lead));
+                int spill = cr;
+                if (t < nextT) {
+                    spill = next;
+                    next = cr;
+                    nextT = t;
+                }
+                if (spill >= 0) {
+                    if (sp < RTG_PK_STACK) {             // written by the first live lane
+                        if ((int)(threadIdx.x & 63) == lead) stk[sp] = spill;
+                        ++sp;
+                    } else {
+                        und |= livef > 0.0f;
+                    }
+                }
+                continue;
+            }
+            const int first = lfw >> 8, cnt = lfw & 255;
+            if constexpr (DEFER) {
+                const uint64_t m = __ballot(hk > 0.0f);
+                if (cnt > RTG_DEFER_ANY_LEAF && __popcll(m) <= RTG_DEFER_ANY_LANES) {
+                    const int lane = threadIdx.x & 63, ld = __ffsll((long long)m) - 1;
+                    int base = 0;
+                    if (lane == ld) base = atomicAdd(ad->count, __popcll(m));
+                    base = __shfl(base, ld);
+                    const int slot = base + __popcll(m & ((1ull << lane) - 1ull));
+                    if (hk > 0.0f && slot < ad->cap) {
+                        float4* qe = ad->e + 3 * (size_t)slot;
+                        qe[0] = make_float4(lr.o.x, lr.o.y, lr.o.z, minT0);
+                        qe[1] = make_float4(lr.d.x, lr.d.y, lr.d.z, limit);
+                        qe[2] = make_float4(__int_as_float(first), __int_as_float(cnt), __int_as_float(ad->q),
+                                            __int_as_float((int)inst_conf));
+                        ad->deferred = true;
+                        hk = -1.0f;
+                    }
+                }
+            }
+            for (int e = first; e < first + cnt; ++e) {
+                rtg_s8 ra;
+                rtg_s4 rb;
+                sload_rec(rec_at<48>(S.ahtris, e), ra, rb);
+                if (hk > 0.0f) c.template tri<true>();
+                const float4 R[3] = {f4(ra[0], ra[1], ra[2], ra[3]), f4(ra[4], ra[5], ra[6], ra[7]), f4(rb[0], rb[1], rb[2], rb[3])};
+                float t;
+                const float okv = tri_test_pk(R, lr, limit, t, hk);
+                if (!__ballot(okv > 0.0f)) continue;
+                // the exact decisions on the face's reference leaf box: reachable at minT0
+                // (necessary), and at limit (sufficient, for an instance whose world box passes)
+                rtg_s8 rn;
+                sload_node(rec_at<32>(S.nodes, ra[3]), rn);
+                const float rv = box_pass_v(__int_as_float(rn[0]), __int_as_float(rn[1]), __int_as_float(rn[2]),
+                                            __int_as_float(rn[3]), __int_as_float(rn[4]), __int_as_float(rn[5]), lr, q,
+                                            minT0, okv, slack0);
+                const float sv = box_pass_v(__int_as_float(rn[0]), __int_as_float(rn[1]), __int_as_float(rn[2]),
+                                            __int_as_float(rn[3]), __int_as_float(rn[4]), __int_as_float(rn[5]), lr, q,
+                                            limit, __builtin_elementwise_minimum(rv, icf), slack0);
+                const bool suff = sv > 0.0f;
+                occ = suff ? 1 : occ;
+                livef = suff ? -1.0f : livef;
+                hk = suff ? -1.0f : hk;
+                und |= (rv > 0.0f) & !suff;
+            }
+        }
+        if (!__ballot(livef > 0.0f)) break;
+        if (next >= 0) {
+            node = next;
+            continue;
+        }
+        if (sp == 0) break;
+        node = stk[--sp];
+    }
+    return occ ? 1 : (und ? -1 : 0);
+#else
     const RayRcp q = ray_rcp(lr);
     const float minTc = minT0 * (1.0f + 0x1p-21f);
     const SlabRay sr = slab_ray(lr, q);
@@ -1363,6 +1561,7 @@ DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0
         node = stk[--sp];
     }
     return occ ? 1 : (undecided ? -1 : 0);
+#endif
 }
 
 // CastShadowRay on the wide BVH: objects in any order (the answer is a boolean), spheres
