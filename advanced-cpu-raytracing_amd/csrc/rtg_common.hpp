@@ -2846,6 +2846,36 @@ DEV int part_pixel(const RenderParams& P, int width, int i) {
     return part_row(P, crow) * width + (i - crow * width);
 }
 
+// The ray trees' level-0 order (rtg_tree.hip): compact index i -> image pixel in 8x8 tiles
+// (8-row bands of the part, each band's 8-column chunks in order; a band of fewer rows or a
+// last chunk of fewer columns keeps its pixels in row-major order), so a wave's 64 camera rays
+// -- and, through the per-block ordered child appends, their reflected and refracted rays --
+// come from one 8x8 block of the image instead of a 64-pixel strip of a row.  A bijection of
+// [0, width * part_rows) onto the part's pixels.  RTG_TREE_TILES=0: row-major (part_pixel).
+#ifndef RTG_TREE_TILES
+#define RTG_TREE_TILES 1
+#endif
+DEV int tree_pixel(const RenderParams& P, int width, int i) {
+#if RTG_TREE_TILES
+    const int band = i / (8 * width), j = i - band * 8 * width;
+    const int rb = min(8, P.part_rows - 8 * band);        // rows of this band
+    const int fc = width >> 3, full = fc * 8 * rb;         // pixels in whole 8-column chunks
+    int x, y;
+    if (j < full) {
+        const int c = j / (8 * rb), k = j - c * 8 * rb;
+        x = 8 * c + (k & 7);
+        y = k >> 3;
+    } else {
+        const int rw = width & 7, k = j - full;
+        x = 8 * fc + k % rw;
+        y = k / rw;
+    }
+    return part_row(P, 8 * band + y) * width + x;
+#else
+    return part_pixel(P, width, i);
+#endif
+}
+
 // tile_pixel also returns the compact row (index of the pixel's work-buffer entries:
 // crow * width + px).
 DEV void tile_pixel(const RenderParams& P, int& px, int& py, int& crow) {
@@ -2964,6 +2994,34 @@ __global__ __launch_bounds__(256, FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(
         } else if (shadow_occluded<STATS, FEAT, FAST>(S, W, q, W.q_o[q], W.q_d[q], cn)) {
             W.occ[W.q_slot[q]] = 1;
         }
+    }
+    flush_counters<STATS>(cn, counters);
+}
+
+// The ray trees' shadow rays on the any-hit tree walked per lane (walk_wide_any: LDS stack per
+// lane; incoherent rays -- the levels below the camera's -- make the wave packet's union of
+// walks large), the reference walk for an undecided ray.  Exact as k_shadow's fast walk.
+#ifndef RTG_LANE_ANY_WAVES
+#define RTG_LANE_ANY_WAVES 5
+#endif
+template <bool STATS, int FEAT>
+__global__ __launch_bounds__(256, RTG_LANE_ANY_WAVES) void k_shadow_lane(const DevScene S, const WaveBufs W,
+                                                                         DevCounters* counters) {
+    const int k = blockIdx.y * 256 + threadIdx.x;
+    const size_t q = ((size_t)blockIdx.x * W.num_slots) * 256 + k;
+    Cnt<STATS> cn;
+    if (k < W.q_count[blockIdx.x]) {
+        const float4 o = W.q_o[q], d = W.q_d[q];
+        Ray r;
+        r.o = mk(o.x, o.y, o.z);
+        r.d = mk(d.x, d.y, d.z);
+        int res = trace_any_wide<STATS, FEAT, false, false>(S, r, o.w, d.w, cn);
+        if (res < 0) {                               // undecided: the reference walk
+            cn.fallback();
+            Hit h;
+            res = trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
+        }
+        if (res > 0) W.occ[W.q_slot[q]] = 1;
     }
     flush_counters<STATS>(cn, counters);
 }

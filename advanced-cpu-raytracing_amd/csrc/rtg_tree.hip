@@ -23,6 +23,7 @@
 // (rtg_mega.hip / the reference), so the result is bit-identical to the fused kernel.
 #include <algorithm>
 #include <cstdlib>
+#include <cstring>
 #include <vector>
 
 #include "rtg_common.hpp"
@@ -42,7 +43,7 @@ __global__ __launch_bounds__(256) void k_tree_gen(const DevCamera C, const Rende
                                                   const TreeLevel L0) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= L0.n) return;
-    const int pixel = part_pixel(P, C.width, i);
+    const int pixel = tree_pixel(P, C.width, i);
     const int px = pixel % C.width, py = pixel / C.width;
     const uint64_t key = root_key(P.seed, pixel, sample);
     float mbTime;
@@ -134,7 +135,7 @@ __global__ __launch_bounds__(256, SK == SK_ALL ? RTG_TREE_SHADE_WAVES : RTG_TREE
         if (obj < 0) {
             f3 v;
             if (level == 0) {
-                const int pixel = part_pixel(P, C.width, i);
+                const int pixel = tree_pixel(P, C.width, i);
                 v = miss_color<SK>(S, C, pixel % C.width, pixel / C.width, r.d);
             } else {
                 const float4 m = L.miss[i];
@@ -356,14 +357,18 @@ __global__ __launch_bounds__(1024) void k_tree_scan(const int* __restrict__ cnt,
     }
 }
 
+// SORT (RTG_TREE_SORT, A/B): the block's children grouped by the octant of their direction
+// (stable: octant, then the order they were appended in), so that a wave of the next level holds
+// rays from one small image area going the same general way.  Positions within a level change
+// nothing but the walks' coherence: every ray's value depends only on its own record and key,
+// and the parents' links follow the rays.
+template <bool SORT>
 __global__ __launch_bounds__(256) void k_tree_compact(const TreeSegs G, const int* __restrict__ offs,
                                                       const TreeLevel cur, const TreeLevel nxt, const int cap) {
     const int b = blockIdx.x;
     const int n = G.c_count[b], base = offs[b];
-    for (int k = threadIdx.x; k < n; k += 256) {
+    auto move = [&](int k, int dst) {
         const size_t q = (size_t)b * 512 + k;
-        const int dst = base + k;
-        if (dst >= cap) break;                       // over the planned capacity (k_tree_scan flagged it)
         nxt.o[dst] = G.c_o[q];
         nxt.d[dst] = G.c_d[q];
         nxt.key[dst] = G.c_key[q];
@@ -372,7 +377,58 @@ __global__ __launch_bounds__(256) void k_tree_compact(const TreeSegs G, const in
         const int parent = p & 0x3FFFFFFF, slot = p >> 30;
         int* ext = reinterpret_cast<int*>(&cur.ext[parent]);
         ext[2 + slot] = dst;
+    };
+    if constexpr (SORT) {
+        __shared__ int wc[2][4][8];                  // per (round, wave, octant): count, then offset
+        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+        int oc[2], rk[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            const int k = r * 256 + (int)threadIdx.x;
+            int o = -1;
+            if (k < n) {
+                const float4 d = G.c_d[(size_t)b * 512 + k];
+                o = (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0);
+            }
+            oc[r] = o;
+            rk[r] = 0;
+            for (int c = 0; c < 8; ++c) {
+                const uint64_t m = __ballot(o == c);
+                if (o == c) rk[r] = __popcll(m & ((1ull << lane) - 1ull));
+                if (lane == 0) wc[r][w][c] = __popcll(m);
+            }
+        }
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            int run = 0;
+            for (int c = 0; c < 8; ++c)
+                for (int r = 0; r < 2; ++r)
+                    for (int v = 0; v < 4; ++v) {
+                        const int t = wc[r][v][c];
+                        wc[r][v][c] = run;
+                        run += t;
+                    }
+        }
+        __syncthreads();
+#pragma unroll
+        for (int r = 0; r < 2; ++r) {
+            if (oc[r] < 0) continue;
+            const int dst = base + wc[r][w][oc[r]] + rk[r];
+            if (dst < cap) move(r * 256 + (int)threadIdx.x, dst);   // (over capacity: k_tree_scan flagged it)
+        }
+    } else {
+        for (int k = threadIdx.x; k < n; k += 256) {
+            const int dst = base + k;
+            if (dst >= cap) break;                   // over the planned capacity (k_tree_scan flagged it)
+            move(k, dst);
+        }
     }
+}
+
+// RTG_TREE_SORT=1 (A/B): k_tree_compact groups each block's children by direction octant
+static bool tree_sort() {
+    const char* v = std::getenv("RTG_TREE_SORT");
+    return v && std::strcmp(v, "0") != 0;
 }
 
 __global__ __launch_bounds__(256) void k_tree_resolve(const DevScene S, const DevCamera C, const RenderParams P,
@@ -456,7 +512,7 @@ __global__ __launch_bounds__(256) void k_tree_resolve(const DevScene S, const De
         return;
     }
     // level 0: the pixel (RenderPixel's colour), spp accumulation as k_resolve
-    const int pixel = part_pixel(P, C.width, i);
+    const int pixel = tree_pixel(P, C.width, i);
     if (C.spp <= 1 && !P.accum_only) {
         const size_t idx = 3 * (size_t)pixel;
         if (hdr) { hdr[idx] = value.x; hdr[idx + 1] = value.y; hdr[idx + 2] = value.z; }
@@ -566,6 +622,14 @@ static int tree_packet_levels() {
     return v ? std::atoi(v) : 0;
 }
 
+// The levels' shadow rays (RTG_TREE_SHADOW_FAST, A/B): 1 the any-hit packet walk, 2 the any-hit
+// tree walked per lane (k_shadow_lane), both exact as in the wavefront pipeline; 0 the reference
+// walk per lane (round 3 measured the packet walk slower on the incoherent levels)
+static int tree_shadow_fast() {
+    const char* v = std::getenv("RTG_TREE_SHADOW_FAST");
+    return v ? std::atoi(v) : 0;
+}
+
 // RTG_TREE_CLOSEST=1 (A/B): the levels not on the packet walk take the checked closest-hit walk
 // of the any-hit tree per lane
 static bool tree_closest() { return std::getenv("RTG_TREE_CLOSEST") != nullptr; }
@@ -594,7 +658,14 @@ static void level_launches(TreeState& T, const DevScene& S, const DevCamera& C, 
         W.num_slots = ns;
         W.hit_obj = L.obj;              // the hits the shadow rays leave (their origin leaf)
         W.hit_face = L.face;
-        hipLaunchKernelGGL((k_shadow<STATS, FEAT, false>), dim3(blocks, ns), dim3(256), 0, st, S, W, cnt);
+        const int sf = tree_shadow_fast();
+        if (sf && S.anodes && !S.exact_shadow && !(FEAT & FEAT_BIGLEAF) && !S.ahb_split) {
+            if (sf == 2)
+                hipLaunchKernelGGL((k_shadow_lane<STATS, FEAT>), dim3(blocks, ns), dim3(256), 0, st, S, W, cnt);
+            else
+                hipLaunchKernelGGL((k_shadow<STATS, FEAT, true>), dim3(blocks, ns), dim3(256), 0, st, S, W, cnt);
+        } else
+            hipLaunchKernelGGL((k_shadow<STATS, FEAT, false>), dim3(blocks, ns), dim3(256), 0, st, S, W, cnt);
     }
     hipLaunchKernelGGL(k_tree_scan, dim3(1), dim3(1024), 0, st, T.G.c_count, blocks, T.offs, next_n, cap_next,
                        T.d_counts ? T.d_counts + kMaxLevels : nullptr);
@@ -630,8 +701,12 @@ static hipError_t tree_pass_sync(TreeState& T, const DevScene& S, const DevCamer
         sizes.push_back(nn);
         if ((int)T.levels.size() <= level + 1) T.levels.emplace_back();
         if ((e = ensure_level(T.levels[level + 1], nn, ns)) != hipSuccess) return e;
-        hipLaunchKernelGGL(k_tree_compact, dim3(blocks), dim3(256), 0, st, T.G, T.offs, T.levels[level].L,
-                           T.levels[level + 1].L, (int)nn);
+        if (tree_sort())
+            hipLaunchKernelGGL(k_tree_compact<true>, dim3(blocks), dim3(256), 0, st, T.G, T.offs, T.levels[level].L,
+                               T.levels[level + 1].L, (int)nn);
+        else
+            hipLaunchKernelGGL(k_tree_compact<false>, dim3(blocks), dim3(256), 0, st, T.G, T.offs, T.levels[level].L,
+                               T.levels[level + 1].L, (int)nn);
         n = nn;
     }
     if (ev) (void)hipEventRecord(ev[1], st);
@@ -670,7 +745,11 @@ static hipError_t tree_pass_async(TreeState& T, const DevScene& S, const DevCame
             TreeLevel& Ln = T.levels[level + 1].L;
             Ln.n = (int)T.plan[level + 1];
             Ln.nd = T.d_counts + level + 1;
-            hipLaunchKernelGGL(k_tree_compact, dim3(blocks), dim3(256), 0, st, T.G, T.offs, L, Ln,
+            if (tree_sort())
+                hipLaunchKernelGGL(k_tree_compact<true>, dim3(blocks), dim3(256), 0, st, T.G, T.offs, L, Ln,
+                               (int)T.plan[level + 1]);
+            else
+                hipLaunchKernelGGL(k_tree_compact<false>, dim3(blocks), dim3(256), 0, st, T.G, T.offs, L, Ln,
                                (int)T.plan[level + 1]);
         }
     }

@@ -769,6 +769,7 @@ bool defer_leaves();
 int defer_any_leaves();
 bool wide_bigleaf();
 bool defer_diag();
+int refwalk_blocks();
 
 // One traversal variant's pass sequence (instantiated in rtg_wave_a.hip / rtg_wave_b.hip).
 template <bool STATS, int FEAT>
@@ -827,7 +828,7 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
                 hipLaunchKernelGGL((k_bigleaf<FEAT>), dim3(2048), dim3(256), 0, st, S, W);
                 hipLaunchKernelGGL((k_hitfix<FEAT>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W,
                                    defer_diag() ? cnt : nullptr);
-                hipLaunchKernelGGL((k_refwalk<FEAT>), dim3(256), dim3(256), 0, st, S, C, P, s, W);
+                hipLaunchKernelGGL((k_refwalk<FEAT>), dim3(refwalk_blocks()), dim3(256), 0, st, S, C, P, s, W);
                 deferred = true;
             }
         }

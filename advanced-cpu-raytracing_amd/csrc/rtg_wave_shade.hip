@@ -32,6 +32,16 @@ __global__ __launch_bounds__(256) void k_resolve(const DevCamera C, const Render
 // (experiment; by default they take the cooperative reference walk)
 bool wide_bigleaf() { return std::getenv("RTG_WIDE_BIGLEAF") != nullptr; }
 
+// k_refwalk's grid (one unsettled pixel's reference walk per wave, grid-stride): 256 blocks,
+// 1 024 waves.  RTG_REFWALK_BLOCKS (A/B): 2 048 blocks, a wave for each of C4's ~2 000
+// pixels per pass, measured the same (C4 k_primary stage 0.895 ms either way,
+// profiles/r05g_c4_refwalk_ab.txt)
+int refwalk_blocks() {
+    const char* v = std::getenv("RTG_REFWALK_BLOCKS");
+    const int n = v ? std::atoi(v) : 256;
+    return n > 0 ? n : 256;
+}
+
 // RTG_DEFER_DIAG=1: k_hitfix counts pending / checked-out pixels of production renders into
 // extend_wide_visits / extend_fallbacks (tools/diag_defer.py); otherwise an uncounted render
 // leaves the counters untouched, as every other pipeline does

@@ -246,12 +246,14 @@ def kernel_bytes(st, W, H):
             "tree_levels": ext + shd, "frame": ext + shd + 15 * W * H}
 
 
-def pmc_summary(kernel, K, world, share=1.0):
-    """Counter-measured bytes per launch of `kernel` for the K-triangle headline scene from
-    the newest committed summary (profiles/r*_pmc*.json, tools/pmc_summary.py over separate
-    rocprofv3 --pmc passes of this bench, tools/pmc_kernels.py): HBM traffic = 2 x FETCH_SIZE +
-    WRITE_SIZE (gfx950 correction, MI355X_MICROARCH.md), L2 hit rate from TCC_HIT / TCC_MISS,
-    L2 requests, vL1D hit rate, SQ instruction counts and wave-cycle split.  None if absent.
+def pmc_summary(kernel, K, world, share=1.0, workload="headline"):
+    """Counter-measured bytes per launch of `kernel` for the K-triangle headline scene (or the
+    BASELINE configuration `workload`) from the newest committed summary (profiles/r*_pmc*.json,
+    tools/pmc_kernels.py over separate rocprofv3 --pmc passes of this bench): HBM traffic =
+    2 x FETCH_SIZE + WRITE_SIZE (gfx950 correction, MI355X_MICROARCH.md), L2 hit rate from
+    TCC_HIT / TCC_MISS, L2 requests, vL1D hit rate, SQ instruction counts and wave-cycle split.
+    A timed stage that spans several kernels (deferred leaves, the ray-tree levels) takes the
+    summary's per-pass stage sums ("stage:<name>").  None if absent.
 
     N > 1 (no committed profile of a 1/N part): the N = 1 counters with every extensive count
     (instructions, bytes, requests, waves) scaled by this rank's share of the frame's rays and
@@ -260,17 +262,20 @@ def pmc_summary(kernel, K, world, share=1.0):
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc*.json"))):
         rec = json.load(open(f))
         cfg = rec.get("config", {"K": 100352, "n_gpus": 1})
-        if cfg.get("K") != K or cfg.get("n_gpus", 1) != world:
+        if cfg.get("workload", "headline") != workload or cfg.get("n_gpus", 1) != world:
+            continue
+        if workload == "headline" and cfg.get("K") != K:
             continue
         # the timed kernels (the counting pass runs the <true> = STATS instantiations)
-        v = rec["kernels"].get(kernel + "<false>") or rec["kernels"].get(kernel)
+        v = (rec["kernels"].get("stage:" + kernel) or rec["kernels"].get(kernel + "<false>") or
+             rec["kernels"].get(kernel))
         if v and "traffic_bytes" in v:
             best = dict(v, source=os.path.basename(f))
             best.setdefault("l2_request_bytes", 128 * v["l2_requests"] if "l2_requests" in v else None)
             if best["l2_request_bytes"] is None:
                 del best["l2_request_bytes"]
     if best is None and world > 1:
-        one = pmc_summary(kernel, K, 1)
+        one = pmc_summary(kernel, K, 1, workload=workload)
         if one:
             best = {k: (v * share if isinstance(v, (int, float)) and not k.endswith(("_frac", "_rate")) else v)
                     for k, v in one.items()}
@@ -523,7 +528,7 @@ def main():
         dom = max((k for k in ktimes if k in kbytes), key=lambda k: ktimes[k])
         K = int(args.K) if args.config == "headline" else None
         share = part_rays / max(rays, 1)
-        rl = roofline(dom, kbytes[dom], ktimes[dom], pmc_summary(dom, K, world, share) if K else None)
+        rl = roofline(dom, kbytes[dom], ktimes[dom], pmc_summary(dom, K, world, share, workload=args.config))
         rl.update({"kernels_ms": {k: round(v, 4) for k, v in ktimes.items()}, "frame_ms": round(kern_ms, 4),
                    "frame_algo_bytes": int(kernel_bytes(st, W, H)["frame"]),
                    "frame_l2_frac": round(kernel_bytes(st, W, H)["frame"] / (kern_ms * 1e-3) / 1e9 / L2_PEAK_GBS, 4)})

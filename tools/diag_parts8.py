@@ -3,6 +3,9 @@ stream), per part: the time per part-frame and the host's issue time -- what one
 N-GPU node does per step (bench.py part_scaling, alone, for A/B of run-time settings).
 
     RTG_DIAG_F=8 RTG_DIAG_N=8 python tools/diag_parts8.py [steps]
+
+RTG_DIAG_PARTS=0,3 renders only those parts (e.g. under rocprofv3 --kernel-trace, whose
+trace tools/trace_parts.py reads).
 """
 import json
 import os
@@ -32,7 +35,9 @@ def main():
              torch.empty((1080, 1920, 3), dtype=torch.uint8, device="cuda")) for _ in range(F)]
     streams = [torch.cuda.Stream() for _ in range(F)]
     full = []
-    for parts in ((0, 1),) + tuple((r, N) for r in range(N)):
+    only = os.environ.get("RTG_DIAG_PARTS")
+    sel = [int(x) for x in only.split(",")] if only else list(range(N))
+    for parts in ((0, 1),) + tuple((r, N) for r in sel):
         def step(k):
             h, l = bufs[k % F]
             reps[k % F].render_device(h.data_ptr(), l.data_ptr(), streams[k % F].cuda_stream, seed=7, part=parts)

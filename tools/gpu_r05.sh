@@ -62,6 +62,14 @@ for s in "${steps[@]}"; do
       echo "$(date +%T) start kt$name" >> $st
       timeout -k 10 ${PMC_TIMEOUT:-120} rocprofv3 --kernel-trace --stats -f csv -d $pd/kt -o run -- python bench.py $args > $pd/kt.log 2>&1
       rc=$?; echo "$(date +%T) kt$name rc=$rc" >> $st
+      if [ $rc -ne 0 ]; then exit $rc; fi
+      # summarise on the box and drop the per-dispatch CSVs (gpurun copies back at most 64 MiB)
+      wl=headline; K=100352
+      case $name in c2|c3|c3ton|c4|c5) wl=$name; K=0 ;; K*) K=${name#K} ;; esac
+      python tools/pmc_kernels.py $pd $pd/summary.json --workload $wl --K $K > $pd/summary.log 2>&1
+      rc=$?; echo "$(date +%T) summary$name rc=$rc" >> $st
+      find $pd -name "*counter_collection.csv" -delete
+      find $pd -name "*kernel_trace.csv" -delete
       if [ $rc -ne 0 ]; then exit $rc; fi ;;
     configs)
       for c in c2 c3 c3ton c4; do
@@ -81,6 +89,17 @@ for s in "${steps[@]}"; do
         envs=()
         [ "$setting" != base ] && IFS=, read -ra envs <<< "$setting"
         run envbench_$name 300 env "${envs[@]}" python bench.py --no-sweep --no-cpu-baseline $extra
+      done ;;
+    envcfg:*)
+      # bench.py --config <c> (no extras) once per setting in $ENV_AB, twice interleaved
+      c=${s#envcfg:}
+      for rep in 1 2; do
+        for setting in $ENV_AB; do
+          name=${setting//[=,]/_}
+          envs=()
+          [ "$setting" != base ] && IFS=, read -ra envs <<< "$setting"
+          run envcfg_${c}_${name}_$rep 400 env "${envs[@]}" python bench.py --config $c --no-extras --no-cpu-baseline --steps ${CFG_STEPS:-10} $extra
+        done
       done ;;
     envpy:*)
       # tools/<name>.py once per setting in $ENV_AB

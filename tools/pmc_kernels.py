@@ -39,7 +39,41 @@ def load(run_dir):
                 base = "k_shade_shadow"                  # SH_FUSED / SH_FUSED_N: shading + shadow rays
             name = base + (f"<{targs[0]}>" if targs else "")
             agg[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
-    return {k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in agg.items()}
+    return ({k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in agg.items()},
+            {k: {c: (sum(v), len(v)) for c, v in d.items()} for k, d in agg.items()})
+
+
+# The library's timed stages (rtg_scene_timings) and the production kernels each one spans:
+# a stage's counters are the sums over its kernels' launches in the run divided by the
+# passes (launches of the stage's first kernel), i.e. per sample pass like its HIP-event time.
+STAGES = {
+    "k_primary": ("k_primary", "k_bigleaf", "k_hitfix", "k_refwalk"),
+    "k_shadow": ("k_shadow", "k_shadow_one", "k_bigleaf_any", "k_shadow_fin", "k_shadow_fin_one"),
+    "tree_levels": ("k_tree_gen", "k_tree_trace", "k_tree_shade", "k_shadow", "k_tree_scan", "k_tree_compact"),
+}
+EXTENSIVE = ("FETCH_SIZE", "WRITE_SIZE", "TCC_HIT_sum", "TCC_MISS_sum", "TCC_REQ_sum", "TCP_TOTAL_CACHE_ACCESSES_sum",
+             "TCP_TCC_READ_REQ_sum", "TCP_TCC_WRITE_REQ_sum", "SQ_WAVES", "SQ_INSTS_VALU", "SQ_INSTS_SALU",
+             "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_LDS", "SQ_INSTS_SMEM", "SQ_INSTS_BRANCH",
+             "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY")
+
+
+def stage_sums(totals, stage, tree):
+    """Per-pass sums of a stage's production kernels (<false> / non-STATS instantiations);
+    tree: the ray-tree pipeline's k_shadow belongs to tree_levels, not to a k_shadow stage."""
+    members = STAGES[stage]
+    names = [k for k in totals if k.split("<")[0] in members and "<true>" not in k]
+    if not names:
+        return None
+    first = next((k for m in members for k in names if k.split("<")[0] == m), None)
+    out = {}
+    passes = 0
+    for c in EXTENSIVE:
+        vals = [totals[k][c][0] for k in names if c in totals[k]]
+        if vals and c in totals[first]:
+            n = totals[first][c][1]            # launches of the first kernel seen by this counter's pass(es)
+            out[c] = sum(vals) / n
+            passes = max(passes, n)
+    return out, sorted(names), passes
 
 
 def summarise(a):
@@ -76,14 +110,24 @@ def main():
     ap.add_argument("out", nargs="?")
     ap.add_argument("--K", type=int, default=100352)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--workload", default="headline")
+    ap.add_argument("--workload", default="headline", help="headline or a bench.py --config name (c3, c3ton, c4, c5)")
     a = ap.parse_args()
     res = {"note": "per launch; read = 2 x FETCH_SIZE (gfx950 correction), write = WRITE_SIZE; l2_hit_rate = "
                    "TCC_HIT / (TCC_HIT + TCC_MISS); l1_hit_rate = 1 - TCP_TCC_READ_REQ / TCP_TOTAL_CACHE_ACCESSES; "
                    "instruction counts SQ_INSTS_*; fractions of SQ_WAVE_CYCLES (tools/pmc_kernels.py)",
            "source": os.path.basename(os.path.normpath(a.run_dir)),
            "config": {"workload": a.workload, "K": a.K, "n_gpus": a.gpus},
-           "kernels": {k: summarise(v) for k, v in sorted(load(a.run_dir).items())}}
+           "kernels": {}}
+    avg, totals = load(a.run_dir)
+    res["kernels"] = {k: summarise(v) for k, v in sorted(avg.items())}
+    tree = any(k.startswith("k_tree_trace") for k in totals)
+    for stage in (("tree_levels",) if tree else ("k_primary", "k_shadow")):
+        got = stage_sums(totals, stage, tree)
+        if got:
+            sums, names, passes = got
+            e = summarise(sums)
+            e.update(members=names, passes=passes, per="sample pass (sum over the stage's kernels)")
+            res["kernels"]["stage:" + stage] = e
     for k, v in res["kernels"].items():
         print(k, json.dumps(v))
     if a.out:
