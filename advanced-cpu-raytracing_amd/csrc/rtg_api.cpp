@@ -1671,13 +1671,14 @@ int rtg_scene_reset_stats(rtg_scene* s) {
 
 int rtg_scene_timings(rtg_scene* s, float* ms, const char** names, int32_t cap, int32_t* count) {
     // stage names per layout (rtg_kernels.hpp LAYOUT_*)
-    static const char* kNames[6][rtg::MAX_STAGES] = {{"k_primary", "k_shade", "k_shadow", "k_resolve"},
+    static const char* kNames[7][rtg::MAX_STAGES] = {{"k_primary", "k_shade", "k_shadow", "k_resolve"},
                                                      {"k_primary", "k_shade", "k_shadow"},
                                                      {"k_primary", "k_shade_shadow"},
                                                      {"tree_levels", "tree_resolve"},
                                                      {"k_render"},
-                                                     {"path_iterations"}};
-    static const int kCount[6] = {rtg::WAVE_STAGES, 3, 2, rtg::TREE_STAGES, rtg::MEGA_STAGES, rtg::PATH_STAGES};
+                                                     {"path_iterations"},
+                                                     {"k_frame"}};
+    static const int kCount[7] = {rtg::WAVE_STAGES, 3, 2, rtg::TREE_STAGES, rtg::MEGA_STAGES, rtg::PATH_STAGES, 1};
     if (!s || !count) return set_err(RTG_ERR_INVALID, "null argument");
     if (s->timed_layout < 0) return set_err(RTG_ERR_INVALID, "no render was issued with RTG_RENDER_TIMING");
     HIP_TRY(hipSetDevice(s->device));

@@ -68,6 +68,7 @@ enum { LAYOUT_WAVE = 0,          // k_primary, k_shade, k_shadow, k_resolve
        LAYOUT_WAVE_ONE = 1,      // k_primary, k_shade, k_shadow (k_shadow_one finishes pixels)
        LAYOUT_WAVE_FUSED = 2,    // k_primary, k_shade_shadow
        LAYOUT_TREE = 3, LAYOUT_MEGA = 4,
-       LAYOUT_PATH = 5 };          // the last sample pass of the wavefront path tracer
+       LAYOUT_PATH = 5,            // the last sample pass of the wavefront path tracer
+       LAYOUT_WAVE_FRAME = 6 };    // k_frame: the fused layout's whole sample pass in one kernel
 
 }  // namespace rtg

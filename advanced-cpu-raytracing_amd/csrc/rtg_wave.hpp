@@ -798,7 +798,8 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
     // shading fused with the shadow ray: plain shading, the fast any-hit walk (RTG_NO_FUSED_SHADE=1
     // keeps the queue: experiments)
     const bool fused = scene_sk == 0 && fast && !(FEAT & FEAT_BIGLEAF) && nshadow > 0 && !no_fused_shade();
-    *layout = fused ? LAYOUT_WAVE_FUSED : (one ? LAYOUT_WAVE_ONE : LAYOUT_WAVE);
+    *layout = fused ? (frame_kernel() && !(FEAT == 0 && S.ordered) ? LAYOUT_WAVE_FRAME : LAYOUT_WAVE_FUSED)
+                    : (one ? LAYOUT_WAVE_ONE : LAYOUT_WAVE);
     for (int s = P.sample_begin; s < P.sample_begin + P.sample_count; ++s) {
         const int first = s == P.sample_begin, last = s == P.sample_begin + P.sample_count - 1;
         const PassOut O{hdr, l, W.accum, first, last};
@@ -815,7 +816,9 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
                 ordered = true;
             }
         }
-        // RTG_FRAME_KERNEL (fused layout, no motion blur): one launch per sample pass
+        // the fused layout's sample pass as one launch (k_frame; RTG_FRAME_KERNEL=0: k_primary +
+        // k_shade_shadow, A/B): round 5, with both walks lean, 0.311 -> 0.288 ms per headline frame
+        // and a part of 1/8 of it 0.0428 -> 0.0403 ms (profiles/r05k_frame_kernel_ab.txt)
         const bool frame = fused && frame_kernel() && !ordered;
         // large-leaf scenes: the camera walk defers large leaves (k_bigleaf, k_hitfix; production
         // renders only -- counting renders keep the cooperative walk and the reference's counts)
@@ -834,7 +837,7 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
         }
         if (!ordered && !frame && !deferred)
             hipLaunchKernelGGL((k_primary<STATS, FEAT>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
-        if (e5) (void)hipEventRecord(e5[1], st);
+        if (e5 && !frame) (void)hipEventRecord(e5[1], st);
         if (frame) {
             if constexpr (!(FEAT & FEAT_BIGLEAF)) {
                 if (one)
@@ -844,7 +847,7 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
                     hipLaunchKernelGGL((k_shade<STATS, 0, SH_FUSED_N, FEAT, true, true>), dim3(P.num_tiles), dim3(256),
                                        0, st, S, C, P, s, W, O, cnt);
             }
-            if (e5) (void)hipEventRecord(e5[2], st);
+            if (e5) (void)hipEventRecord(e5[1], st);             // LAYOUT_WAVE_FRAME: one stage
         } else if (fused) {
             if constexpr (!(FEAT & FEAT_BIGLEAF)) {
                 if (one)

@@ -71,10 +71,11 @@ int defer_any_leaves() {
     return !v ? 2 : std::strcmp(v, "0") == 0 ? 0 : 1;
 }
 
-// RTG_FRAME_KERNEL=1: the fused layout's two kernels as one (k_shade<..., FRAME>: A/B)
+// The fused layout's two kernels as one (k_shade<..., FRAME>, default since round 5;
+// RTG_FRAME_KERNEL=0: k_primary + k_shade_shadow)
 bool frame_kernel() {
-    static const bool v = std::getenv("RTG_FRAME_KERNEL") != nullptr;
-    return v;
+    const char* e = std::getenv("RTG_FRAME_KERNEL");
+    return !e || std::strcmp(e, "0") != 0;
 }
 
 bool no_fused_shade() {

@@ -237,13 +237,14 @@ def kernel_bytes(st, W, H):
     """Algorithmic bytes per launch of each kernel (32 B per node visit,
     36 B per triangle test, 64 B per ray = ray in + hit out, 15 B per pixel written; the
     shadow rays' 4-wide BVH nodes are 128 B: four child boxes + references, RTG_SHADOW_MODE 3, the
-    default build)."""
+    default build).  k_frame (the fused layout's one kernel per sample pass, the headline's
+    default since round 5): camera + shadow rays + pixels."""
     ext_rays = st["camera_rays"] + st["secondary_rays"]
     ext = 32 * st["node_visits"] + 36 * st["tri_tests"] + 64 * ext_rays
     shd = (32 * st["shadow_node_visits"] + 128 * st.get("shadow_wide_visits", 0) + 36 * st["shadow_tri_tests"]
            + 64 * st["shadow_rays"])
     return {"k_primary": ext, "k_shadow": shd, "k_shade_shadow": shd + 15 * W * H, "k_render": ext + shd + 15 * W * H,
-            "tree_levels": ext + shd, "frame": ext + shd + 15 * W * H}
+            "k_frame": ext + shd + 15 * W * H, "tree_levels": ext + shd, "frame": ext + shd + 15 * W * H}
 
 
 def pmc_summary(kernel, K, world, share=1.0, workload="headline"):

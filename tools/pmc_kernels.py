@@ -36,7 +36,8 @@ def load(run_dir):
                 continue
             base, targs = m.group(1), [t.strip() for t in (m.group(3) or "").split(",") if t.strip()]
             if base == "k_shade" and len(targs) >= 3 and targs[2] in ("2", "3"):
-                base = "k_shade_shadow"                  # SH_FUSED / SH_FUSED_N: shading + shadow rays
+                # SH_FUSED / SH_FUSED_N: shading + shadow rays; with FRAME also the camera walk
+                base = "k_frame" if len(targs) >= 6 and targs[5] == "true" else "k_shade_shadow"
             name = base + (f"<{targs[0]}>" if targs else "")
             agg[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
     return ({k: {c: sum(v) / len(v) for c, v in d.items()} for k, d in agg.items()},
