@@ -259,13 +259,11 @@ DEV float vmin3(float a, float b, float c) {
 // no NaN among tmax, d1, d2.  Unsure lanes inside their walk take the exact test (uniform branch).
 // Returns a value whose sign is the answer (> 0: the lane takes part and the box passes), so a
 // caller's ballot of `> 0` is one comparison; actf > 0: the lane takes part.
-// INT: actf is an integer (rel), so `act & !sure` is one comparison, !(max(su, 0.5 - actf) > 0)
+// INT: actf is an integer (rel), so `act & !sure` is one comparison, !(max(su, 0.5 - actf) > 0).
+// box_pass_t takes the six slab distances (m - o) * rcp; the box for the exact fallback.
 template <bool INT = false>
-DEV float box_pass_v(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, const Ray& r, const RayRcp& q,
-                     float minT, float actf, float slack0) {
-    const float tx1 = (mnx - r.o.x) * q.ix, tx2 = (mxx - r.o.x) * q.ix;
-    const float ty1 = (mny - r.o.y) * q.iy, ty2 = (mxy - r.o.y) * q.iy;
-    const float tz1 = (mnz - r.o.z) * q.iz, tz2 = (mxz - r.o.z) * q.iz;
+DEV float box_pass_t(float tx1, float tx2, float ty1, float ty2, float tz1, float tz2, float mnx, float mny, float mnz,
+                     float mxx, float mxy, float mxz, const Ray& r, float minT, float actf, float slack0) {
     const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
     const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
     const float atmin = fabsf(tmin), atmax = fabsf(tmax);
@@ -280,6 +278,14 @@ DEV float box_pass_v(float mnx, float mny, float mnz, float mxx, float mxy, floa
         if (unsure) pv = box_hit(mnx, mny, mnz, mxx, mxy, mxz, r, minT) ? 1.0f : -1.0f;
     }
     return pv;
+}
+template <bool INT = false>
+DEV float box_pass_v(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, const Ray& r, const RayRcp& q,
+                     float minT, float actf, float slack0) {
+    const float tx1 = (mnx - r.o.x) * q.ix, tx2 = (mxx - r.o.x) * q.ix;
+    const float ty1 = (mny - r.o.y) * q.iy, ty2 = (mxy - r.o.y) * q.iy;
+    const float tz1 = (mnz - r.o.z) * q.iz, tz2 = (mxz - r.o.z) * q.iz;
+    return box_pass_t<INT>(tx1, tx2, ty1, ty2, tz1, tz2, mnx, mny, mnz, mxx, mxy, mxz, r, minT, actf, slack0);
 }
 DEV bool box_pass_pk(float mnx, float mny, float mnz, float mxx, float mxy, float mxz, const Ray& r, const RayRcp& q,
                      float minT, int rel, float slack0) {
@@ -499,6 +505,34 @@ DEV void sload_node(const float4* p, rtg_s8& a) {                // 32 B: a refe
 }
 DEV float4 f4(int x, int y, int z, int w) {
     return make_float4(__int_as_float(x), __int_as_float(y), __int_as_float(z), __int_as_float(w));
+}
+// Packed slab distances of a reference node record {min.xyz, max.x}{max.yz, skip, leaf} in
+// SGPRs: its adjacent pairs (min.x, min.y), (min.z, max.x), (max.y, max.z) against the ray
+// origin and reciprocal arranged the same way, three v_pk_add_f32 + three v_pk_mul_f32 for the
+// six (m - o) * rcp (each lane of a packed op rounds as the scalar op: the same values)
+typedef float rtg_f2 __attribute__((ext_vector_type(2)));
+struct RayPk {
+    rtg_f2 o01, o20, o12, i01, i20, i12;
+};
+template <typename RQ>
+DEV RayPk ray_pk(const Ray& r, const RQ& q) {
+    RayPk p;
+    p.o01 = rtg_f2{r.o.x, r.o.y};
+    p.o20 = rtg_f2{r.o.z, r.o.x};
+    p.o12 = rtg_f2{r.o.y, r.o.z};
+    p.i01 = rtg_f2{q.ix, q.iy};
+    p.i20 = rtg_f2{q.iz, q.ix};
+    p.i12 = rtg_f2{q.iy, q.iz};
+    return p;
+}
+// box_pass_pk on a node record in SGPRs with packed slab distances (rel: as box_pass_pk)
+DEV bool box_pass_rec(const int* nd, const RayPk& rp, const Ray& r, float minT, int rel, float slack0) {
+    const rtg_f2 t01 = (rtg_f2{__int_as_float(nd[0]), __int_as_float(nd[1])} - rp.o01) * rp.i01;   // tx1, ty1
+    const rtg_f2 t20 = (rtg_f2{__int_as_float(nd[2]), __int_as_float(nd[3])} - rp.o20) * rp.i20;   // tz1, tx2
+    const rtg_f2 t12 = (rtg_f2{__int_as_float(nd[4]), __int_as_float(nd[5])} - rp.o12) * rp.i12;   // ty2, tz2
+    return box_pass_t<true>(t01.x, t20.y, t01.y, t12.x, t20.x, t12.y, __int_as_float(nd[0]), __int_as_float(nd[1]),
+                            __int_as_float(nd[2]), __int_as_float(nd[3]), __int_as_float(nd[4]), __int_as_float(nd[5]),
+                            r, minT, (float)rel, slack0) > 0.0f;
 }
 
 // 64-bit lexicographic (t, face) key of a candidate hit; t > 0, so the float bits order
@@ -795,6 +829,10 @@ DEV const T* rec_at(const T* base, int i) {
 #ifndef RTG_PK_LEAN
 #define RTG_PK_LEAN 1
 #endif
+// the camera packet walk's slab distances as three packed pairs of the node record (box_pass_rec)
+#ifndef RTG_PK_PAIRS
+#define RTG_PK_PAIRS 1
+#endif
 // (A/B parts of the lean packet walks: the any-hit walk, the closest-hit walk's face test)
 #ifndef RTG_PK_LEAN_ANY
 #define RTG_PK_LEAN_ANY RTG_PK_LEAN
@@ -831,6 +869,9 @@ DEV bool walk_bvh_packet(const DevScene& S, int begin, int end, const Ray& r, fl
     const RayRcp q = ray_rcp(r);
 #if RTG_PK_LEAN
     const float slack0 = q.fast ? 1e-30f : INFINITY;   // box_pass_pk: a ray off the fast path is never sure
+#if RTG_PK_PAIRS
+    const RayPk rp = ray_pk(r, q);
+#endif
 #endif
     const int kDone = 0x7FFFFFFF;
     int resume = begin;                              // per lane: first node it takes part in again
@@ -853,12 +894,16 @@ DEV bool walk_bvh_packet(const DevScene& S, int begin, int end, const Ray& r, fl
             continue;
         }
         i = __builtin_amdgcn_readfirstlane(i);
+        const int ip1 = i + 1;                       // (shared by rel and the next-node select)
         float4 a, b;
+        int ndr[8];
         if constexpr (SC) {
             rtg_s8 nd;
             sload_node(rec_at<32>(S.nodes, i), nd);
             a = f4(nd[0], nd[1], nd[2], nd[3]);
             b = f4(nd[4], nd[5], nd[6], nd[7]);
+#pragma unroll
+            for (int u = 0; u < 8; ++u) ndr[u] = nd[u];
         } else {
             a = S.nodes[2 * i];
             b = S.nodes[2 * i + 1];
@@ -869,7 +914,11 @@ DEV bool walk_bvh_packet(const DevScene& S, int begin, int end, const Ray& r, fl
         if constexpr (SC) {
             if (act) c.template node<ANY>();
 #if RTG_PK_LEAN
-            pass = box_pass_pk(a.x, a.y, a.z, a.w, b.x, b.y, r, q, minT, i + 1 - resume, slack0);
+#if RTG_PK_PAIRS
+            pass = box_pass_rec(ndr, rp, r, minT, ip1 - resume, slack0);
+#else
+            pass = box_pass_pk(a.x, a.y, a.z, a.w, b.x, b.y, r, q, minT, ip1 - resume, slack0);
+#endif
             // a lane inside its walk that fails the box resumes at the box's skip; lanes outside it
             // already wait for a node past this box's subtree (resume >= skip), as do lanes that pass
             resume = max(resume, pass ? 0 : skip);
@@ -900,11 +949,10 @@ DEV bool walk_bvh_packet(const DevScene& S, int begin, int end, const Ray& r, fl
             int nx;
             asm("s_cmp_lg_u64 %[pm], 0\n\t"
                 "s_cselect_b32 %[lf], %[leaf], 0\n\t"
-                "s_add_i32 %[nx], %[i], 1\n\t"
                 "s_cmp_lt_i32 %[lf], 0\n\t"
-                "s_cselect_b32 %[nx], %[nx], %[skip]"
+                "s_cselect_b32 %[nx], %[ip1], %[skip]"
                 : [lf] "=&s"(lf), [nx] "=&s"(nx)
-                : [pm] "s"(pm), [leaf] "s"(leaf), [i] "s"(i), [skip] "s"(skip)
+                : [pm] "s"(pm), [leaf] "s"(leaf), [ip1] "s"(ip1), [skip] "s"(skip)
                 : "scc");
             i = nx;
         }
