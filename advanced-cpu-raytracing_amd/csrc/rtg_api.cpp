@@ -193,6 +193,14 @@ extern "C" {
 const char* rtg_last_error(void) { return g_err.c_str(); }
 int rtg_abi_version(void) { return RTG_ABI_VERSION; }
 
+// Build provenance (not part of the ABI): the SHA-256 prefix of the sources this library was
+// compiled from (csrc/*, include/rtgpu.h, the Makefile's recipe), so that smoke() can show the
+// prebuilt library that travels to the GPU box is the build of the tree it runs beside.
+#ifndef RTG_SRC_HASH
+#define RTG_SRC_HASH "unknown"
+#endif
+extern "C" __attribute__((visibility("default"))) const char rtg_source_hash[] = RTG_SRC_HASH;
+
 int rtg_host_scene_load_xml(const char* xml_path, rtg_host_scene** out) {
     return rtg_host_scene_load_xml_ex(xml_path, 0, out);
 }
