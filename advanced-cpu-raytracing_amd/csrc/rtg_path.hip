@@ -33,6 +33,14 @@
 // Every path sits in one queue at a time (trace T, rest R, unwind U); its RestArgs (112 B) or
 // ChildVal (32 B) wait in HBM by path index.
 //
+// Path regeneration (the default for the single step kernel; RTG_PATH_REGEN=0: one pass per
+// sample): a pass covers all of the render's samples.  Path slot i is pixel i of the chunk; when
+// its sample finishes, the step kernel accumulates it and starts the slot's next sample (its
+// camera ray) in the same iteration, so the queue stays full until the last samples and each
+// pixel's samples are still summed in sample order (one slot does them one after another).  A
+// per-sample pass instead ends in the tail of its few longest paths (pt_rr: Russian-roulette
+// chains), once per sample.
+//
 // Iterations are host-driven on a plan's first pass (each iteration's queue size comes back
 // to the host); the sizes seen become the plan of later passes, which launch every iteration
 // with no host synchronisation (grid-stride kernels read the queue size on the device).  A
@@ -55,7 +63,7 @@
 namespace rtg {
 
 constexpr int kFrameChunks = (int)((sizeof(FramePT) + 15) / 16);
-constexpr int kPathMaxIter = 1024;           // iterations per pass (the fused kernel beyond)
+constexpr int kPathMaxIter = 4096;           // iterations per pass (the fused kernel beyond)
 #pragma clang diagnostic push
 #pragma clang diagnostic ignored "-Winvalid-offsetof"
 constexpr int kSkipOffset = (int)offsetof(FramePT, skip);
@@ -64,7 +72,7 @@ static_assert(kSkipOffset % 4 == 0, "FramePT::skip alignment");
 
 struct PathBufs {
     // pending ray by path: origin + medium, direction + remaining depth (int bits), RNG key,
-    // throughput + (pend | stack depth << 8) (int bits)
+    // throughput + (pend | stack depth << 8 | sample within the pass << 16) (int bits)
     float4* ro;
     float4* rd;
     unsigned long long* key;
@@ -110,6 +118,45 @@ DEV void frame_store_skip(const PathBufs& B, int lv, int i, int skip) {
     reinterpret_cast<int*>(c)[(kSkipOffset % 16) / 4] = skip;
 }
 
+// the path's sample finished with `value`: its pixel, or the spp accumulation (in sample order)
+DEV void path_pixel(const DevCamera& C, const RenderParams& P, int sample, int first, int last, int pixel, f3 value,
+                    float* __restrict__ hdr, unsigned char* __restrict__ ldrOut, float4* __restrict__ accum) {
+    if (C.spp <= 1 && !P.accum_only) {
+        const size_t idx = 3 * (size_t)pixel;
+        if (hdr) { hdr[idx] = value.x; hdr[idx + 1] = value.y; hdr[idx + 2] = value.z; }
+        if (ldrOut) { ldrOut[idx] = ldr(value.x); ldrOut[idx + 1] = ldr(value.y); ldrOut[idx + 2] = ldr(value.z); }
+    } else {
+        // renderThreadMain multisampling (main.cpp:60-101), samples summed in order
+        const float gw = sample_weight(C.spp, sample, root_key(P.seed, pixel, sample));
+        float4 a = first ? make_float4(0.f, 0.f, 0.f, 0.f) : accum[pixel];
+        a.x += value.x * gw;
+        a.y += value.y * gw;
+        a.z += value.z * gw;
+        a.w += gw;
+        accum[pixel] = a;
+        if (last && !P.accum_only) {
+            const f3 cc = mk(a.x / a.w, a.y / a.w, a.z / a.w);
+            const size_t idx = 3 * (size_t)pixel;
+            if (hdr) { hdr[idx] = cc.x; hdr[idx + 1] = cc.y; hdr[idx + 2] = cc.z; }
+            if (ldrOut) { ldrOut[idx] = ldr(cc.x); ldrOut[idx + 1] = ldr(cc.y); ldrOut[idx + 2] = ldr(cc.z); }
+        }
+    }
+}
+
+// path i's camera ray (GenerateRay, raytracer.cpp:661-699) for `sample`, the k-th of its pass
+template <bool STATS>
+DEV void path_camera(const DevCamera& C, const RenderParams& P, const PathBufs& B, int sample, int k, int pixel,
+                     int i, int max_depth, Cnt<STATS>& cn) {
+    const uint64_t key = root_key(P.seed, pixel, sample);
+    float mbTime;
+    const Ray r = camera_ray(C, pixel % C.width, pixel / C.width, key, mbTime);
+    cn.cam();
+    B.ro[i] = make_float4(r.o.x, r.o.y, r.o.z, 1.0f);
+    B.rd[i] = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(max_depth));
+    B.key[i] = key;
+    B.tp[i] = make_float4(1.0f, 1.0f, 1.0f, __int_as_float(k << 16));
+}
+
 template <bool STATS>
 __global__ __launch_bounds__(256) void k_path_gen(const DevCamera C, const RenderParams P, const PathBufs B,
                                                   const int sample, const int base, const int n, const int max_depth,
@@ -117,15 +164,7 @@ __global__ __launch_bounds__(256) void k_path_gen(const DevCamera C, const Rende
     const int i = blockIdx.x * 256 + threadIdx.x;
     Cnt<STATS> cn;
     if (i < n) {
-        const int pixel = part_pixel(P, C.width, base + i);
-        const uint64_t key = root_key(P.seed, pixel, sample);
-        float mbTime;
-        const Ray r = camera_ray(C, pixel % C.width, pixel / C.width, key, mbTime);
-        cn.cam();
-        B.ro[i] = make_float4(r.o.x, r.o.y, r.o.z, 1.0f);
-        B.rd[i] = make_float4(r.d.x, r.d.y, r.d.z, __int_as_float(max_depth));
-        B.key[i] = key;
-        B.tp[i] = make_float4(1.0f, 1.0f, 1.0f, __int_as_float(0));
+        path_camera<STATS>(C, P, B, sample, 0, part_pixel(P, C.width, base + i), i, max_depth, cn);
         B.act0[i] = i;
         if (i == 0) B.cnt[0] = n;
     }
@@ -155,11 +194,12 @@ __global__ __launch_bounds__(256, RTG_TRACE_WAVES(FEAT)) void k_path_trace(const
 
 // One iteration of render_sample's loop (rtg_mega.hip) after its trace, per active path.
 // SK / FEAT: the scene's shading and traversal features (a superset of them); maxd: the frame
-// levels (the fused kernel's MAXD).
+// levels (the fused kernel's MAXD).  The pass runs samples [sample, sample + count) of each
+// path, the render samples [first, last].
 template <bool STATS, int SK, int FEAT>
 __global__ __launch_bounds__(256, RTG_PATH_STEP_WAVES) void k_path_step(
     const DevScene S, const DevCamera C, const RenderParams P, const PathBufs B, const int it, const int sample,
-    const int first, const int last, const int base, const int maxd, float* __restrict__ hdr,
+    const int first, const int last, const int count, const int base, const int maxd, float* __restrict__ hdr,
     unsigned char* __restrict__ ldrOut, float4* __restrict__ accum, DevCounters* counters) {
     const int* act = (it & 1) ? B.act1 : B.act0;
     int* nact = (it & 1) ? B.act0 : B.act1;
@@ -182,7 +222,8 @@ __global__ __launch_bounds__(256, RTG_PATH_STEP_WAVES) void k_path_step(
             p.tp = mk(t4.x, t4.y, t4.z);
             const int ps = __float_as_int(t4.w);
             p.pend = ps & 255;
-            int sp = ps >> 8;
+            int sp = (ps >> 8) & 255;
+            const int k = ps >> 16;
             Node cur;
             cur.h.t = B.ht[i];
             cur.h.obj = B.hobj[i];
@@ -267,32 +308,18 @@ __global__ __launch_bounds__(256, RTG_PATH_STEP_WAVES) void k_path_step(
                 done = !descended;
             }
             if (done) {
-                const f3 value = v.value;
-                if (C.spp <= 1 && !P.accum_only) {
-                    const size_t idx = 3 * (size_t)pixel;
-                    if (hdr) { hdr[idx] = value.x; hdr[idx + 1] = value.y; hdr[idx + 2] = value.z; }
-                    if (ldrOut) { ldrOut[idx] = ldr(value.x); ldrOut[idx + 1] = ldr(value.y); ldrOut[idx + 2] = ldr(value.z); }
-                } else {
-                    // renderThreadMain multisampling (main.cpp:60-101), samples summed in order
-                    const float gw = sample_weight(C.spp, sample, root_key(P.seed, pixel, sample));
-                    float4 a = first ? make_float4(0.f, 0.f, 0.f, 0.f) : accum[pixel];
-                    a.x += value.x * gw;
-                    a.y += value.y * gw;
-                    a.z += value.z * gw;
-                    a.w += gw;
-                    accum[pixel] = a;
-                    if (last && !P.accum_only) {
-                        const f3 cc = mk(a.x / a.w, a.y / a.w, a.z / a.w);
-                        const size_t idx = 3 * (size_t)pixel;
-                        if (hdr) { hdr[idx] = cc.x; hdr[idx + 1] = cc.y; hdr[idx + 2] = cc.z; }
-                        if (ldrOut) { ldrOut[idx] = ldr(cc.x); ldrOut[idx + 1] = ldr(cc.y); ldrOut[idx + 2] = ldr(cc.z); }
-                    }
+                const int s = sample + k;
+                path_pixel(C, P, s, s == first, s == last, pixel, v.value, hdr, ldrOut, accum);
+                // regeneration: the slot's next sample
+                if (k + 1 < count) {
+                    path_camera<STATS>(C, P, B, s + 1, k + 1, pixel, path, S.max_depth, cn);
+                    cont = true;
                 }
             } else {
                 B.ro[path] = make_float4(p.R.o.x, p.R.o.y, p.R.o.z, p.medium);
                 B.rd[path] = make_float4(p.R.d.x, p.R.d.y, p.R.d.z, __int_as_float(p.depth));
                 B.key[path] = p.key;
-                B.tp[path] = make_float4(p.tp.x, p.tp.y, p.tp.z, __int_as_float(p.pend | (sp << 8)));
+                B.tp[path] = make_float4(p.tp.x, p.tp.y, p.tp.z, __int_as_float(p.pend | (sp << 8) | (k << 16)));
                 cont = true;
             }
         }
@@ -387,31 +414,6 @@ DEV void pending_store(const PathBufs& B, int path, const Pending& p, int sp) {
     B.tp[path] = make_float4(p.tp.x, p.tp.y, p.tp.z, __int_as_float(p.pend | (sp << 8)));
 }
 
-// the path's sample finished with `value`: its pixel, or the spp accumulation (in sample order)
-DEV void path_pixel(const DevCamera& C, const RenderParams& P, int sample, int first, int last, int pixel, f3 value,
-                    float* __restrict__ hdr, unsigned char* __restrict__ ldrOut, float4* __restrict__ accum) {
-    if (C.spp <= 1 && !P.accum_only) {
-        const size_t idx = 3 * (size_t)pixel;
-        if (hdr) { hdr[idx] = value.x; hdr[idx + 1] = value.y; hdr[idx + 2] = value.z; }
-        if (ldrOut) { ldrOut[idx] = ldr(value.x); ldrOut[idx + 1] = ldr(value.y); ldrOut[idx + 2] = ldr(value.z); }
-    } else {
-        // renderThreadMain multisampling (main.cpp:60-101), samples summed in order
-        const float gw = sample_weight(C.spp, sample, root_key(P.seed, pixel, sample));
-        float4 a = first ? make_float4(0.f, 0.f, 0.f, 0.f) : accum[pixel];
-        a.x += value.x * gw;
-        a.y += value.y * gw;
-        a.z += value.z * gw;
-        a.w += gw;
-        accum[pixel] = a;
-        if (last && !P.accum_only) {
-            const f3 cc = mk(a.x / a.w, a.y / a.w, a.z / a.w);
-            const size_t idx = 3 * (size_t)pixel;
-            if (hdr) { hdr[idx] = cc.x; hdr[idx + 1] = cc.y; hdr[idx + 2] = cc.z; }
-            if (ldrOut) { ldrOut[idx] = ldr(cc.x); ldrOut[idx + 1] = ldr(cc.y); ldrOut[idx + 2] = ldr(cc.z); }
-        }
-    }
-}
-
 DEV int* rest_queue(const PathBufs& B, int it) { return (it & 1) ? B.ract1 : B.ract0; }
 DEV int* unwind_count(const PathBufs& B, int it) { return B.rcnt + (kPathMaxIter + 2) + it; }
 
@@ -442,7 +444,7 @@ __global__ __launch_bounds__(256, RTG_PATH_HIT_WAVES) void k_path_hit(const DevS
             p.tp = mk(t4.x, t4.y, t4.z);
             const int ps = __float_as_int(t4.w);
             p.pend = ps & 255;
-            int sp = ps >> 8;
+            int sp = (ps >> 8) & 255;
             Node cur;
             cur.h.t = B.ht[i];
             cur.h.obj = B.hobj[i];
@@ -664,7 +666,8 @@ using GenFn = void (*)(const DevCamera, const RenderParams, const PathBufs, cons
                        DevCounters*);
 using TraceFn = void (*)(const DevScene, const PathBufs, const int, DevCounters*);
 using StepFn = void (*)(const DevScene, const DevCamera, const RenderParams, const PathBufs, const int, const int,
-                        const int, const int, const int, const int, float*, unsigned char*, float4*, DevCounters*);
+                        const int, const int, const int, const int, const int, float*, unsigned char*, float4*,
+                        DevCounters*);
 using HitFn = void (*)(const DevScene, const DevCamera, const RenderParams, const PathBufs, const int, const int,
                       const int, DevCounters*);
 using RestFn = void (*)(const DevScene, const DevCamera, const PathBufs, const int, DevCounters*);
@@ -680,11 +683,12 @@ struct PathKernels {
     bool split;
 };
 
-// One sample pass over paths [base, base + n) of the frame part.  plan == nullptr:
-// host-driven (one synchronisation per iteration; `seen` receives the queue sizes);
-// otherwise the plan's iterations, no synchronisation.
+// One pass over paths [base, base + n) of the frame part: samples [s, s + count) of each path
+// (count > 1: regeneration, single step kernel only).  plan == nullptr: host-driven (one
+// synchronisation per iteration; `seen` receives the queue sizes); otherwise the plan's
+// iterations, no synchronisation.
 static hipError_t path_pass(PathState& T, const PathKernels& K, const DevScene& S, const DevCamera& C,
-                            const RenderParams& P, int maxd, int s, int base, int n, bool first, bool last, float* hdr,
+                            const RenderParams& P, int maxd, int s, int count, int base, int n, float* hdr,
                             unsigned char* l, float4* accum, DevCounters* cnt, hipStream_t st, hipEvent_t* ev,
                             const PathState* plan, std::vector<int>& seen, std::vector<int>& rseen) {
     hipError_t e;
@@ -698,15 +702,15 @@ static hipError_t path_pass(PathState& T, const PathKernels& K, const DevScene& 
         const int g = grid_for(paths);
         hipLaunchKernelGGL(K.trace, dim3(g), dim3(256), 0, st, S, B, it, cnt);
         if (!K.split) {
-            hipLaunchKernelGGL(K.step, dim3(g), dim3(256), 0, st, S, C, P, B, it, s, (int)first, (int)last, base, maxd,
-                               hdr, l, accum, cnt);
+            hipLaunchKernelGGL(K.step, dim3(g), dim3(256), 0, st, S, C, P, B, it, s, P.sample_begin,
+                               P.sample_begin + P.sample_count - 1, count, base, maxd, hdr, l, accum, cnt);
             return;
         }
         const int g2 = grid_for(std::min<long long>(n, paths + rpaths));
         hipLaunchKernelGGL(K.hit, dim3(g), dim3(256), 0, st, S, C, P, B, it, base, maxd, cnt);
         hipLaunchKernelGGL(K.rest, dim3(g2), dim3(256), 0, st, S, C, B, it, cnt);
-        hipLaunchKernelGGL(K.unwind, dim3(g2), dim3(256), 0, st, S, C, P, B, it, s, (int)first, (int)last, base, hdr, l,
-                           accum, cnt);
+        hipLaunchKernelGGL(K.unwind, dim3(g2), dim3(256), 0, st, S, C, P, B, it, s, (int)(s == P.sample_begin),
+                           (int)(s == P.sample_begin + P.sample_count - 1), base, hdr, l, accum, cnt);
     };
     if (plan) {
         const int D = (int)plan->plan.size();
@@ -739,6 +743,14 @@ static hipError_t path_pass(PathState& T, const PathKernels& K, const DevScene& 
 // RTG_PATH_SYNC=1: every pass host-driven (A/B)
 static bool path_sync_only() { return std::getenv("RTG_PATH_SYNC") != nullptr; }
 
+// samples per pass: all of the render's with regeneration (RTG_PATH_REGEN=0: one; the split step
+// has no regeneration), at most 64 so a pass's iterations stay well inside kPathMaxIter
+static int path_pass_samples(const PathKernels& K, const RenderParams& P) {
+    const char* v = std::getenv("RTG_PATH_REGEN");
+    if (K.split || (v && std::strcmp(v, "0") == 0)) return 1;
+    return std::max(1, std::min(P.sample_count, 64));
+}
+
 static hipError_t path_run(PathState& T, const PathKernels& K, bool stats, const DevScene& S, const DevCamera& C,
                            const RenderParams& P, int maxd, float* hdr, unsigned char* l, float4* accum,
                            DevCounters* cnt, hipStream_t st, hipEvent_t* ev) {
@@ -756,10 +768,11 @@ static hipError_t path_run(PathState& T, const PathKernels& K, bool stats, const
     mem_free += T.cap * (size_t)T.levels * kFrameChunks * 16;        // the buffers held now are reusable
     const long long budget = std::max<long long>(1 << 16, (long long)(mem_free / 2 / per_path));
     const int chunk = (int)std::min<long long>(std::min(npix, 1 << 20), budget);
+    const int per_pass = path_pass_samples(K, P);
     if ((e = ensure_paths(T, (size_t)chunk, maxd)) != hipSuccess) return e;
     const std::vector<long long> key = {P.row_begin, P.row_end, P.part_index, P.part_count, C.width, C.height,
                                         (long long)(size_t)S.objects, S.max_depth, (long long)chunk, maxd,
-                                        (long long)camera_hash(C), (long long)K.split};
+                                        (long long)camera_hash(C), (long long)K.split, (long long)per_pass};
     for (int attempt = 0; attempt < 2; ++attempt) {
         // attempt 0: planned passes when this frame part has a plan (the first pass otherwise
         // host-driven, planning the rest); attempt 1 (a plan was too short): host-driven.
@@ -771,11 +784,12 @@ static hipError_t path_run(PathState& T, const PathKernels& K, bool stats, const
         std::vector<int> seen_max, rseen_max;
         for (int base = 0; base < npix; base += chunk) {
             const int n = std::min(chunk, npix - base);
-            for (int s = P.sample_begin; s < P.sample_begin + P.sample_count; ++s) {
-                const bool first = s == P.sample_begin, last = s == P.sample_begin + P.sample_count - 1;
-                hipEvent_t* pev = (last && base + chunk >= npix) ? ev : nullptr;
+            const int s_end = P.sample_begin + P.sample_count;
+            for (int s = P.sample_begin; s < s_end; s += per_pass) {
+                const int count = std::min(per_pass, s_end - s);
+                hipEvent_t* pev = (s + count == s_end && base + chunk >= npix) ? ev : nullptr;
                 std::vector<int> seen, rseen;
-                e = path_pass(T, K, S, C, P, maxd, s, base, n, first, last, hdr, l, accum, cnt, st, pev,
+                e = path_pass(T, K, S, C, P, maxd, s, count, base, n, hdr, l, accum, cnt, st, pev,
                               planned ? &T : nullptr, seen, rseen);
                 if (e != hipSuccess) return e;
                 if (planned) {

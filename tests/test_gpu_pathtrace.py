@@ -123,16 +123,24 @@ def _bits(a):
     return a.view(np.uint32)
 
 
-@pytest.mark.parametrize("split", ["1", "0"])
+# step kernel modes: split by node kind, one kernel with path regeneration (the default), one
+# kernel with a pass per sample
+MODES = {"split": {"RTG_PATH_SPLIT": "1"}, "regen": {"RTG_PATH_SPLIT": "0"},
+         "noregen": {"RTG_PATH_SPLIT": "0", "RTG_PATH_REGEN": "0"}}
+
+
+@pytest.mark.parametrize("mode", list(MODES))
 @pytest.mark.parametrize("name", PT_ONLY)
 @pytest.mark.parametrize("spp", [1, 4])
-def test_path_wavefront_equals_fused(name, spp, split, tmp_path, monkeypatch):
+def test_path_wavefront_equals_fused(name, spp, mode, tmp_path, monkeypatch):
     """The wavefront path tracer (rtg_path.hip, forced with RTG_RENDER_TREE) gives the fused
     kernel's image bit for bit: the same node steps (rtg_node.hpp) on the same RNG keys -- with
-    the step as one kernel (the default) and split by node kind (RTG_PATH_SPLIT=1: k_path_hit /
-    k_path_rest / k_path_unwind).  The first render plans its later passes from its first; the
-    second runs planned throughout."""
-    monkeypatch.setenv("RTG_PATH_SPLIT", split)
+    the step as one kernel (the default), with or without path regeneration (a finished sample's
+    slot starting the pixel's next sample inside the pass), and split by node kind
+    (RTG_PATH_SPLIT=1: k_path_hit / k_path_rest / k_path_unwind).  The first render plans its
+    later passes from its first; the second runs planned throughout."""
+    for k, v in MODES[mode].items():
+        monkeypatch.setenv(k, v)
     hs = _scene(tmp_path, name, spp)
     ds = rtgpu.DeviceScene(hs, 0)
     b, lb = ds.render(0, seed=11, flags=rtgpu.RTG_RENDER_FUSED)
@@ -181,3 +189,30 @@ def test_path_wavefront_stats_and_bands(name, split, tmp_path, monkeypatch):
         band, _ = ds.render(0, rows=(t * 16, t * 16 + 16), seed=17, flags=rtgpu.RTG_RENDER_TREE)
         out[t * 16:t * 16 + 16] = band[t * 16:t * 16 + 16]
     assert np.array_equal(_bits(out), _bits(full))
+
+
+@pytest.mark.parametrize("regen", ["1", "0"])
+def test_path_regeneration_passes_and_sample_ranges(regen, tmp_path, monkeypatch):
+    """Regeneration across pass boundaries (70 spp: passes of 64 and 6 samples per slot) and
+    with sample ranges accumulated separately (RTG_RENDER_ACCUM_ONLY, samples [0, 3) and
+    [3, 7)): the fused kernel's bits, so each pixel's samples are still summed in sample order."""
+    torch = pytest.importorskip("torch")
+    monkeypatch.setenv("RTG_PATH_SPLIT", "0")
+    monkeypatch.setenv("RTG_PATH_REGEN", regen)
+    hs = _scene(tmp_path, "pt_rr", 70)
+    ds = rtgpu.DeviceScene(hs, 0)
+    b, lb = ds.render(0, seed=23, flags=rtgpu.RTG_RENDER_FUSED)
+    for _ in range(2):
+        a, la = ds.render(0, seed=23, flags=rtgpu.RTG_RENDER_TREE)
+        assert np.array_equal(_bits(a), _bits(b)), ob.compare(a, b)
+        assert np.array_equal(la, lb)
+    h, w = a.shape[:2]
+    for s0, n in ((0, 3), (3, 4)):
+        accs = []
+        for flags in (rtgpu.RTG_RENDER_FUSED, rtgpu.RTG_RENDER_TREE):
+            acc = torch.zeros((h, w, 4), dtype=torch.float32, device="cuda:0")
+            ds.render_device(0, 0, 0, accum_ptr=acc.data_ptr(), flags=flags | rtgpu.RTG_RENDER_ACCUM_ONLY,
+                             sample_begin=s0, sample_count=n, seed=23)
+            torch.cuda.synchronize()
+            accs.append(acc.cpu().numpy())
+        assert np.array_equal(_bits(accs[0]), _bits(accs[1]))

@@ -1,5 +1,5 @@
 """Path tracing: device-resident frame time of the fused kernel vs the wavefront path tracer
-(rtg_path.hip, RTG_RENDER_TREE), per scene at size^2 x spp.  Rays per frame from a counted
+(rtg_path.hip, RTG_RENDER_TREE; with path regeneration and with a pass per sample), per scene at size^2 x spp.  Rays per frame from a counted
 fused render.  One JSON line per (scene, path).
 
     python tools/diag_ptwave.py [size] [spp] [scene ...]
@@ -40,7 +40,9 @@ for name in names:
     s = ds.stats()
     rays = s["camera_rays"] + s["secondary_rays"] + s["shadow_rays"]
     ref = None
-    for path, flags in (("fused", rtgpu.RTG_RENDER_FUSED), ("wavefront", rtgpu.RTG_RENDER_TREE)):
+    for path, flags, regen in (("fused", rtgpu.RTG_RENDER_FUSED, "1"), ("wavefront", rtgpu.RTG_RENDER_TREE, "1"),
+                               ("wavefront_noregen", rtgpu.RTG_RENDER_TREE, "0")):
+        os.environ["RTG_PATH_REGEN"] = regen    # read per render (rtg_path.hip path_pass_samples)
         for _ in range(2):
             ds.render_device(hdr.data_ptr(), ldr.data_ptr(), st, flags=flags)
         torch.cuda.synchronize()
