@@ -33,13 +33,17 @@
 // Every path sits in one queue at a time (trace T, rest R, unwind U); its RestArgs (112 B) or
 // ChildVal (32 B) wait in HBM by path index.
 //
-// Path regeneration (the default for the single step kernel; RTG_PATH_REGEN=0: one pass per
-// sample): a pass covers all of the render's samples.  Path slot i is pixel i of the chunk; when
+// Path regeneration (single step kernel, cameras with Russian roulette; RTG_PATH_REGEN=1 / 0
+// forces it on / off): a pass covers all of the render's samples.  Path slot i is pixel i of the chunk; when
 // its sample finishes, the step kernel accumulates it and starts the slot's next sample (its
 // camera ray) in the same iteration, so the queue stays full until the last samples and each
 // pixel's samples are still summed in sample order (one slot does them one after another).  A
 // per-sample pass instead ends in the tail of its few longest paths (pt_rr: Russian-roulette
-// chains), once per sample.
+// chains), once per sample.  Without Russian roulette there is no such tail, and mixing the
+// samples' stages in one queue costs more than it saves: a wave whose lanes sit at different
+// depths pays for every lane's unwinding of its stack each iteration (1024^2 x 16 spp: pt_rr
+// 1 048 -> 1 405 Mrays/s with regeneration, pt_cornell 2 642 -> 1 725, pt_nee 3 629 -> 1 871;
+// profiles/r05p_ptwave_regen.txt).
 //
 // Iterations are host-driven on a plan's first pass (each iteration's queue size comes back
 // to the host); the sizes seen become the plan of later passes, which launch every iteration
@@ -743,11 +747,13 @@ static hipError_t path_pass(PathState& T, const PathKernels& K, const DevScene& 
 // RTG_PATH_SYNC=1: every pass host-driven (A/B)
 static bool path_sync_only() { return std::getenv("RTG_PATH_SYNC") != nullptr; }
 
-// samples per pass: all of the render's with regeneration (RTG_PATH_REGEN=0: one; the split step
-// has no regeneration), at most 64 so a pass's iterations stay well inside kPathMaxIter
-static int path_pass_samples(const PathKernels& K, const RenderParams& P) {
+// samples per pass: all of the render's with regeneration (Russian roulette, or
+// RTG_PATH_REGEN=1; the split step has none), at most 64 so a pass's iterations stay well inside
+// kPathMaxIter; one otherwise
+static int path_pass_samples(const PathKernels& K, const DevCamera& C, const RenderParams& P) {
     const char* v = std::getenv("RTG_PATH_REGEN");
-    if (K.split || (v && std::strcmp(v, "0") == 0)) return 1;
+    const bool regen = v ? std::strcmp(v, "0") != 0 : C.russian_roulette != 0;
+    if (K.split || !regen) return 1;
     return std::max(1, std::min(P.sample_count, 64));
 }
 
@@ -768,7 +774,7 @@ static hipError_t path_run(PathState& T, const PathKernels& K, bool stats, const
     mem_free += T.cap * (size_t)T.levels * kFrameChunks * 16;        // the buffers held now are reusable
     const long long budget = std::max<long long>(1 << 16, (long long)(mem_free / 2 / per_path));
     const int chunk = (int)std::min<long long>(std::min(npix, 1 << 20), budget);
-    const int per_pass = path_pass_samples(K, P);
+    const int per_pass = path_pass_samples(K, C, P);
     if ((e = ensure_paths(T, (size_t)chunk, maxd)) != hipSuccess) return e;
     const std::vector<long long> key = {P.row_begin, P.row_end, P.part_index, P.part_count, C.width, C.height,
                                         (long long)(size_t)S.objects, S.max_depth, (long long)chunk, maxd,

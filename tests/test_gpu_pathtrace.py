@@ -123,9 +123,10 @@ def _bits(a):
     return a.view(np.uint32)
 
 
-# step kernel modes: split by node kind, one kernel with path regeneration (the default), one
-# kernel with a pass per sample
-MODES = {"split": {"RTG_PATH_SPLIT": "1"}, "regen": {"RTG_PATH_SPLIT": "0"},
+# step kernel modes: split by node kind; one kernel as chosen by the camera (regeneration with
+# Russian roulette), with path regeneration forced, and with a pass per sample
+MODES = {"split": {"RTG_PATH_SPLIT": "1"}, "default": {"RTG_PATH_SPLIT": "0"},
+         "regen": {"RTG_PATH_SPLIT": "0", "RTG_PATH_REGEN": "1"},
          "noregen": {"RTG_PATH_SPLIT": "0", "RTG_PATH_REGEN": "0"}}
 
 
@@ -136,7 +137,8 @@ def test_path_wavefront_equals_fused(name, spp, mode, tmp_path, monkeypatch):
     """The wavefront path tracer (rtg_path.hip, forced with RTG_RENDER_TREE) gives the fused
     kernel's image bit for bit: the same node steps (rtg_node.hpp) on the same RNG keys -- with
     the step as one kernel (the default), with or without path regeneration (a finished sample's
-    slot starting the pixel's next sample inside the pass), and split by node kind
+    slot starting the pixel's next sample inside the pass; by default with Russian roulette), and
+    split by node kind
     (RTG_PATH_SPLIT=1: k_path_hit / k_path_rest / k_path_unwind).  The first render plans its
     later passes from its first; the second runs planned throughout."""
     for k, v in MODES[mode].items():

@@ -40,7 +40,7 @@ for name in names:
     s = ds.stats()
     rays = s["camera_rays"] + s["secondary_rays"] + s["shadow_rays"]
     ref = None
-    for path, flags, regen in (("fused", rtgpu.RTG_RENDER_FUSED, "1"), ("wavefront", rtgpu.RTG_RENDER_TREE, "1"),
+    for path, flags, regen in (("fused", rtgpu.RTG_RENDER_FUSED, "1"), ("wavefront_regen", rtgpu.RTG_RENDER_TREE, "1"),
                                ("wavefront_noregen", rtgpu.RTG_RENDER_TREE, "0")):
         os.environ["RTG_PATH_REGEN"] = regen    # read per render (rtg_path.hip path_pass_samples)
         for _ in range(2):
