@@ -44,8 +44,10 @@
 #ifndef RTG_BIGLEAF_LEAN
 #define RTG_BIGLEAF_LEAN 0
 #endif
+// instance scenes' walks (camera and any-hit) at six waves: C4 2 944 -> 3 150 Mrays/s, C3-ton
+// 5 450 -> 5 600 (profiles/r05n_pairs_inst6_deferany_ab.txt)
 #ifndef RTG_INST_WAVES
-#define RTG_INST_WAVES 5
+#define RTG_INST_WAVES 6
 #endif
 #define RTG_TRACE_WAVES(FEAT) \
     (((FEAT) & ~(FEAT_SPHERE | (RTG_BIGLEAF_LEAN ? FEAT_BIGLEAF : 0))) \
@@ -829,9 +831,11 @@ DEV const T* rec_at(const T* base, int i) {
 #ifndef RTG_PK_LEAN
 #define RTG_PK_LEAN 1
 #endif
-// the camera packet walk's slab distances as three packed pairs of the node record (box_pass_rec)
+// the camera packet walk's slab distances as three packed pairs of the node record (box_pass_rec):
+// six fewer VALU per node step in the listing, but k_frame 0.289 -> 0.300 ms on the GPU
+// (profiles/r05n_pairs_inst6_deferany_ab.txt), so off
 #ifndef RTG_PK_PAIRS
-#define RTG_PK_PAIRS 1
+#define RTG_PK_PAIRS 0
 #endif
 // (A/B parts of the lean packet walks: the any-hit walk, the closest-hit walk's face test)
 #ifndef RTG_PK_LEAN_ANY

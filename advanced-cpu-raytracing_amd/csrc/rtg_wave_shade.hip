@@ -57,8 +57,11 @@ bool defer_leaves() {
     return !v || std::strcmp(v, "0") != 0;
 }
 
-// RTG_DEFER_ANY: shadow rays of large-leaf scenes -- 0 the cooperative reference walk, 1 the
-// deferring any-hit walk, unset: chosen per pass on the device (GATE, rtg_common.hpp)
+// RTG_DEFER_ANY: shadow rays of large-leaf scenes -- 0 the cooperative reference walk, 1 or
+// unset the deferring any-hit walk, 2 chosen per pass on the device (GATE, rtg_common.hpp).
+// Round 5, with the lean any-hit walk, the deferring walk wins on every large-leaf config
+// (C3 5 527 -> 5 872, C3-ton 5 517 -> 5 602, C4 3 165 -> 3 164 Mrays/s against the per-pass
+// choice; profiles/r05q_deferany_ab.txt)
 // RTG_DEFER_ANY_GATE=g: the deferring walk when the camera pass reached large leaves with at
 // least pixels / g lanes (default 50: 2 %)
 int defer_any_gate() {
@@ -68,7 +71,7 @@ int defer_any_gate() {
 
 int defer_any_leaves() {
     const char* v = std::getenv("RTG_DEFER_ANY");
-    return !v ? 2 : std::strcmp(v, "0") == 0 ? 0 : 1;
+    return !v ? 1 : std::strcmp(v, "0") == 0 ? 0 : std::strcmp(v, "2") == 0 ? 2 : 1;
 }
 
 // The fused layout's two kernels as one (k_shade<..., FRAME>, default since round 5;

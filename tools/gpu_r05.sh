@@ -90,9 +90,6 @@ for s in "${steps[@]}"; do
         [ "$setting" != base ] && IFS=, read -ra envs <<< "$setting"
         run envbench_$name 300 env "${envs[@]}" python bench.py --no-sweep --no-cpu-baseline $extra
       done ;;
-    pcsamp)
-      # PC sampling of the headline's kernels (host-trap, time-based): where the waves' time goes
-      run pcsamp 240 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method host_trap --pc-sampling-unit time --pc-sampling-interval ${PCS_INTERVAL:-1} -f csv -d $out/pcs -o run -- python bench.py --steps 20 --warmup 2 --inflight 1 --no-cpu-baseline --no-sweep --no-extras $extra ;;
     envcfg:*)
       # bench.py --config <c> (no extras) once per setting in $ENV_AB, twice interleaved
       c=${s#envcfg:}
