@@ -570,6 +570,10 @@ DEV uint64_t wave_min_key(uint64_t key, uint64_t em) {
 
 // Sequential form: each lane tests its leaves' faces in order inside the walk (scenes
 // whose leaves are all small: the lean kernels).
+// (Loading node i + 1 -- where a passing inner node descends -- before node i is tested measured
+// slower too: C5 1 712 -> 1 205 Mrays/s at eight waves (spills), 1 435 at seven (1 630 without
+// the prefetch), C2 12 700 -> 12 100; the walks' memory traffic, not the chain's latency alone,
+// bounds them (profiles/r05r_seq_prefetch_ab.txt).)
 // (A "while-while" form -- an inner loop over boxes until the lane stands on a passing leaf,
 // the faces after it, Aila & Laine HPG 2009 -- measured slower: k_primary 0.238 -> 0.309 ms,
 // C5 1471 -> 954 Mrays/s; profiles/r03l_*.  The lanes that reach a leaf early idle in the box
