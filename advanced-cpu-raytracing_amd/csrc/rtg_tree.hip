@@ -630,6 +630,11 @@ static int tree_shadow_fast() {
     return v ? std::atoi(v) : 0;
 }
 
+// (Round 5 measured an XCD-aware block order for the levels' trace / shade / shadow grids --
+// runs of 2^c consecutive blocks per XCD dealt round-robin, so a block's rays, hits and shadow
+// queue stay in one XCD's L2: C5 1 726 / 1 722 / 1 718 / 1 721 Mrays/s for block order and
+// c = 4 / 2 / 6; the levels' misses are not a matter of which XCD walks which rays --
+// profiles/r05s_tree_xcd_ab.txt.)
 // RTG_TREE_CLOSEST=1 (A/B): the levels not on the packet walk take the checked closest-hit walk
 // of the any-hit tree per lane
 static bool tree_closest() { return std::getenv("RTG_TREE_CLOSEST") != nullptr; }
