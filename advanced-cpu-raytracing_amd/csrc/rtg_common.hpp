@@ -1212,7 +1212,13 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
 #ifndef RTG_WIDE_WAVES_PLAIN
 #define RTG_WIDE_WAVES_PLAIN (RTG_ANY_PACKET ? 7 : 5)
 #endif
-#define RTG_WIDE_WAVES(FEAT) (((FEAT) & FEAT_INSTANCE) ? RTG_INST_WAVES : RTG_WIDE_WAVES_PLAIN)
+// instance scenes' any-hit walks (their own knob): the deferring shadow walk spills 124 B per
+// lane at six waves, 76 at five and none at four (118 VGPRs), and six is the fastest -- C4
+// 3 163 / 3 093 / 2 963 Mrays/s (profiles/r05w_c4_any_waves_ab.txt): occupancy over spill traffic
+#ifndef RTG_INST_ANY_WAVES
+#define RTG_INST_ANY_WAVES 6
+#endif
+#define RTG_WIDE_WAVES(FEAT) (((FEAT) & FEAT_INSTANCE) ? RTG_INST_ANY_WAVES : RTG_WIDE_WAVES_PLAIN)
 
 
 // Conservative slab test: accepts every box the exact test (box_hit) accepts at minT.  The
