@@ -85,7 +85,7 @@ for s in "${steps[@]}"; do
       # the headline bench (with gather / host-frame / parts / ordered extras) once per setting in
       # $ENV_AB ("base" or NAME=VALUE[,NAME=VALUE])
       for setting in $ENV_AB; do
-        name=${setting//[=,]/_}
+        name=$(echo "$setting" | tr "=,/" "___")
         envs=()
         [ "$setting" != base ] && IFS=, read -ra envs <<< "$setting"
         run envbench_$name 300 env "${envs[@]}" python bench.py --no-sweep --no-cpu-baseline $extra
@@ -95,7 +95,7 @@ for s in "${steps[@]}"; do
       c=${s#envcfg:}
       for rep in 1 2; do
         for setting in $ENV_AB; do
-          name=${setting//[=,]/_}
+          name=$(echo "$setting" | tr "=,/" "___")
           envs=()
           [ "$setting" != base ] && IFS=, read -ra envs <<< "$setting"
           run envcfg_${c}_${name}_$rep 400 env "${envs[@]}" python bench.py --config $c --no-extras --no-cpu-baseline --steps ${CFG_STEPS:-10} $extra
@@ -105,7 +105,7 @@ for s in "${steps[@]}"; do
       # tools/<name>.py once per setting in $ENV_AB
       t=${s#envpy:}
       for setting in $ENV_AB; do
-        name=${setting//[=,]/_}
+        name=$(echo "$setting" | tr "=,/" "___")
         envs=()
         [ "$setting" != base ] && IFS=, read -ra envs <<< "$setting"
         run ${t}_$name 300 env "${envs[@]}" python -u tools/$t.py
