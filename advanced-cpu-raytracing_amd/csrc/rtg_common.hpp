@@ -835,6 +835,10 @@ DEV const T* rec_at(const T* base, int i) {
 #ifndef RTG_PK_LEAN
 #define RTG_PK_LEAN 1
 #endif
+// (Round 5 also started node i + 1's record -- where a passing inner node descends -- while node
+// i was tested, waiting for it at the end of the step: k_frame 0.2878 -> 0.2912 ms, C3-ton +1 %,
+// C4 -0.7 %; profiles/r05ac_pk_prefetch_ab.txt.  The scalar loads' latency is already covered by
+// the other waves.)
 // the camera packet walk's slab distances as three packed pairs of the node record (box_pass_rec):
 // six fewer VALU per node step in the listing, but k_frame 0.289 -> 0.300 ms on the GPU
 // (profiles/r05n_pairs_inst6_deferany_ab.txt), so off
