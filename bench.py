@@ -270,6 +270,9 @@ def pmc_summary(kernel, K, world, share=1.0, workload="headline"):
         # the timed kernels (the counting pass runs the <true> = STATS instantiations)
         v = (rec["kernels"].get("stage:" + kernel) or rec["kernels"].get(kernel + "<false>") or
              rec["kernels"].get(kernel))
+        if v is None:     # a kernel whose first template argument is not STATS (C2's k_render<FEAT>)
+            named = [n for n in rec["kernels"] if n.startswith(kernel + "<") and n != kernel + "<true>"]
+            v = rec["kernels"][named[0]] if len(named) == 1 else None
         if v and "traffic_bytes" in v:
             best = dict(v, source=os.path.basename(f))
             best.setdefault("l2_request_bytes", 128 * v["l2_requests"] if "l2_requests" in v else None)
