@@ -1055,6 +1055,9 @@ DEV bool walk_bvh_packet(const DevScene& S, int begin, int end, const Ray& r, fl
     return hit;
 }
 
+#ifndef RTG_SPHERE_LAUNDER
+#define RTG_SPHERE_LAUNDER 1
+#endif
 // Sphere::Intersect (sphere.cpp:13-78): root selection and acceptance; lo/ld local ray.
 DEV bool sphere_t(const DevObject& ob, const Ray& lr, float minT, float& tout) {
     const f3 center = mk(ob.center[0], ob.center[1], ob.center[2]);
@@ -1142,7 +1145,16 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
         c.obj();
         if ((FEAT & FEAT_SPHERE) && ob.kind == OBJ_SPHERE) {
             c.sph();
-            Ray lr = trav_ray(ob, r, mbTime);
+            // the ray laundered here, so the compiler does not hoist trav_ray's double
+            // conversions of it out of the object loop (twelve VGPRs live through every mesh
+            // walk, spilled at eight waves): C5's k_tree_trace / k_shadow 28 B of scratch -> 0,
+            // C5 1 715 -> 1 784 Mrays/s (profiles/r05ag_sphere_launder_ab.txt); the fused
+            // kernels (rtg_mega*.hip) set RTG_SPHERE_LAUNDER 0 -- C2 loses 6 % with it
+            Ray rs = r;
+#if RTG_SPHERE_LAUNDER
+            asm volatile("" : "+v"(rs.o.x), "+v"(rs.o.y), "+v"(rs.o.z), "+v"(rs.d.x), "+v"(rs.d.y), "+v"(rs.d.z));
+#endif
+            Ray lr = trav_ray(ob, rs, mbTime);
             float t;
             if (sphere_t(ob, lr, h.t, t)) {
                 h.t = t; h.obj = k; h.face = -1; h.o = r.o;
