@@ -1055,8 +1055,8 @@ DEV bool walk_bvh_packet(const DevScene& S, int begin, int end, const Ray& r, fl
     return hit;
 }
 
-#ifndef RTG_SPHERE_LAUNDER
-#define RTG_SPHERE_LAUNDER 1
+#ifndef RTG_XFORM_LAUNDER
+#define RTG_XFORM_LAUNDER 1
 #endif
 // Sphere::Intersect (sphere.cpp:13-78): root selection and acceptance; lo/ld local ray.
 DEV bool sphere_t(const DevObject& ob, const Ray& lr, float minT, float& tout) {
@@ -1089,7 +1089,16 @@ DEV Ray local_ray(const DevObject& ob, const Ray& r, float mbTime) {
 // Traversal-only variant: an exact identity transform changes at most the sign of a zero
 // component (1*x + 0*y + ...), which no box / triangle / sphere decision or t value
 // depends on, so it is skipped.  Shading (surface()) always applies the full transform.
-DEV Ray trav_ray(const DevObject& ob, const Ray& r, float mbTime) {
+DEV Ray trav_ray(const DevObject& ob, const Ray& r0, float mbTime) {
+    // the ray laundered, so the compiler does not hoist the transform's double conversions of
+    // it out of the caller's object loop (twelve VGPRs live through every mesh walk, spilled at
+    // eight waves): C5's k_tree_trace / k_shadow 28 B of scratch -> 0, C5 1 715 -> 1 787 Mrays/s
+    // (profiles/r05ag_sphere_launder_ab.txt); the fused kernels (rtg_mega*.hip) set
+    // RTG_XFORM_LAUNDER 0 -- C2 loses 6 % with it
+    Ray r = r0;
+#if RTG_XFORM_LAUNDER
+    asm volatile("" : "+v"(r.o.x), "+v"(r.o.y), "+v"(r.o.z), "+v"(r.d.x), "+v"(r.d.y), "+v"(r.d.z));
+#endif
     if (!(ob.flags & OBJF_IDENTITY)) return local_ray(ob, r, mbTime);
     Ray lr = r;
     if (ob.flags & OBJF_MOTION_BLUR) lr.o = add(lr.o, muls(ld3(ob.mbv), mbTime));
@@ -1145,16 +1154,7 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
         c.obj();
         if ((FEAT & FEAT_SPHERE) && ob.kind == OBJ_SPHERE) {
             c.sph();
-            // the ray laundered here, so the compiler does not hoist trav_ray's double
-            // conversions of it out of the object loop (twelve VGPRs live through every mesh
-            // walk, spilled at eight waves): C5's k_tree_trace / k_shadow 28 B of scratch -> 0,
-            // C5 1 715 -> 1 784 Mrays/s (profiles/r05ag_sphere_launder_ab.txt); the fused
-            // kernels (rtg_mega*.hip) set RTG_SPHERE_LAUNDER 0 -- C2 loses 6 % with it
-            Ray rs = r;
-#if RTG_SPHERE_LAUNDER
-            asm volatile("" : "+v"(rs.o.x), "+v"(rs.o.y), "+v"(rs.o.z), "+v"(rs.d.x), "+v"(rs.d.y), "+v"(rs.d.z));
-#endif
-            Ray lr = trav_ray(ob, rs, mbTime);
+            Ray lr = trav_ray(ob, r, mbTime);
             float t;
             if (sphere_t(ob, lr, h.t, t)) {
                 h.t = t; h.obj = k; h.face = -1; h.o = r.o;

@@ -4,9 +4,9 @@
 // (raytracer.cpp:135-191) unrolled onto an explicit per-thread stack.  Used for path
 // tracing, motion blur and small ray-tree frames; other scenes take the wavefront
 // pipelines (rtg_wave.hip, rtg_tree.hip).
-// the fused kernels keep the ray unlaundered in trace()'s sphere branch (rtg_common.hpp:
-// laundering it there costs C2 6 %, profiles/r05ag_sphere_launder_ab.txt)
-#define RTG_SPHERE_LAUNDER 0
+// the fused kernels keep trav_ray's ray unlaundered (rtg_common.hpp: laundering it costs C2
+// 6 %, profiles/r05ag_sphere_launder_ab.txt)
+#define RTG_XFORM_LAUNDER 0
 #include "rtg_common.hpp"
 #include "rtg_kernels.hpp"
 #include "rtg_mega_impl.hpp"

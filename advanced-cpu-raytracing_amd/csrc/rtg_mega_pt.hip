@@ -6,9 +6,9 @@
 // drop code the scene cannot reach.
 #include <cstdlib>
 
-// the fused kernels keep the ray unlaundered in trace()'s sphere branch (rtg_common.hpp:
-// laundering it there costs C2 6 %, profiles/r05ag_sphere_launder_ab.txt)
-#define RTG_SPHERE_LAUNDER 0
+// the fused kernels keep trav_ray's ray unlaundered (rtg_common.hpp: laundering it costs C2
+// 6 %, profiles/r05ag_sphere_launder_ab.txt)
+#define RTG_XFORM_LAUNDER 0
 #include "rtg_kernels.hpp"
 #include "rtg_mega_impl.hpp"
 
