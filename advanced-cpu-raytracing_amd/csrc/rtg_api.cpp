@@ -84,13 +84,14 @@ void f4(float* dst, const rtg_float3& v, float w = 0.f) { dst[0] = v.x; dst[1] =
 struct WaveWork {
     size_t pixels = 0, tiles = 0;
     int slots = 0;
+    bool col = false;                 // with the multi-sample colour buffer
     void* mem = nullptr;
     void* dq = nullptr;               // deferred-leaf queue + per-pixel hit keys (ensure_defer)
     size_t dq_nq = 0;                 // its shadow-state entries
     size_t dq_pixels = 0;             // the pixel count its hit-key array (and so its layout) was sized for
     rtg::WaveBufs W{};
 };
-constexpr int kWorkCtx = 3;
+constexpr int kWorkCtx = 1;
 struct TileMap {
     int tx, ty, mode;
     DevBuf<int> map;
@@ -121,10 +122,8 @@ struct rtg_scene {
     DevBuf<rtg::DevDirLight> dir_lights;
     DevBuf<rtg::DevSpotLight> spot_lights;
     DevBuf<rtg::DevCounters> counters;
-    DevBuf<rtg::WNode> wnodes;
     DevBuf<rtg::WNode> anodes;
     DevBuf<float4> ahtris;
-    DevBuf<int2> node_up;
     DevBuf<int> face_leaf;
     DevBuf<int> guard;                // RTG_GUARD builds: index-violation bits
     DevBuf<int> perm;
@@ -137,8 +136,7 @@ struct rtg_scene {
     int feat = rtg::FEAT_ALL;         // scene feature bits (traversal specialisation)
     int num_slots = 0;                // lights per pixel (wavefront light slots)
     int shade_sk = rtg::SK_ALL;       // shading features (k_shade variant, rtg_common.hpp SK_*)
-    // wavefront buffers, grown on demand: work context 0 for every render, 1 and 2 for the
-    // row chunks of rtg_render's overlapped host path (two chunks in flight on two streams)
+    // wavefront buffers, grown on demand
     WaveWork work[kWorkCtx];
     // scratch for the host-buffer entry point
     float* d_hdr = nullptr;
@@ -147,13 +145,10 @@ struct rtg_scene {
     // block -> tile tables, one per (tiles_x, tiles_y, mode) met (never re-uploaded: kernels of
     // several streams may be reading them)
     std::vector<std::unique_ptr<TileMap>> tile_maps;
-    // rtg_render's overlapped host path: the chunk streams and the copy stream
-    hipStream_t chunk_stream[2] = {nullptr, nullptr};
-    hipStream_t copy_stream = nullptr;
-    std::vector<hipEvent_t> chunk_ev;
     // RTG_RENDER_TIMING events (stage k runs between ev[k] and ev[k+1])
     hipEvent_t ev[rtg::MAX_STAGES + 1] = {};
     int timed_layout = -1;            // stage layout of the last timed render (rtg_kernels.hpp LAYOUT_*)
+    int timed_samples = 1;            // samples per pixel its timed stages covered (rtg_scene_timed_samples)
     // the scene's own stream (rtg_render) and the event marking the end of its last render
     // on whatever stream it was issued (rtg_scene_stats waits for it, not for the device)
     hipStream_t stream = nullptr;
@@ -180,11 +175,6 @@ struct rtg_scene {
             if (w.mem) (void)hipFree(w.mem);
             if (w.dq) (void)hipFree(w.dq);
         }
-        for (auto& c : chunk_stream)
-            if (c) (void)hipStreamDestroy(c);
-        if (copy_stream) (void)hipStreamDestroy(copy_stream);
-        for (auto& e : chunk_ev)
-            if (e) (void)hipEventDestroy(e);
     }
 };
 
@@ -444,69 +434,6 @@ static bool anyhit_trees(const rtg_scene_desc* d, const std::vector<float4>& nd,
     return ahbOk;
 }
 
-// Any-hit wide BVH (rtg_device.hpp WNode, rtg_common.hpp trace_any_wide): each mesh's
-// reference BVH (pre-order records with skip links, as uploaded) collapsed to 4-wide nodes.
-// A wide node's children are found by opening, from {left, right}, the inner child of largest
-// surface area until four remain (the collapse of Ylitie et al., HPG 2017, without a re-build):
-// every slot is a reference node with its box copied bit for bit, and the leaves are the
-// reference's leaves -- what the exactness argument of trace_any_wide needs.  Returns the root.
-static int build_wide(const std::vector<float4>& nodes, int root, std::vector<rtg::WNode>& out) {
-    auto leafv = [&](int i) { int l; std::memcpy(&l, &nodes[2 * i + 1].w, 4); return l; };
-    auto skipv = [&](int i) { int k; std::memcpy(&k, &nodes[2 * i + 1].z, 4); return k; };
-    auto area = [&](int i) {
-        const float4 a = nodes[2 * i], b = nodes[2 * i + 1];
-        const double dx = (double)a.w - a.x, dy = (double)b.x - a.y, dz = (double)b.y - a.z;
-        return dx * dy + dy * dz + dz * dx;
-    };
-    struct Job { int ref, slot_owner, slot; };
-    std::vector<Job> jobs{{root, -1, 0}};
-    int rootIdx = -1;
-    while (!jobs.empty()) {
-        const Job j = jobs.back();
-        jobs.pop_back();
-        std::vector<int> C;
-        if (leafv(j.ref) >= 0) C.push_back(j.ref);
-        else { C.push_back(j.ref + 1); C.push_back(skipv(j.ref + 1)); }
-        while (C.size() < 4) {
-            int best = -1;
-            double ba = -1.0;
-            for (size_t k = 0; k < C.size(); ++k)
-                if (leafv(C[k]) < 0 && area(C[k]) > ba) { ba = area(C[k]); best = (int)k; }
-            if (best < 0) break;
-            const int x = C[best];
-            C[best] = x + 1;
-            C.insert(C.begin() + best + 1, skipv(x + 1));
-        }
-        const int w = (int)out.size();
-        out.emplace_back();
-        rtg::WNode& W = out.back();
-        float* lo[3] = {&W.lox.x, &W.loy.x, &W.loz.x};
-        float* hi[3] = {&W.hix.x, &W.hiy.x, &W.hiz.x};
-        int* ch = &W.child.x;
-        int* lf = &W.leaf.x;
-        for (int k = 0; k < 4; ++k) {
-            if (k >= (int)C.size()) {
-                for (int a = 0; a < 3; ++a) { lo[a][k] = INFINITY; hi[a][k] = -INFINITY; }
-                ch[k] = rtg::WCHILD_EMPTY;
-                lf[k] = 0;
-                continue;
-            }
-            const float4 a = nodes[2 * C[k]], b = nodes[2 * C[k] + 1];
-            lo[0][k] = a.x; lo[1][k] = a.y; lo[2][k] = a.z;
-            hi[0][k] = a.w; hi[1][k] = b.x; hi[2][k] = b.y;
-            const int l = leafv(C[k]);
-            ch[k] = l >= 0 ? -2 - C[k] : rtg::WCHILD_EMPTY;
-            lf[k] = l >= 0 ? l : 0;
-        }
-        if (j.slot_owner >= 0) (&out[j.slot_owner].child.x)[j.slot] = w;
-        else rootIdx = w;
-        for (int k = (int)C.size() - 1; k >= 0; --k)
-            if (leafv(C[k]) < 0) jobs.push_back({C[k], w, k});
-    }
-    return rootIdx;
-}
-
-
 int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     if (!d || !out) return set_err(RTG_ERR_INVALID, "null argument");
     *out = nullptr;
@@ -640,16 +567,15 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
         else if (o.kind == RTG_OBJ_INSTANCE) feat |= rtg::FEAT_INSTANCE;
         else if (!ident || (o.flags & RTG_OBJF_MOTION_BLUR)) feat |= rtg::FEAT_XFORM;
     }
-    // shadow-ray acceleration (rtg_common.hpp): parent links + face -> leaf for the walk from
-    // the origin's leaf (trace_any_up), and the any-hit wide BVH (trace_any_wide, A/B builds).
+    // shadow-ray acceleration (rtg_common.hpp): the any-hit wide BVH (trace_any_wide) and
+    // face -> reference leaf (its exact leaf-box decisions, the deferred leaves' checks).
     // RTG_NO_FAST_SHADOW=1: shadow rays walk the reference BVH top-down.
-    std::vector<rtg::WNode> wide, anodes;
+    std::vector<rtg::WNode> anodes;
     std::vector<float4> ahtris;
     int ahbMode = rtg::AHB_EXACT;
-    std::vector<int2> nodeUp;
     std::vector<int> faceLeaf;
-    for (int i = 0; i < d->num_objects; ++i) objs[i].wroot = objs[i].aroot = -1;
-    if (!std::getenv("RTG_NO_FAST_SHADOW") && d->num_meshes > 0 && RTG_SHADOW_MODE >= 2) {
+    for (int i = 0; i < d->num_objects; ++i) objs[i].aroot = -1;
+    if (!std::getenv("RTG_NO_FAST_SHADOW") && d->num_meshes > 0) {
         std::vector<float4> dn;
         std::vector<int2> dx;
         if (gpuBuild) {
@@ -661,28 +587,15 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
         const std::vector<float4>& nd = gpuBuild ? dn : nodes;
         const std::vector<int2>& nx = gpuBuild ? dx : next;
         auto leafv = [&](int i) { int l; std::memcpy(&l, &nd[2 * i + 1].w, 4); return l; };
-        auto skipv = [&](int i) { int k; std::memcpy(&k, &nd[2 * i + 1].z, 4); return k; };
-        const size_t nn = nd.size() / 2;
-        nodeUp.assign(nn, make_int2(-1, -1));
         faceLeaf.assign((size_t)d->num_faces, -1);
-        std::vector<int> wroot(d->num_meshes, -1);
-        for (int m = 0; m < d->num_meshes; ++m) {
+        for (int m = 0; m < d->num_meshes; ++m)
             for (int p = meshBegin[m]; p < meshEnd[m]; ++p) {
                 const int l = leafv(p);
-                if (l < 0) {
-                    const int2 up = make_int2(p, skipv(p));
-                    nodeUp[p + 1] = up;
-                    nodeUp[skipv(p + 1)] = up;
-                } else {
-                    int first = l >> 8, cnt = l & 255;
-                    if (l == rtg::LEAF_EXT) { first = nx[p].x; cnt = nx[p].y; }
-                    for (int f = first; f < first + cnt; ++f) faceLeaf[f] = p;
-                }
+                if (l < 0) continue;
+                int first = l >> 8, cnt = l & 255;
+                if (l == rtg::LEAF_EXT) { first = nx[p].x; cnt = nx[p].y; }
+                for (int f = first; f < first + cnt; ++f) faceLeaf[f] = p;
             }
-            if (meshEnd[m] > meshBegin[m]) wroot[m] = build_wide(nd, meshBegin[m], wide);
-        }
-        for (int i = 0; i < d->num_objects; ++i)
-            objs[i].wroot = d->objects[i].kind != RTG_OBJ_SPHERE ? wroot[d->objects[i].mesh] : -1;
 
         // any-hit tree per mesh (anyhit_trees, rtg_ahb.cpp)
         std::vector<float4> ht;
@@ -740,9 +653,6 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     }
     for (int i = 0; i < d->num_objects; ++i) blur |= (d->objects[i].flags & RTG_OBJF_MOTION_BLUR) != 0;
     sc->feat = feat | (bigleaf ? rtg::FEAT_BIGLEAF : 0);
-    // RTG_FEAT_FORCE=<bits> ORs traversal feature bits in (experiments: a superset of the
-    // scene's features selects a more general kernel with the same results)
-    if (const char* e = std::getenv("RTG_FEAT_FORCE")) sc->feat |= std::atoi(e) & rtg::FEAT_ALL;
     // RTG_NO_COOP=1: large leaves tested by their own lane (the sequential walk handles any
     // leaf size; the cooperative one is only faster)
     if (std::getenv("RTG_NO_COOP")) sc->feat &= ~rtg::FEAT_BIGLEAF;
@@ -887,10 +797,8 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     HIP_TRY(sc->point_lights.upload(pls)); HIP_TRY(sc->area_lights.upload(als)); HIP_TRY(sc->dir_lights.upload(dls));
     HIP_TRY(sc->spot_lights.upload(sls)); HIP_TRY(sc->env_images.upload(envs));
     HIP_TRY(sc->mesh_lights.upload(mls)); HIP_TRY(sc->light_faces.upload(lfs));
-    HIP_TRY(sc->wnodes.upload(wide));
     HIP_TRY(sc->anodes.upload(anodes));
     HIP_TRY(sc->ahtris.upload(ahtris));
-    HIP_TRY(sc->node_up.upload(nodeUp));
     HIP_TRY(sc->face_leaf.upload(faceLeaf));
     std::vector<rtg::DevCounters> zero(1);
     std::memset(zero.data(), 0, sizeof(rtg::DevCounters));
@@ -923,7 +831,6 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     S.ambient[0] = d->ambient_light.x; S.ambient[1] = d->ambient_light.y; S.ambient[2] = d->ambient_light.z;
     for (int k = 0; k < 3; ++k) S.background[k] = d->background[k];
     S.coop = (sc->feat & rtg::FEAT_BIGLEAF) ? 1 : 0;
-    S.wnodes = wide.empty() ? nullptr : sc->wnodes.p;
     S.anodes = anodes.empty() ? nullptr : sc->anodes.p;
     S.ahtris = ahtris.empty() ? nullptr : sc->ahtris.p;
     S.ahb_split = ahbMode == rtg::AHB_SPLIT && !anodes.empty();
@@ -934,7 +841,6 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     HIP_TRY(sc->guard.alloc(1));
     HIP_TRY(hipMemset(sc->guard.p, 0, sizeof(int)));
     S.guard = sc->guard.p;
-    S.node_up = nodeUp.empty() ? nullptr : sc->node_up.p;
     S.face_leaf = faceLeaf.empty() ? nullptr : sc->face_leaf.p;
     HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&sc->done, hipEventDisableTiming));
@@ -1099,6 +1005,10 @@ static int prepare(rtg_scene* s, const rtg_render_opts* o, rtg::DevCamera& C, rt
     P.tiles_y = (P.part_rows + 15) / 16;
     P.num_tiles = P.tiles_x * P.tiles_y;
     if (P.num_tiles == 0) return RTG_OK;   // nothing of this part in the row range
+    // one sample per pass until launch() chooses more (pass_slabs)
+    P.slabs = 1;
+    P.slab_tiles = P.num_tiles;
+    P.slab_px = 16 * P.tiles_y * c.width;
     P.seed = o->seed;
     const int* map = nullptr;
     int rc = ensure_tile_map(s, P.tiles_x, P.tiles_y, &map);
@@ -1107,21 +1017,23 @@ static int prepare(rtg_scene* s, const rtg_render_opts* o, rtg::DevCamera& C, rt
     return RTG_OK;
 }
 
-// Sizes the wavefront buffers for `pixels` pixels x `slots` light slots and `tiles`
-// shade blocks (queue segments of 256 * slots entries), one allocation.
-static int ensure_wave(WaveWork& ww, size_t pixels, int slots, size_t tiles) {
-    if (ww.mem && ww.pixels >= pixels && ww.slots >= slots && ww.tiles >= tiles) return RTG_OK;
+// Sizes the wavefront buffers for `pixels` pixel entries x `slots` light slots and `tiles`
+// shade blocks (queue segments of 256 * slots entries), one allocation; `col`: with the colour
+// buffer of multi-sample passes (one float4 per entry).
+static int ensure_wave(WaveWork& ww, size_t pixels, int slots, size_t tiles, bool col = false) {
+    if (ww.mem && ww.pixels >= pixels && ww.slots >= slots && ww.tiles >= tiles && (ww.col || !col)) return RTG_OK;
     if (ww.dq) { (void)hipFree(ww.dq); ww.dq = nullptr; }
     if (ww.mem) { (void)hipFree(ww.mem); ww.mem = nullptr; }
     pixels = std::max(pixels, ww.pixels);
     tiles = std::max(tiles, ww.tiles);
+    col = col || ww.col;
     const size_t ns = pixels * (size_t)std::max(slots, 1);
     const size_t nq = tiles * 256 * (size_t)std::max(slots, 1);
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-    size_t off[12], total = 0;
-    const size_t sz[12] = {pixels * 4, pixels * 4, pixels * 4, pixels * 16, ns * 16, ns, nq * 16, nq * 16, nq * 4,
-                           tiles * 4, pixels * 16, slots <= 1 ? nq * 32 : 0};
-    for (int k = 0; k < 12; ++k) { off[k] = total; total += al(sz[k]); }
+    size_t off[13], total = 0;
+    const size_t sz[13] = {pixels * 4, pixels * 4, pixels * 4, pixels * 16, ns * 16, ns, nq * 16, nq * 16, nq * 4,
+                           tiles * 4, pixels * 16, slots <= 1 ? nq * 32 : 0, col ? pixels * 16 : 0};
+    for (int k = 0; k < 13; ++k) { off[k] = total; total += al(sz[k]); }
     HIP_TRY(hipMalloc(&ww.mem, total));
     char* b = (char*)ww.mem;
     rtg::WaveBufs& W = ww.W;
@@ -1130,6 +1042,8 @@ static int ensure_wave(WaveWork& ww, size_t pixels, int slots, size_t tiles) {
     W.q_o = (float4*)(b + off[6]); W.q_d = (float4*)(b + off[7]); W.q_slot = (int*)(b + off[8]);
     W.q_count = (int*)(b + off[9]); W.accum = (float4*)(b + off[10]);
     W.q_pay = slots <= 1 ? (float4*)(b + off[11]) : nullptr;
+    W.col = col ? (float4*)(b + off[12]) : nullptr;
+    ww.col = col;
     ww.pixels = pixels;
     ww.slots = slots;
     ww.tiles = tiles;
@@ -1179,24 +1093,44 @@ static int pipeline(const rtg_scene* s, const rtg_render_opts* o, const rtg::Dev
     return PIPE_MEGA;
 }
 
-// ctx: the wavefront work context (rtg_scene::work); pipe >= 0 forces the pipeline chosen
-// for the whole frame (row chunks of one frame must not fall below the ray-tree threshold)
-static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& C, const rtg::RenderParams& P,
-                  float* d_hdr, uint8_t* d_ldr, float* d_accum, hipStream_t stream, int ctx = 0, int pipe = -1) {
-    WaveWork& ww = s->work[ctx];
-    if (pipe < 0) pipe = pipeline(s, o, C, P);
+// Samples per pass of the wavefront and ray-tree pipelines (RenderParams::slabs): as many as
+// keep a pass at most ~RTG_PASS_RAYS camera rays (default 8 Mi: a 1920x1080 frame of 4 samples,
+// one 3840x2160 sample), spread evenly over the passes.  A pass's launches then stay full when
+// a GPU renders a small part of the frame, and a frame of few passes pays the tail of its
+// slowest waves (C3's pole fans, C5's deepest trees) once per pass, not once per sample.
+// RTG_PASS_RAYS=0: one sample per pass (round 5's passes; the image is the same bit for bit).
+static int pass_slabs(const rtg::RenderParams& P, int width) {
+    const char* v = std::getenv("RTG_PASS_RAYS");
+    const long long target = v ? std::atoll(v) : (8ll << 20);
+    const long long px = (long long)P.part_rows * width;
+    if (target <= 0 || P.sample_count <= 1 || px <= 0) return 1;
+    const long long k = std::max(1ll, std::min<long long>(target / px, P.sample_count));
+    const long long passes = (P.sample_count + k - 1) / k;
+    return (int)((P.sample_count + passes - 1) / passes);
+}
+
+// samples of the last pass (the one RTG_RENDER_TIMING times)
+static int last_pass_samples(const rtg::RenderParams& P) {
+    return P.sample_count - ((P.sample_count - 1) / P.slabs) * P.slabs;
+}
+
+static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& C, const rtg::RenderParams& P0,
+                  float* d_hdr, uint8_t* d_ldr, float* d_accum, hipStream_t stream) {
+    WaveWork& ww = s->work[0];
+    int pipe = pipeline(s, o, C, P0);
+    rtg::RenderParams P = P0;
+    if ((pipe == PIPE_WAVE || pipe == PIPE_TREE) && !(o->flags & RTG_RENDER_SAMPLE_PASSES)) {
+        P.slabs = pass_slabs(P, C.width);
+        if (P.slabs > 1) P.slab_tiles = (P.num_tiles + 7) & ~7;   // a tile keeps its XCD in every slab
+    }
     const bool stats = (o->flags & RTG_RENDER_COUNT_STATS) != 0;
     // RTG_RENDER_EXACT_SHADOW: shadow rays walk the reference BVH (cross-checks of the wide one)
     rtg::DevScene ds = s->ds;
     if (o->flags & RTG_RENDER_EXACT_SHADOW) ds.exact_shadow = 1;
-    // RTG_RENDER_ORDERED: the closest-hit walk on the any-hit tree (mode 2; its leaf boxes must be
-    // the reference's: not the split tree) or, with RTG_ORDERED_WALK=collapsed, round 3's per-lane
-    // walk of the collapsed reference tree (mode 1)
-    if (o->flags & RTG_RENDER_ORDERED) {
-        const bool collapsed = std::getenv("RTG_ORDERED_WALK") && !std::strcmp(std::getenv("RTG_ORDERED_WALK"), "collapsed");
-        if (!collapsed && ds.anodes && !ds.ahb_split) ds.ordered = 2;
-        else if (ds.wnodes && ds.face_leaf) ds.ordered = 1;
-    }
+    // RTG_RENDER_ORDERED: the checked closest-hit walk on the any-hit tree (its leaf boxes must be
+    // the reference's: not the split tree).  (Round 3's per-lane walk of the reference tree
+    // collapsed to 4 wide was removed in round 6.)
+    if ((o->flags & RTG_RENDER_ORDERED) && ds.anodes && !ds.ahb_split && ds.face_leaf) ds.ordered = 1;
     hipEvent_t* ev = nullptr;
     if (o->flags & RTG_RENDER_TIMING) {
         for (auto& e : s->ev)
@@ -1225,7 +1159,7 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
         const hipError_t pe = rtg::launch_path(s->path, ds, C, P, d_hdr, d_ldr, acc, s->counters.p, stats, s->feat,
                                                s->shade_sk, stream, ev);
         if (pe == hipSuccess) {
-            if (ev) s->timed_layout = rtg::LAYOUT_PATH;
+            if (ev) { s->timed_layout = rtg::LAYOUT_PATH; s->timed_samples = 1; }
             return RTG_OK;
         }
         if (pe != hipErrorNotSupported) HIP_TRY(pe);
@@ -1245,12 +1179,14 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
         }
         HIP_TRY(rtg::launch_tree(s->tree, ds, C, P, d_hdr, d_ldr, acc, s->counters.p, stats, s->feat, s->shade_sk,
                                  stream, ev));
-        if (ev) s->timed_layout = rtg::LAYOUT_TREE;
+        if (ev) { s->timed_layout = rtg::LAYOUT_TREE; s->timed_samples = last_pass_samples(P); }
         return RTG_OK;
     }
     if (pipe == PIPE_WAVE) {
-        const size_t rows = (size_t)P.part_rows;
-        int rc = ensure_wave(ww, rows * C.width, s->num_slots, (size_t)P.num_tiles);
+        // work-buffer entries and shade blocks of a pass (all its sample slabs)
+        const size_t entries = P.slabs > 1 ? (size_t)P.slabs * P.slab_px : (size_t)P.part_rows * C.width;
+        const size_t blocks = (size_t)P.slab_tiles * P.slabs;
+        int rc = ensure_wave(ww, entries, s->num_slots, blocks, P.slabs > 1);
         if (rc) return rc;
 
         rtg::WaveBufs W = ww.W;
@@ -1259,30 +1195,29 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
         else if (C.spp > 1) {   // internal accumulator indexed by absolute pixel
             size_t need = (size_t)C.width * C.height;
             if (need > ww.pixels) {
-                int rc2 = ensure_wave(ww, need, s->num_slots, (size_t)P.num_tiles);
+                int rc2 = ensure_wave(ww, need, s->num_slots, blocks, P.slabs > 1);
                 if (rc2) return rc2;
                 W = ww.W;
                 W.num_slots = s->num_slots;
             }
         }
         if ((s->feat & rtg::FEAT_BIGLEAF) && !stats && rtg::defer_leaves()) {
-            rc = ensure_defer(ww, rows * C.width, (size_t)P.num_tiles * 256 * std::max(s->num_slots, 1));
+            rc = ensure_defer(ww, entries, blocks * 256 * std::max(s->num_slots, 1));
             if (rc) return rc;
             W.dq_e = ww.W.dq_e;
             W.dq_count = ww.W.dq_count;
             W.hit_key = ww.W.hit_key;
             W.shadow_state = ww.W.shadow_state;
             W.dq_cap = ww.W.dq_cap;
-            W.defer_any_min = (int)std::max<int64_t>(1, (int64_t)rows * C.width / rtg::defer_any_gate());
         }
         int layout = rtg::LAYOUT_WAVE;
         HIP_TRY(rtg::launch_wave(ds, C, P, W, d_hdr, d_ldr, s->counters.p, stats, s->feat, s->shade_sk, stream, ev,
                                  &layout));
-        if (ev) s->timed_layout = layout;
+        if (ev) { s->timed_layout = layout; s->timed_samples = last_pass_samples(P); }
         return RTG_OK;
     }
     HIP_TRY(rtg::launch_mega(ds, C, P, d_hdr, d_ldr, d_accum, s->counters.p, stats, s->shade_sk, s->feat, stream, ev));
-    if (ev) s->timed_layout = rtg::LAYOUT_MEGA;
+    if (ev) { s->timed_layout = rtg::LAYOUT_MEGA; s->timed_samples = P.sample_count; }
     return RTG_OK;
 }
 
@@ -1333,83 +1268,10 @@ int rtg_copy_part_to_host(rtg_scene* s, const rtg_render_opts* o, const float* d
     return copy_part(o, c.width, c.height, d_hdr, d_ldr, hdr_rgb, ldr_rgb, (hipStream_t)stream);
 }
 
-// The overlapped host path of rtg_render (one device, frames of >= kChunkMinPixels): the
-// frame part is rendered in row chunks, alternately on two streams with their own work
-// buffers (rtg_scene::work 1 and 2), and each chunk's rows are copied to the host on a third
-// stream as soon as the chunk is done -- the D2H copy of chunk j runs under the rendering of
-// chunks j+1.., so only the last chunk's copy adds to the frame.  A chunk is a run of whole
-// rounds of the partition's bands (8 x part_count rows per round): part p's bands inside a
-// chunk starting at round m are the bands of part (p - m) mod part_count of that chunk (the
-// rotation of part_band), so the chunks together cover exactly part p's rows.  Pixels are
-// keyed by their image position (RNG included): the image is the one-launch image bit for bit.
-// Measured slower than one launch + one copy at every chunk count (2-16 chunks: 0.63-1.15 ms
-// against 0.58 ms per 1080p frame, profiles/r04d_hostpath.jsonl: each chunk's host-side launch
-// work and small grids cost more than the copy they hide), so it runs only on request:
-// RTG_HOST_CHUNKS=<chunks> (A/B).
-constexpr long long kChunkMinPixels = 1ll << 20;
-static bool chunk_disabled() { return std::getenv("RTG_HOST_CHUNKS") == nullptr; }
-static int host_chunks() {
-    const char* v = std::getenv("RTG_HOST_CHUNKS");
-    return v ? std::max(1, std::atoi(v)) : 8;
-}
-static bool chunk_copy_own() {
-    const char* v = std::getenv("RTG_HOST_CHUNK_COPY");
-    return v && !std::strcmp(v, "own");
-}
-
-static int render_chunked(rtg_scene* s, const rtg_render_opts* o, const rtg::RenderParams& P0, int pipe, int width,
-                          float* hdr_rgb, uint8_t* ldr_rgb) {
-    const int N = P0.part_count, per_round = RTG_PART_BAND_ROWS * N;
-    const int rounds = (P0.row_end - P0.row_begin + per_round - 1) / per_round;
-    const int kChunks = host_chunks();
-    const bool own = chunk_copy_own();
-    int cr = (rounds + kChunks - 1) / kChunks;
-    cr += cr & 1;                                    // even: a chunk's compact rows fill whole 16-row tiles
-    for (auto& c : s->chunk_stream)
-        if (!c) HIP_TRY(hipStreamCreateWithFlags(&c, hipStreamNonBlocking));
-    if (!s->copy_stream) HIP_TRY(hipStreamCreateWithFlags(&s->copy_stream, hipStreamNonBlocking));
-    const int nc = (rounds + cr - 1) / cr;
-    while ((int)s->chunk_ev.size() < nc) {
-        hipEvent_t e;
-        HIP_TRY(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-        s->chunk_ev.push_back(e);
-    }
-    // the chunks start after whatever the scene's stream holds
-    HIP_TRY(hipEventRecord(s->done, s->stream));
-    for (auto& c : s->chunk_stream) HIP_TRY(hipStreamWaitEvent(c, s->done, 0));
-    for (int j = 0; j < nc; ++j) {
-        const int m0 = j * cr;
-        rtg_render_opts oj = *o;
-        oj.row_begin = P0.row_begin + m0 * per_round;
-        oj.row_end = std::min(P0.row_end, P0.row_begin + (m0 + cr) * per_round);
-        oj.part_count = N;
-        oj.part_index = ((P0.part_index - m0) % N + N) % N;
-        rtg::DevCamera C;
-        rtg::RenderParams P;
-        int rc = prepare(s, &oj, C, P);
-        if (rc) return rc;
-        if (P.num_tiles == 0) continue;
-        hipStream_t st = s->chunk_stream[j & 1];
-        rc = launch(s, &oj, C, P, s->d_hdr, s->d_ldr, nullptr, st, 1 + (j & 1), pipe);
-        if (rc) return rc;
-        if (!own) {
-            HIP_TRY(hipEventRecord(s->chunk_ev[j], st));
-            HIP_TRY(hipStreamWaitEvent(s->copy_stream, s->chunk_ev[j], 0));
-        }
-        rc = copy_part(&oj, width, C.height, s->d_hdr, s->d_ldr, hdr_rgb, ldr_rgb, own ? st : s->copy_stream);
-        if (rc) return rc;
-    }
-    if (own)
-        for (auto& c : s->chunk_stream) {
-            HIP_TRY(hipEventRecord(s->chunk_ev[0], c));
-            HIP_TRY(hipStreamWaitEvent(s->copy_stream, s->chunk_ev[0], 0));
-        }
-    // the scene's stream (rtg_render_device callers, the next rtg_render) follows the copies
-    HIP_TRY(hipEventRecord(s->done, s->copy_stream));
-    HIP_TRY(hipStreamWaitEvent(s->stream, s->done, 0));
-    HIP_TRY(hipStreamSynchronize(s->copy_stream));
-    return RTG_OK;
-}
+// (Round 4's overlapped host path -- the frame rendered in row chunks on two streams, each
+// chunk's rows copied to the host under the next chunks -- measured slower than one launch + one
+// copy at every chunk count, profiles/r04d_hostpath.jsonl, and was removed in round 6; page-locked
+// frames take the direct writes below.)
 
 // The device's view of a page-locked host buffer (rtg_host_alloc / rtg_host_register), or null.
 static void* device_view(void* p) {
@@ -1434,8 +1296,7 @@ static bool host_direct() {
 // Replaces main.cpp:164-185.  With replicas (rtg_scene_create_multi) replica i renders part
 // i of n on its own stream and copies its rows into the caller's buffers; the renders of all
 // replicas are enqueued before any copy (a copy to pageable memory may block the host), then
-// every stream is synchronised -- never the whole device.  One device: frames of a million
-// pixels or more take the overlapped chunked path above (render_chunked).
+// every stream is synchronised -- never the whole device.
 int rtg_render(rtg_scene* s, const rtg_render_opts* o, float* hdr_rgb, uint8_t* ldr_rgb) {
     if (!s || !o) return set_err(RTG_ERR_INVALID, "null argument");
     if (o->flags & RTG_RENDER_ACCUM_ONLY) return set_err(RTG_ERR_INVALID, "use rtg_render_device for RTG_RENDER_ACCUM_ONLY");
@@ -1463,28 +1324,6 @@ int rtg_render(rtg_scene* s, const rtg_render_opts* o, float* hdr_rgb, uint8_t* 
             HIP_TRY(hipEventRecord(s->done, s->stream));
             HIP_TRY(hipStreamSynchronize(s->stream));
             return RTG_OK;
-        }
-    }
-    if (n == 1 && !chunk_disabled() && !(o->flags & (RTG_RENDER_TIMING | RTG_RENDER_COUNT_STATS)) &&
-        (long long)cam.width * cam.height >= kChunkMinPixels && !(cam.has_tonemapper)) {
-        rtg::DevCamera C;
-        rtg::RenderParams P;
-        int rc = prepare(s, o, C, P);
-        if (rc) return rc;
-        const int pipe = pipeline(s, o, C, P);
-        if (P.num_tiles > 0 && (pipe == PIPE_WAVE || pipe == PIPE_MEGA)) {
-            HIP_TRY(hipSetDevice(s->device));
-            const size_t pixels = (size_t)C.width * C.height;
-            if (s->d_pixels < pixels) {
-                HIP_TRY(hipStreamSynchronize(s->stream));
-                if (s->d_hdr) { (void)hipFree(s->d_hdr); s->d_hdr = nullptr; }
-                if (s->d_ldr) { (void)hipFree(s->d_ldr); s->d_ldr = nullptr; }
-                s->d_pixels = 0;
-                HIP_TRY(hipMalloc(&s->d_hdr, pixels * 3 * sizeof(float)));
-                HIP_TRY(hipMalloc(&s->d_ldr, pixels * 3));
-                s->d_pixels = pixels;
-            }
-            return render_chunked(s, o, P, pipe, C.width, hdr_rgb, ldr_rgb);
         }
     }
     for (int i = 0; i < n; ++i) {
@@ -1700,6 +1539,13 @@ int rtg_scene_timings(rtg_scene* s, float* ms, const char** names, int32_t cap, 
         if (names) names[k] = nm[k];
     }
     *count = n;
+    return RTG_OK;
+}
+
+int rtg_scene_timed_samples(const rtg_scene* s, int32_t* samples) {
+    if (!s || !samples) return set_err(RTG_ERR_INVALID, "null argument");
+    if (s->timed_layout < 0) return set_err(RTG_ERR_INVALID, "no render was issued with RTG_RENDER_TIMING");
+    *samples = s->timed_samples;
     return RTG_OK;
 }
 

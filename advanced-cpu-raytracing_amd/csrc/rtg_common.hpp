@@ -508,35 +508,6 @@ DEV void sload_node(const float4* p, rtg_s8& a) {                // 32 B: a refe
 DEV float4 f4(int x, int y, int z, int w) {
     return make_float4(__int_as_float(x), __int_as_float(y), __int_as_float(z), __int_as_float(w));
 }
-// Packed slab distances of a reference node record {min.xyz, max.x}{max.yz, skip, leaf} in
-// SGPRs: its adjacent pairs (min.x, min.y), (min.z, max.x), (max.y, max.z) against the ray
-// origin and reciprocal arranged the same way, three v_pk_add_f32 + three v_pk_mul_f32 for the
-// six (m - o) * rcp (each lane of a packed op rounds as the scalar op: the same values)
-typedef float rtg_f2 __attribute__((ext_vector_type(2)));
-struct RayPk {
-    rtg_f2 o01, o20, o12, i01, i20, i12;
-};
-template <typename RQ>
-DEV RayPk ray_pk(const Ray& r, const RQ& q) {
-    RayPk p;
-    p.o01 = rtg_f2{r.o.x, r.o.y};
-    p.o20 = rtg_f2{r.o.z, r.o.x};
-    p.o12 = rtg_f2{r.o.y, r.o.z};
-    p.i01 = rtg_f2{q.ix, q.iy};
-    p.i20 = rtg_f2{q.iz, q.ix};
-    p.i12 = rtg_f2{q.iy, q.iz};
-    return p;
-}
-// box_pass_pk on a node record in SGPRs with packed slab distances (rel: as box_pass_pk)
-DEV bool box_pass_rec(const int* nd, const RayPk& rp, const Ray& r, float minT, int rel, float slack0) {
-    const rtg_f2 t01 = (rtg_f2{__int_as_float(nd[0]), __int_as_float(nd[1])} - rp.o01) * rp.i01;   // tx1, ty1
-    const rtg_f2 t20 = (rtg_f2{__int_as_float(nd[2]), __int_as_float(nd[3])} - rp.o20) * rp.i20;   // tz1, tx2
-    const rtg_f2 t12 = (rtg_f2{__int_as_float(nd[4]), __int_as_float(nd[5])} - rp.o12) * rp.i12;   // ty2, tz2
-    return box_pass_t<true>(t01.x, t20.y, t01.y, t12.x, t20.x, t12.y, __int_as_float(nd[0]), __int_as_float(nd[1]),
-                            __int_as_float(nd[2]), __int_as_float(nd[3]), __int_as_float(nd[4]), __int_as_float(nd[5]),
-                            r, minT, (float)rel, slack0) > 0.0f;
-}
-
 // 64-bit lexicographic (t, face) key of a candidate hit; t > 0, so the float bits order
 // like the values.  Non-candidates: ~0.
 DEV uint64_t hit_key(float t, int f) { return ((uint64_t)__float_as_uint(t) << 32) | (uint32_t)f; }
@@ -818,47 +789,27 @@ constexpr int kDeferLeaf = 16;
 // record than a 64-bit index; scenes are limited to 2^25 faces (rtg_scene_create), which keeps
 // every node, wide node and face-record array below 4 GiB (k_primary 0.1881 -> 0.1828 ms,
 // profiles/r04aa_addr_on_ab.txt)
-#ifndef RTG_NODE_ADDR32
-#define RTG_NODE_ADDR32 1
-#endif
 template <int BYTES, typename T>
 DEV const T* rec_at(const T* base, int i) {
-#if RTG_NODE_ADDR32
     return (const T*)((const char*)base + (uint32_t)i * (uint32_t)BYTES);
-#else
-    return (const T*)((const char*)base + (size_t)i * BYTES);
-#endif
 }
 #ifndef RTG_DEFER_LANES
 #define RTG_DEFER_LANES 16
-#endif
-#ifndef RTG_PK_LEAN
-#define RTG_PK_LEAN 1
 #endif
 // (Round 5 also started node i + 1's record -- where a passing inner node descends -- while node
 // i was tested, waiting for it at the end of the step: k_frame 0.2878 -> 0.2912 ms, C3-ton +1 %,
 // C4 -0.7 %; profiles/r05ac_pk_prefetch_ab.txt.  The scalar loads' latency is already covered by
 // the other waves.)
-// the camera packet walk's slab distances as three packed pairs of the node record (box_pass_rec):
-// six fewer VALU per node step in the listing, but k_frame 0.289 -> 0.300 ms on the GPU
-// (profiles/r05n_pairs_inst6_deferany_ab.txt), so off
-#ifndef RTG_PK_PAIRS
-#define RTG_PK_PAIRS 0
-#endif
+// (The camera packet walk's slab distances as three packed pairs of the node record: six fewer
+// VALU per node step in the listing, but k_frame 0.289 -> 0.300 ms on the GPU,
+// profiles/r05n_pairs_inst6_deferany_ab.txt -- removed.)
 // (A/B parts of the lean packet walks: the any-hit walk, the closest-hit walk's face test)
-#ifndef RTG_PK_LEAN_ANY
-#define RTG_PK_LEAN_ANY RTG_PK_LEAN
-#endif
-#ifndef RTG_PK_LEAN_TRI
-#define RTG_PK_LEAN_TRI RTG_PK_LEAN
-#endif
 struct DeferCtx {
     float4* e;
     int* count;
     int cap;
     int ray;                          // the pixel's work-buffer index
     bool deferred;                    // this lane appended an entry
-    int big;                          // wave-uniform: lanes that tested a large leaf in the walk
 };
 // (t, object, face) as one 64-bit key: t > 0 orders like its bits; objects < 2^12, faces < 2^20
 // (defer_ok); a sphere's face field is all ones
@@ -869,22 +820,15 @@ DEV uint64_t obj_key(float t, int k, int f) {
 template <bool ANY, bool STATS, bool SC = false, bool DEFER = false>
 DEV bool walk_bvh_packet(const DevScene& S, int begin, int end, const Ray& r, float& minT, int& hitFace,
                          float limit, Cnt<STATS>& c, DeferCtx* dc = nullptr, int k = 0) {
-#if RTG_PK_LEAN
     // the node range is the object's (wave-uniform): SGPRs, so the loop index and its bound stay
     // scalar; "a face was accepted" is read off hitFace at the end instead of a lane mask kept
     // through every iteration
     begin = __builtin_amdgcn_readfirstlane(begin);
     end = __builtin_amdgcn_readfirstlane(end);
     const int face0 = hitFace;
-#endif
     bool hit = false;
     const RayRcp q = ray_rcp(r);
-#if RTG_PK_LEAN
     const float slack0 = q.fast ? 1e-30f : INFINITY;   // box_pass_pk: a ray off the fast path is never sure
-#if RTG_PK_PAIRS
-    const RayPk rp = ray_pk(r, q);
-#endif
-#endif
     const int kDone = 0x7FFFFFFF;
     int resume = begin;                              // per lane: first node it takes part in again
     int i = begin;                                   // wave-uniform
@@ -925,19 +869,10 @@ DEV bool walk_bvh_packet(const DevScene& S, int begin, int end, const Ray& r, fl
         bool pass;
         if constexpr (SC) {
             if (act) c.template node<ANY>();
-#if RTG_PK_LEAN
-#if RTG_PK_PAIRS
-            pass = box_pass_rec(ndr, rp, r, minT, ip1 - resume, slack0);
-#else
             pass = box_pass_pk(a.x, a.y, a.z, a.w, b.x, b.y, r, q, minT, ip1 - resume, slack0);
-#endif
             // a lane inside its walk that fails the box resumes at the box's skip; lanes outside it
             // already wait for a node past this box's subtree (resume >= skip), as do lanes that pass
             resume = max(resume, pass ? 0 : skip);
-#else
-            pass = act & box_hit_fast<true>(a.x, a.y, a.z, a.w, b.x, b.y, r, q, minT, act);
-            resume = (act & !pass) ? skip : resume;
-#endif
         } else {
             pass = false;
             if (act) {
@@ -946,10 +881,6 @@ DEV bool walk_bvh_packet(const DevScene& S, int begin, int end, const Ray& r, fl
                 if (!pass) resume = skip;
             }
         }
-#if !RTG_PK_LEAN
-        const bool any = __ballot(pass) != 0;
-#endif
-#if RTG_PK_LEAN
         // the next node and the leaf to test in five scalar instructions (the compiler kept the
         // two wave-uniform conditions as 64-bit masks with selects and branches between them):
         // lf = the leaf word when some lane passed, else 0 (no faces); next = lf < 0 (a passed
@@ -970,11 +901,6 @@ DEV bool walk_bvh_packet(const DevScene& S, int begin, int end, const Ray& r, fl
         }
         if (lf > 0) {
             {
-#else
-        const int cur = i;
-        if (leaf >= 0) {
-            if (any) {
-#endif
                 int first = leaf >> 8, cnt = leaf & 255;
                 if (leaf == LEAF_EXT) {
                     const int2 e = S.node_ext[cur];
@@ -999,8 +925,6 @@ DEV bool walk_bvh_packet(const DevScene& S, int begin, int end, const Ray& r, fl
                             pass = false;                // queued: no test here, minT unchanged
                         }
                         // (a lane whose entry did not fit tests the leaf below)
-                    } else if (cnt > kDeferLeaf) {
-                        dc->big += __popcll(m);          // the shadow walk's choice reads these (GATE)
                     }
                 }
                 for (int f = first; f < first + cnt; ++f) {
@@ -1012,16 +936,9 @@ DEV bool walk_bvh_packet(const DevScene& S, int begin, int end, const Ray& r, fl
                                              f4(rb[0], rb[1], rb[2], rb[3])};
                         if (pass) c.template tri<ANY>();
                         float t;
-#if RTG_PK_LEAN_TRI
                         const bool ok = tri_test_pk(R, r, minT, t, pass ? 1.0f : -1.0f) > 0.0f;
-#else
-                        const bool ok = pass & tri_test_sel(R, r, minT, t, pass);
-#endif
                         minT = ok ? t : minT;
                         hitFace = ok ? f : hitFace;
-#if !RTG_PK_LEAN
-                        hit |= ok;
-#endif
                         if (ANY) {
                             const bool fin = ok & (t < limit);
                             pass &= !fin;
@@ -1042,16 +959,9 @@ DEV bool walk_bvh_packet(const DevScene& S, int begin, int end, const Ray& r, fl
                     }
                 }
             }
-#if !RTG_PK_LEAN
-            i = skip;
-        } else {
-            i = any ? i + 1 : skip;
-#endif
         }
     }
-#if RTG_PK_LEAN
     if constexpr (SC) return hit | (hitFace != face0);
-#endif
     return hit;
 }
 
@@ -1209,24 +1119,14 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
 // (its leaf box entry within rounding of lightT -- a light lying on a surface) or a full
 // traversal stack make the answer "undecided" (-1): the caller then runs the reference
 // walk for that ray.  0: no face meets the necessary condition -- not in shadow.
-#ifndef RTG_WIDE_STACK
-#define RTG_WIDE_STACK 24
-#endif
-// Shadow rays walk the any-hit tree as wave packets (walk_wide_any_pk) -- 1, the default:
-// headline k_shade_shadow 0.246 -> 0.211 ms, 0 differing pixels (profiles/r03pk*) -- or per
-// lane (walk_wide_any) -- 0.
-#ifndef RTG_ANY_PACKET
-#define RTG_ANY_PACKET 1
-#endif
 // k_shadow<FAST> / the fused shade kernel (the wide walk + the in-place reference fallback)
-// compiled for this many waves per SIMD.  Per-lane walk (RTG_ANY_PACKET=0): five (96 VGPRs, no
-// spills) measured 0.228 ms on the headline against 0.291 at six (76 B of spills) and 0.26 at the
-// natural four.  Packet walk (default): 81 VGPRs and no LDS stack at five, six 0.211 ms, seven
+// compiled for this many waves per SIMD.  (Round 3's per-lane walk, removed: five waves, 96
+// VGPRs, 0.228 ms on the headline.)  Packet walk: 81 VGPRs and no LDS stack at five, six 0.211 ms, seven
 // 0.215, eight 0.216 (profiles/r03pk4_*); instance scenes keep RTG_INST_WAVES.  Round 4, after
 // the leaner slab test and mask copies: five 0.193, six 0.1804, seven 0.1742, eight 0.270 ms
 // (spills), large-leaf configurations unchanged (profiles/r04ad_wide_waves_ab.txt, r04ae_wide_waves_configs_ab.txt)
 #ifndef RTG_WIDE_WAVES_PLAIN
-#define RTG_WIDE_WAVES_PLAIN (RTG_ANY_PACKET ? 7 : 5)
+#define RTG_WIDE_WAVES_PLAIN 7
 #endif
 // instance scenes' any-hit walks (their own knob): the deferring shadow walk spills 124 B per
 // lane at six waves, 76 at five and none at four (118 VGPRs), and six is the fastest -- C4
@@ -1282,79 +1182,9 @@ struct AnyDefer {
     int q;                            // the shadow ray's queue entry
     bool deferred;
 };
-// One mesh's any-hit tree (rtg_ahb.cpp; local ray lr).  inst_conf: the instance's world box
-// passes at limit (true for plain meshes).  Returns 1 / 0 / -1 as above.  A node's leaf
-// children are tested in place (all lanes stay in step: a separate iteration per leaf measured
-// 2x slower), then the nearest hit inner child is the next node and the others go onto the
-// stack.  A leaf is a range of entries, each a face record with its reference leaf node in
-// the first record's w: the exact decisions use that leaf's own box.
-template <bool STATS>
-DEV int walk_wide_any(const DevScene& S, int node, const Ray& lr, float minT0, float limit, bool inst_conf,
-                      Cnt<STATS>& c) {
-    __shared__ int stack[RTG_WIDE_STACK][256];
-    const RayRcp q = ray_rcp(lr);
-    if (!q.fast) return -1;                          // zero / tiny direction component: reference walk
-    const float minTc = minT0 * (1.0f + 0x1p-21f);
-    const SlabRay sr = slab_ray(lr, q);
-    const int tid = threadIdx.x;
-    int sp = 0;
-    bool undecided = false;
-    while (true) {
-        const WNode* N = S.anodes + node;
-        const float4 lox = N->lox, hix = N->hix, loy = N->loy, hiy = N->hiy, loz = N->loz, hiz = N->hiz;
-        const int4 ch = N->child, lf = N->leaf;
-        c.wnode();
-        float tn[4];
-        bool h[4];
-        h[0] = slab_cons(lox.x, loy.x, loz.x, hix.x, hiy.x, hiz.x, sr, minTc, tn[0]) & (ch.x != WCHILD_EMPTY);
-        h[1] = slab_cons(lox.y, loy.y, loz.y, hix.y, hiy.y, hiz.y, sr, minTc, tn[1]) & (ch.y != WCHILD_EMPTY);
-        h[2] = slab_cons(lox.z, loy.z, loz.z, hix.z, hiy.z, hiz.z, sr, minTc, tn[2]) & (ch.z != WCHILD_EMPTY);
-        h[3] = slab_cons(lox.w, loy.w, loz.w, hix.w, hiy.w, hiz.w, sr, minTc, tn[3]) & (ch.w != WCHILD_EMPTY);
-        const int cidx[4] = {ch.x, ch.y, ch.z, ch.w};
-        const int lidx[4] = {lf.x, lf.y, lf.z, lf.w};
-        int next = -1;
-        float nextT = INFINITY;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            if (!h[k]) continue;
-            const int cr = cidx[k];
-            if (cr >= 0) {
-                int spill = cr;
-                if (tn[k] < nextT) {
-                    spill = next;
-                    next = cr;
-                    nextT = tn[k];
-                }
-                if (spill >= 0) {
-                    if (sp < RTG_WIDE_STACK) stack[sp++][tid] = spill;
-                    else undecided = true;
-                }
-                continue;
-            }
-            const int first = lidx[k] >> 8, cnt = lidx[k] & 255;
-            for (int e = first; e < first + cnt; ++e) {
-                c.template tri<true>();
-                float t;
-                if (!tri_test_fast_rec(S.ahtris + 3 * (size_t)e, lr, limit, t)) continue;
-                // exact decisions on the face's reference leaf box
-                const int ref = __float_as_int(S.ahtris[3 * (size_t)e].w);
-                const float4 a = S.nodes[2 * ref], b = S.nodes[2 * ref + 1];
-                if (!box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, minT0)) continue;   // leaf unreachable
-                if (inst_conf && box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, limit)) return 1;
-                undecided = true;
-            }
-        }
-        if (next >= 0) {
-            node = next;
-            continue;
-        }
-        if (sp == 0) break;
-        node = stack[--sp][tid];
-    }
-    return undecided ? -1 : 0;
-}
-
-// The same walk as a wave packet (RTG_ANY_PACKET): the wave visits one node sequence, the
+// One mesh's any-hit tree (rtg_ahb.cpp; local ray lr) walked as a wave packet.  inst_conf: the
+// instance's world box passes at limit (true for plain meshes).  Returns 1 / 0 / -1 as above.
+// The wave visits one node sequence, the
 // union of its live lanes' walks, so node, face and reference-leaf records are wave-uniform
 // (scalar loads through the scalar cache, nothing through the vector memory path) and the
 // stack is wave-uniform too (64 LDS words per wave, written by one live lane).  A lane tests a child, a face or a
@@ -1366,13 +1196,9 @@ DEV int walk_wide_any(const DevScene& S, int node, const Ray& lr, float minT0, f
 #define RTG_PK_STACK 64
 // the packet walk's face tests with selects and wave-uniform branches (1: k_shade_shadow 0.211 ->
 // 0.190 ms, profiles/r03sel_ab.txt) or per-lane early outs (0)
-#ifndef RTG_PK_SELECT
-#define RTG_PK_SELECT 1
-#endif
 #ifndef RTG_PK_MAX_STEPS
 #define RTG_PK_MAX_STEPS 4096
 #endif
-#if RTG_PK_LEAN_ANY
 // slab_cons as a value (> 0: the conservative test passes and the lane walks, livef > 0): tmax >
 // -1e-30 is tmax + 1e-30 > 0 and tmin < minTc is minTc - tmin > 0 (exact: rounded sums and
 // differences keep their signs); tmax >= tmin (1 - 2^-21) - 1e-30 is loosened by another 1e-30
@@ -1389,12 +1215,10 @@ DEV float slab_cons_v(float lx, float ly, float lz, float hx, float hy, float hz
     return __builtin_elementwise_minimum(
         vmin3(tmax + 1e-30f, (tmax - fmaf(tmin, 1.0f - 0x1p-21f, -1e-30f)) + 1e-30f, minTc - tmin), livef);
 }
-#endif
 
 template <bool STATS, bool DEFER = false>
 DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0, float limit, bool inst_conf,
                          Cnt<STATS>& c, AnyDefer* ad = nullptr) {
-#if RTG_PK_LEAN_ANY
     // The lane state as values, every wave-level test one comparison (the mask version kept
     // live / occluded / undecided and the four child masks as SGPR pairs merged at every block
     // and spilled to VGPR lanes): livef > 0 walking, occ / und flags, a child's hk > 0 taking it.
@@ -1507,145 +1331,12 @@ DEV int walk_wide_any_pk(const DevScene& S, int node, const Ray& lr, float minT0
         node = stk[--sp];
     }
     return occ ? 1 : (und ? -1 : 0);
-#else
-    const RayRcp q = ray_rcp(lr);
-    const float minTc = minT0 * (1.0f + 0x1p-21f);
-    const SlabRay sr = slab_ray(lr, q);
-    bool live = q.fast;                              // still walking
-    bool occ = false;                                // a sufficient face found
-    bool undecided = !q.fast;                        // zero / tiny direction component: reference walk
-    __shared__ int pk_stack[4][RTG_PK_STACK];        // the wave's stack (256-thread blocks)
-    int* const stk = pk_stack[(threadIdx.x >> 6) & 3];
-    int sp = 0;                                      // wave-uniform
-    node = __builtin_amdgcn_readfirstlane(node);
-    int steps = 0;                                   // bound: a walk visits each node once
-    while (__ballot(live)) {
-        if (++steps > RTG_PK_MAX_STEPS) {
-            undecided |= live;
-            break;
-        }
-        node = __builtin_amdgcn_readfirstlane(node);
-        rtg_s16 na, nb;
-        sload_wnode(rec_at<128>(S.anodes, node), na, nb);
-        const float4 lox = f4(na[0], na[1], na[2], na[3]), hix = f4(na[4], na[5], na[6], na[7]);
-        const float4 loy = f4(na[8], na[9], na[10], na[11]), hiy = f4(na[12], na[13], na[14], na[15]);
-        const float4 loz = f4(nb[0], nb[1], nb[2], nb[3]), hiz = f4(nb[4], nb[5], nb[6], nb[7]);
-        const int4 ch = make_int4(nb[8], nb[9], nb[10], nb[11]), lf = make_int4(nb[12], nb[13], nb[14], nb[15]);
-        if (live) c.wnode();
-        float tn[4];
-        bool h[4];
-        h[0] = slab_cons(lox.x, loy.x, loz.x, hix.x, hiy.x, hiz.x, sr, minTc, tn[0]) & live;
-        h[1] = slab_cons(lox.y, loy.y, loz.y, hix.y, hiy.y, hiz.y, sr, minTc, tn[1]) & live;
-        h[2] = slab_cons(lox.z, loy.z, loz.z, hix.z, hiy.z, hiz.z, sr, minTc, tn[2]) & live;
-        h[3] = slab_cons(lox.w, loy.w, loz.w, hix.w, hiy.w, hiz.w, sr, minTc, tn[3]) & live;
-        const int cidx[4] = {ch.x, ch.y, ch.z, ch.w};
-        const int lidx[4] = {lf.x, lf.y, lf.z, lf.w};
-        const uint64_t lm = __ballot(live);
-        const int lead = __ffsll((long long)lm) - 1;
-        int next = -1;
-        float nextT = INFINITY;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            const int cr = cidx[k];
-            // (a local copy: writes into h[] made the compiler pack the four masks into VGPR bytes)
-            bool hk = h[k];
-            if (cr == WCHILD_EMPTY || !__ballot(hk)) continue;
-            if (cr >= 0) {
-                const float t = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(tn[k]), lead));
-                int spill = cr;
-                if (t < nextT) {
-                    spill = next;
-                    next = cr;
-                    nextT = t;
-                }
-                if (spill >= 0) {
-                    if (sp < RTG_PK_STACK) {             // written by the first live lane
-                        if ((int)(threadIdx.x & 63) == lead) stk[sp] = spill;
-                        ++sp;
-                    }
-                    else undecided |= live;
-                }
-                continue;
-            }
-            const int first = lidx[k] >> 8, cnt = lidx[k] & 255;
-            if constexpr (DEFER) {
-                const uint64_t m = __ballot(hk);
-                if (cnt > RTG_DEFER_ANY_LEAF && __popcll(m) <= RTG_DEFER_ANY_LANES) {
-                    const int lane = threadIdx.x & 63, lead = __ffsll((long long)m) - 1;
-                    int base = 0;
-                    if (lane == lead) base = atomicAdd(ad->count, __popcll(m));
-                    base = __shfl(base, lead);
-                    const int slot = base + __popcll(m & ((1ull << lane) - 1ull));
-                    if (hk && slot < ad->cap) {
-                        float4* qe = ad->e + 3 * (size_t)slot;
-                        qe[0] = make_float4(lr.o.x, lr.o.y, lr.o.z, minT0);
-                        qe[1] = make_float4(lr.d.x, lr.d.y, lr.d.z, limit);
-                        qe[2] = make_float4(__int_as_float(first), __int_as_float(cnt), __int_as_float(ad->q),
-                                            __int_as_float((int)inst_conf));
-                        ad->deferred = true;
-                        hk = false;
-                    }
-                }
-            }
-            for (int e = first; e < first + cnt; ++e) {
-                rtg_s8 ra;
-                rtg_s4 rb;
-                sload_rec(rec_at<48>(S.ahtris, e), ra, rb);
-#if RTG_PK_SELECT
-                if (hk) c.template tri<true>();
-                const float4 R[3] = {f4(ra[0], ra[1], ra[2], ra[3]), f4(ra[4], ra[5], ra[6], ra[7]), f4(rb[0], rb[1], rb[2], rb[3])};
-                float t;
-                const bool ok = tri_test_sel(R, lr, limit, t) & hk;
-                if (!__ballot(ok)) continue;
-                rtg_s8 rn;
-                sload_node(rec_at<32>(S.nodes, ra[3]), rn);
-                const bool reach = ok & box_hit_fast<true>(__int_as_float(rn[0]), __int_as_float(rn[1]), __int_as_float(rn[2]),
-                                                           __int_as_float(rn[3]), __int_as_float(rn[4]), __int_as_float(rn[5]),
-                                                           lr, q, minT0);
-                const bool suff = reach & inst_conf &
-                                  box_hit_fast<true>(__int_as_float(rn[0]), __int_as_float(rn[1]), __int_as_float(rn[2]),
-                                                     __int_as_float(rn[3]), __int_as_float(rn[4]), __int_as_float(rn[5]),
-                                                     lr, q, limit);
-                occ |= suff;
-                live &= !suff;
-                hk &= !suff;
-                undecided |= reach & !suff;
-#else
-                if (!hk) continue;
-                c.template tri<true>();
-                const float4 R[3] = {f4(ra[0], ra[1], ra[2], ra[3]), f4(ra[4], ra[5], ra[6], ra[7]), f4(rb[0], rb[1], rb[2], rb[3])};
-                float t;
-                if (!tri_test_fast_rec(R, lr, limit, t)) continue;
-                rtg_s8 rn;
-                sload_node(rec_at<32>(S.nodes, ra[3]), rn);
-                const float4 a = f4(rn[0], rn[1], rn[2], rn[3]), b = f4(rn[4], rn[5], rn[6], rn[7]);
-                if (!box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, minT0)) continue;   // leaf unreachable
-                if (inst_conf && box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, limit)) {
-                    live = false;
-                    occ = true;
-                    hk = false;
-                    continue;
-                }
-                undecided = true;
-#endif
-            }
-        }
-        if (!__ballot(live)) break;
-        if (next >= 0) {
-            node = next;
-            continue;
-        }
-        if (sp == 0) break;
-        node = stk[--sp];
-    }
-    return occ ? 1 : (undecided ? -1 : 0);
-#endif
 }
 
 // CastShadowRay on the wide BVH: objects in any order (the answer is a boolean), spheres
 // exactly (a sphere hit with t < limit is accepted at any minT_cur >= limit, one with
 // t >= limit never decides).  Returns 1 / 0 / -1 (undecided: run trace<true>).
-template <bool STATS, int FEAT, bool DEFER = false, bool PK = RTG_ANY_PACKET || DEFER>
+template <bool STATS, int FEAT, bool DEFER = false>
 DEV int trace_any_wide(const DevScene& S, const Ray& r, float minT0, float limit, Cnt<STATS>& c,
                        AnyDefer* ad = nullptr) {
     const RayRcp rq = (FEAT & FEAT_INSTANCE) ? ray_rcp(r) : RayRcp{};
@@ -1656,21 +1347,16 @@ DEV int trace_any_wide(const DevScene& S, const Ray& r, float minT0, float limit
         const DevObject& ob = S.objects[k];
         if ((FEAT & FEAT_INSTANCE) && ob.group_end > k) {
             const float4 ga = S.group_box[2 * k], gb = S.group_box[2 * k + 1];
-            if (PK) {
-                // the packet walk needs one object (one root) per wave: a lane whose group box
-                // fails sits the group out, and the wave jumps over it when every lane does
-                if (k >= gskip && !box_hit_fast(ga.x, ga.y, ga.z, gb.x, gb.y, gb.z, r, rq, minT0))
-                    gskip = ob.group_end;
-                if (!__ballot(k >= gskip)) {
-                    k = ob.group_end - 1;
-                    continue;
-                }
-            } else if (!box_hit_fast(ga.x, ga.y, ga.z, gb.x, gb.y, gb.z, r, rq, minT0)) {
+            // the packet walk needs one object (one root) per wave: a lane whose group box
+            // fails sits the group out, and the wave jumps over it when every lane does
+            if (k >= gskip && !box_hit_fast(ga.x, ga.y, ga.z, gb.x, gb.y, gb.z, r, rq, minT0))
+                gskip = ob.group_end;
+            if (!__ballot(k >= gskip)) {
                 k = ob.group_end - 1;
                 continue;
             }
         }
-        if (PK && k < gskip) continue;
+        if (k < gskip) continue;
         c.obj();
         if ((FEAT & FEAT_SPHERE) && ob.kind == OBJ_SPHERE) {
             c.sph();
@@ -1688,8 +1374,7 @@ DEV int trace_any_wide(const DevScene& S, const Ray& r, float minT0, float limit
         }
         const Ray lr = (FEAT & FEAT_XFORM) ? trav_ray(ob, r, 0.f) : r;
         if (ob.aroot < 0) return -1;                 // no any-hit tree for this mesh: reference walk
-        const int res = PK ? walk_wide_any_pk<STATS, DEFER>(S, ob.aroot, lr, minT0, limit, conf, c, ad)
-                           : walk_wide_any<STATS>(S, ob.aroot, lr, minT0, limit, conf, c);
+        const int res = walk_wide_any_pk<STATS, DEFER>(S, ob.aroot, lr, minT0, limit, conf, c, ad);
         if (res > 0) return 1;
         undecided |= res < 0;
     }
@@ -1716,122 +1401,6 @@ DEV int trace_any_wide(const DevScene& S, const Ray& r, float minT0, float limit
 // agreement with the reference order (tests/test_gpu_ordered.py).
 // Smallest float above a positive x (inf stays inf): "minT = next_up(t)" accepts t' <= t.
 DEV float next_up(float x) { return x == INFINITY ? x : __uint_as_float(__float_as_uint(x) + 1u); }
-#ifndef RTG_ORD_STACK
-#define RTG_ORD_STACK 12
-#endif
-template <bool STATS>
-DEV bool trace_ordered(const DevScene& S, const Ray& r, Hit& h, Cnt<STATS>& c) {
-    __shared__ int s_node[RTG_ORD_STACK][256];
-    __shared__ float s_tn[RTG_ORD_STACK][256];
-    h.t = INFINITY;
-    h.obj = -1;
-    h.face = -1;
-    h.o = r.o;
-    const RayRcp q = ray_rcp(r);
-    if (!q.fast) return false;
-    const SlabRay sr = slab_ray(r, q);
-    const int tid = threadIdx.x;
-    float bestT = INFINITY, cullMin = INFINITY;
-    int bestF = -1, bestK = -1;
-    for (int k = 0; k < S.num_objects; ++k) {
-        const DevObject& ob = S.objects[k];
-        c.obj();
-        if (ob.wroot < 0) continue;
-        int node = ob.wroot, sp = 0;
-        while (true) {
-            const WNode* N = S.wnodes + node;
-            const float4 lox = N->lox, hix = N->hix, loy = N->loy, hiy = N->hiy, loz = N->loz, hiz = N->hiz;
-            const int4 ch = N->child, lf = N->leaf;
-            c.ewnode();
-            // a child passes when its conservative entry is at most the best t (ties may still win)
-            const float minTc = bestT * (1.0f + 0x1p-21f);
-            float tn[4];
-            bool hinf[4];
-            const float inf = INFINITY;
-            hinf[0] = slab_cons(lox.x, loy.x, loz.x, hix.x, hiy.x, hiz.x, sr, inf, tn[0]) & (ch.x != WCHILD_EMPTY);
-            hinf[1] = slab_cons(lox.y, loy.y, loz.y, hix.y, hiy.y, hiz.y, sr, inf, tn[1]) & (ch.y != WCHILD_EMPTY);
-            hinf[2] = slab_cons(lox.z, loy.z, loz.z, hix.z, hiy.z, hiz.z, sr, inf, tn[2]) & (ch.z != WCHILD_EMPTY);
-            hinf[3] = slab_cons(lox.w, loy.w, loz.w, hix.w, hiy.w, hiz.w, sr, inf, tn[3]) & (ch.w != WCHILD_EMPTY);
-            const int cidx[4] = {ch.x, ch.y, ch.z, ch.w};
-            const int lidx[4] = {lf.x, lf.y, lf.z, lf.w};
-            // leaves first (they can only lower bestT), then the inner children nearest first
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (!hinf[j] || cidx[j] >= 0) continue;
-                if (!(tn[j] < minTc)) { cullMin = fminf(cullMin, tn[j]); continue; }
-                const int ref = -2 - cidx[j];
-                int first = lidx[j] >> 8, cnt = lidx[j] & 255;
-                if (lidx[j] == LEAF_EXT) {
-                    const int2 e = S.node_ext[ref];
-                    first = e.x;
-                    cnt = e.y;
-                }
-                for (int f = first; f < first + cnt; ++f) {
-                    c.template tri<false>();
-                    float t;
-                    // accepted at minT just above bestT: t <= bestT
-                    if (!tri_test_fast(S, f, r, next_up(bestT), t)) continue;
-                    // (t, object, face) order; t <= bestT here, objects come in order
-                    if (t < bestT || (k == bestK && f < bestF)) {
-                        bestT = t;
-                        bestF = f;
-                        bestK = k;
-                    }
-                }
-            }
-            const float minTc2 = bestT * (1.0f + 0x1p-21f);
-            int next = -1;
-            float nextT = INFINITY;
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {
-                if (!hinf[j] || cidx[j] < 0) continue;
-                if (!(tn[j] < minTc2)) { cullMin = fminf(cullMin, tn[j]); continue; }
-                int spillN = cidx[j];
-                float spillT = tn[j];
-                if (tn[j] < nextT) {
-                    spillN = next;
-                    spillT = nextT;
-                    next = cidx[j];
-                    nextT = tn[j];
-                }
-                if (spillN >= 0) {
-                    if (sp >= RTG_ORD_STACK) return false;            // stack full: reference walk
-                    s_node[sp][tid] = spillN;
-                    s_tn[sp][tid] = spillT;
-                    ++sp;
-                }
-            }
-            if (next >= 0) {
-                node = next;
-                continue;
-            }
-            // pop the nearest remaining entry still in front of the best hit
-            bool found = false;
-            while (sp > 0) {
-                --sp;
-                const float t = s_tn[sp][tid];
-                if (t < bestT * (1.0f + 0x1p-21f)) {
-                    node = s_node[sp][tid];
-                    found = true;
-                    break;
-                }
-                cullMin = fminf(cullMin, t);
-            }
-            if (!found) break;
-        }
-    }
-    if (bestF < 0) return true;                                        // no hit: exact
-    // certificate: the winner's reference leaf box passes exactly at t* (tmin <= t*), and
-    // nothing was culled within 2^-16 of t*
-    if (!(cullMin > bestT * (1.0f + 0x1p-16f))) return false;
-    const int leaf = S.face_leaf[bestF];
-    const float4 a = S.nodes[2 * leaf], b = S.nodes[2 * leaf + 1];
-    if (!box_hit(a.x, a.y, a.z, a.w, b.x, b.y, r, next_up(bestT))) return false;
-    h.t = bestT;
-    h.obj = bestK;
-    h.face = bestF;
-    return true;
-}
 
 // ---------------------------------------------------------------------------
 // Closest hit on the any-hit tree as wave packets (RTG_RENDER_ORDERED, mode 2: the default
@@ -2044,229 +1613,6 @@ DEV bool trace_closest_pk(const DevScene& S, const Ray& r, Hit& h, Cnt<STATS>& c
     h.face = B.bestT < INFINITY ? B.bestF : -1;
     h.o = r.o;
     return sure;
-}
-
-// The same closest-hit walk per lane (incoherent rays: the ray trees' secondary levels): each
-// lane walks the any-hit tree nearest child first with its own LDS stack of node indices (a
-// popped node is culled child by child at the lane's best t then), vector loads of the 128-B
-// node and 48-B face records.  Same certificate as walk_closest_pk; false: reference walk.
-#ifndef RTG_CL_STACK
-#define RTG_CL_STACK 16
-#endif
-template <bool STATS>
-DEV bool walk_closest_lane(const DevScene& S, int node, const int k, const Ray& lr, const RayRcp& q, const SlabRay& sr,
-                           ClosestState& B, Cnt<STATS>& c) {
-    __shared__ int cl_stack[RTG_CL_STACK][256];
-    const int tid = threadIdx.x;
-    int sp = 0;
-    int steps = 0;
-    while (true) {
-        if (++steps > RTG_PK_MAX_STEPS) return false;
-        const WNode* N = S.anodes + node;
-        const float4 lox = N->lox, hix = N->hix, loy = N->loy, hiy = N->hiy, loz = N->loz, hiz = N->hiz;
-        const int4 ch = N->child, lf = N->leaf;
-        c.ewnode();
-        const float minTc = cull_limit(B.bestT);
-        float tn[4];
-        bool h[4], hi[4];
-        h[0] = slab_cons2(lox.x, loy.x, loz.x, hix.x, hiy.x, hiz.x, sr, minTc, tn[0], hi[0]);
-        h[1] = slab_cons2(lox.y, loy.y, loz.y, hix.y, hiy.y, hiz.y, sr, minTc, tn[1], hi[1]);
-        h[2] = slab_cons2(lox.z, loy.z, loz.z, hix.z, hiy.z, hiz.z, sr, minTc, tn[2], hi[2]);
-        h[3] = slab_cons2(lox.w, loy.w, loz.w, hix.w, hiy.w, hiz.w, sr, minTc, tn[3], hi[3]);
-        const int cidx[4] = {ch.x, ch.y, ch.z, ch.w};
-        const int lidx[4] = {lf.x, lf.y, lf.z, lf.w};
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (cidx[j] == WCHILD_EMPTY || cidx[j] >= 0) continue;
-            if (hi[j] & !h[j]) B.cullMin = fminf(B.cullMin, tn[j]);
-            if (!h[j]) continue;
-            const int first = lidx[j] >> 8, cnt = lidx[j] & 255;
-            for (int e = first; e < first + cnt; ++e) {
-                const float4* R = S.ahtris + 3 * (size_t)e;
-                c.template tri<false>();
-                float t;
-                if (!tri_test_fast_rec(R, lr, INFINITY, t)) continue;
-                const float4 r0 = R[0], r1 = R[1];
-                const int f = __float_as_int(r1.w);
-                if (!hit_less(t, k, f, B.bestT, B.bestK, B.bestF)) continue;
-                const int ref = __float_as_int(r0.w);
-                const float4 a = S.nodes[2 * ref], b = S.nodes[2 * ref + 1];
-                if (box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, next_up(t))) {
-                    B.bestT = t; B.bestK = k; B.bestF = f;
-                } else if (box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, INFINITY) &&
-                           hit_less(t, k, f, B.hidT, B.hidK, B.hidF)) {
-                    B.hidT = t; B.hidK = k; B.hidF = f;
-                }
-            }
-        }
-        const float minTc2 = cull_limit(B.bestT);
-        int next = -1;
-        float nextT = INFINITY;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (cidx[j] < 0) continue;
-            if (!(h[j] & (tn[j] < minTc2))) {
-                if (hi[j]) B.cullMin = fminf(B.cullMin, tn[j]);
-                continue;
-            }
-            int spill = cidx[j];
-            if (tn[j] < nextT) {
-                spill = next;
-                next = cidx[j];
-                nextT = tn[j];
-            }
-            if (spill >= 0) {
-                if (sp >= RTG_CL_STACK) return false;
-                cl_stack[sp++][tid] = spill;
-            }
-        }
-        if (next >= 0) {
-            node = next;
-            continue;
-        }
-        if (sp == 0) break;
-        node = cl_stack[--sp][tid];
-    }
-    return true;
-}
-
-template <bool STATS, int FEAT>
-DEV bool trace_closest_lane(const DevScene& S, const Ray& r, Hit& h, Cnt<STATS>& c) {
-    static_assert((FEAT & ~FEAT_SPHERE) == 0, "meshes with identity transforms and spheres only");
-    const RayRcp q = ray_rcp(r);
-    if (!q.fast) return false;
-    const SlabRay sr = slab_ray(r, q);
-    ClosestState B;
-    B.bestT = B.hidT = B.cullMin = INFINITY;
-    B.bestK = B.bestF = B.hidK = B.hidF = 0x7FFFFFFF;
-    for (int k = 0; k < S.num_objects; ++k) {
-        const DevObject& ob = S.objects[k];
-        c.obj();
-        if ((FEAT & FEAT_SPHERE) && ob.kind == OBJ_SPHERE) {
-            c.sph();
-            float t;
-            if (sphere_t(ob, r, B.bestT, t)) { B.bestT = t; B.bestK = k; B.bestF = -1; }
-            continue;
-        }
-        if (ob.aroot < 0) return false;
-        if (!walk_closest_lane<STATS>(S, ob.aroot, k, r, q, sr, B, c)) return false;
-    }
-    if (hit_less(B.hidT, B.hidK, B.hidF, B.bestT, B.bestK, B.bestF)) return false;
-    if (B.bestT < INFINITY && B.cullMin <= B.bestT * (1.0f + 0x1p-16f)) return false;
-    h.t = B.bestT;
-    h.obj = B.bestT < INFINITY ? B.bestK : -1;
-    h.face = B.bestT < INFINITY ? B.bestF : -1;
-    h.o = r.o;
-    return true;
-}
-
-// The same decision on the reference BVH itself, walked from the shadow ray's origin
-// upwards.  A shadow ray starts on the surface it leaves (hit point + eps n), so top-down
-// every ancestor of the origin's leaf is hit and both children are tested at every level;
-// starting at the origin's leaf L0 (the leaf of the hit face) and climbing, only the
-// sibling subtree of each ancestor is walked -- the path boxes are not tested at all (taken
-// as hit: a superset, which the necessary condition allows), nearby subtrees come first
-// (early exit), and L0 plus the siblings' subtrees cover the whole tree whatever L0 is.
-// Boxes are tested conservatively at minT0 (slab_cons); the exact decisions on a leaf's box
-// (at minT0: necessary, at limit: sufficient) are taken only for a face with tri_ok.
-// One mesh (node range [begin, end), local ray lr): from leaf `start` upwards when the ray
-// leaves this object (start >= 0), else top-down.  node_up[i] = (parent, parent's skip).
-// One flat loop (a node visit or a climb per iteration) keeps the wave's lanes in step.
-template <bool STATS>
-DEV int walk_any_up(const DevScene& S, const int begin, const int end, const int start, const Ray& lr,
-                    float minT0, float limit, bool conf, bool& undecided, Cnt<STATS>& c) {
-    const RayRcp q = ray_rcp(lr);
-    if (!q.fast) {                                   // zero / tiny direction component: reference walk
-        undecided = true;
-        return 0;
-    }
-    const float minTc = minT0 * (1.0f + 0x1p-21f);
-    const SlabRay sr = slab_ray(lr, q);
-    const bool up = start >= begin && start < end;
-    int i = up ? start : begin, e = up ? start + 1 : end;   // node range being walked
-    int cur = up ? start : begin, cur_end = up ? start + 1 : end;   // top of the climbed path
-    while (true) {
-        if (i >= e) {
-            if (cur == begin) break;
-            // climb: left child (cur == parent + 1): the right sibling is [cur_end, parent's
-            // end); right child: the left sibling is [parent + 1, cur)
-            const int2 u = S.node_up[cur];
-            const bool left = cur == u.x + 1;
-            i = left ? cur_end : u.x + 1;
-            e = left ? u.y : cur;
-            cur = u.x;
-            cur_end = u.y;
-            continue;
-        }
-        const float4 a = S.nodes[2 * i];
-        const float4 b = S.nodes[2 * i + 1];
-        c.template node<true>();
-        const int skip = __float_as_int(b.z);
-        float tn;
-        const int leaf = __float_as_int(b.w);
-        if (!slab_cons(a.x, a.y, a.z, a.w, b.x, b.y, sr, minTc, tn)) {
-            i = skip;
-            continue;
-        }
-        if (leaf < 0) {
-            i = i + 1;
-            continue;
-        }
-        int first = leaf >> 8, cnt = leaf & 255;
-        if (leaf == LEAF_EXT) {
-            const int2 x = S.node_ext[i];
-            first = x.x;
-            cnt = x.y;
-        }
-        for (int f = first; f < first + cnt; ++f) {
-            c.template tri<true>();
-            float t;
-            if (!tri_test_fast(S, f, lr, limit, t)) continue;
-            if (!box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, minT0)) break;   // leaf unreachable
-            if (conf && box_hit_fast(a.x, a.y, a.z, a.w, b.x, b.y, lr, q, limit)) return 1;
-            undecided = true;
-        }
-        i = skip;
-    }
-    return 0;
-}
-
-// CastShadowRay from the hit (object sobj, face sface) it leaves; returns 1 / 0 / -1.
-template <bool STATS, int FEAT>
-DEV int trace_any_up(const DevScene& S, const Ray& r, float minT0, float limit, int sobj, int sface,
-                     Cnt<STATS>& c) {
-    const RayRcp rq = (FEAT & FEAT_INSTANCE) ? ray_rcp(r) : RayRcp{};
-    if ((FEAT & FEAT_INSTANCE) && !rq.fast) return -1;
-    bool undecided = false;
-    for (int k = 0; k < S.num_objects; ++k) {
-        const DevObject& ob = S.objects[k];
-        if ((FEAT & FEAT_INSTANCE) && ob.group_end > k) {
-            const float4 ga = S.group_box[2 * k], gb = S.group_box[2 * k + 1];
-            if (!box_hit_fast(ga.x, ga.y, ga.z, gb.x, gb.y, gb.z, r, rq, minT0)) {
-                k = ob.group_end - 1;
-                continue;
-            }
-        }
-        c.obj();
-        if ((FEAT & FEAT_SPHERE) && ob.kind == OBJ_SPHERE) {
-            c.sph();
-            Ray lr = trav_ray(ob, r, 0.f);
-            float t;
-            if (sphere_t(ob, lr, limit, t)) return 1;
-            continue;
-        }
-        if (ob.flags & OBJF_SHADOW_SKIP) continue;
-        bool conf = true;
-        if ((FEAT & FEAT_INSTANCE) && ob.kind == OBJ_INSTANCE) {
-            if (!box_hit_fast(ob.bmin[0], ob.bmin[1], ob.bmin[2], ob.bmax[0], ob.bmax[1], ob.bmax[2], r, rq, minT0))
-                continue;
-            conf = box_hit_fast(ob.bmin[0], ob.bmin[1], ob.bmin[2], ob.bmax[0], ob.bmax[1], ob.bmax[2], r, rq, limit);
-        }
-        const Ray lr = (FEAT & FEAT_XFORM) ? trav_ray(ob, r, 0.f) : r;
-        const int start = (k == sobj && sface >= 0) ? S.face_leaf[sface] : -1;
-        if (walk_any_up<STATS>(S, ob.node_begin, ob.node_end, start, lr, minT0, limit, conf, undecided, c)) return 1;
-    }
-    return undecided ? -1 : 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -2906,6 +2252,33 @@ DEV unsigned char ldr(float c) {
     return (unsigned char)(i < 0 ? 0 : (i > 255 ? 255 : i));
 }
 
+// The end of a multi-sample pass for one pixel (RenderParams::slabs): its colours of samples
+// sample0, sample0 + 1, ... (col[j * stride]) added to the accumulator one after the other with
+// the Gaussian sample weights -- the operations, in the order, of one-sample passes
+// (renderThreadMain's spp loop, main.cpp:80-121) -- and after the frame's last sample the pixel
+// itself.  first: the pass starts the render's accumulation.
+DEV void accum_samples(const DevCamera& C, const RenderParams& P, int sample0, int nslab, bool first, bool last,
+                       int pixel, const float4* __restrict__ col, size_t stride, float4* __restrict__ accum,
+                       float* __restrict__ hdr, unsigned char* __restrict__ ldrOut) {
+    float4 a = first ? make_float4(0.f, 0.f, 0.f, 0.f) : accum[pixel];
+    for (int j = 0; j < nslab; ++j) {
+        const float4 c = col[j * stride];
+        const int s = sample0 + j;
+        const float gw = sample_weight(C.spp, s, root_key(P.seed, pixel, s));
+        a.x += c.x * gw;
+        a.y += c.y * gw;
+        a.z += c.z * gw;
+        a.w += gw;
+    }
+    accum[pixel] = a;
+    if (last && !P.accum_only) {
+        const size_t idx = 3 * (size_t)pixel;
+        const float r = a.x / a.w, g = a.y / a.w, b = a.z / a.w;
+        if (hdr) { hdr[idx] = r; hdr[idx + 1] = g; hdr[idx + 2] = b; }
+        if (ldrOut) { ldrOut[idx] = ldr(r); ldrOut[idx + 1] = ldr(g); ldrOut[idx + 2] = ldr(b); }
+    }
+}
+
 // 16x16-pixel tile per 256-thread block, 8x8 per wave; tiles dealt so that consecutive
 // tiles share an XCD (blocks b and b+8 share one under round-robin dispatch).
 // Image row of compact row `crow` of this render's part (RenderParams): compact rows are
@@ -2930,11 +2303,7 @@ DEV int part_pixel(const RenderParams& P, int width, int i) {
 // -- and, through the per-block ordered child appends, their reflected and refracted rays --
 // come from one 8x8 block of the image instead of a 64-pixel strip of a row.  A bijection of
 // [0, width * part_rows) onto the part's pixels.  RTG_TREE_TILES=0: row-major (part_pixel).
-#ifndef RTG_TREE_TILES
-#define RTG_TREE_TILES 1
-#endif
 DEV int tree_pixel(const RenderParams& P, int width, int i) {
-#if RTG_TREE_TILES
     const int band = i / (8 * width), j = i - band * 8 * width;
     const int rb = min(8, P.part_rows - 8 * band);        // rows of this band
     const int fc = width >> 3, full = fc * 8 * rb;         // pixels in whole 8-column chunks
@@ -2949,15 +2318,22 @@ DEV int tree_pixel(const RenderParams& P, int width, int i) {
         y = k / rw;
     }
     return part_row(P, 8 * band + y) * width + x;
-#else
-    return part_pixel(P, width, i);
-#endif
 }
 
-// tile_pixel also returns the compact row (index of the pixel's work-buffer entries:
-// crow * width + px).
-DEV void tile_pixel(const RenderParams& P, int& px, int& py, int& crow) {
-    const int tile = P.tile_map[blockIdx.x];
+// tile_pixel also returns the compact row and the block's sample slab (multi-sample passes,
+// RenderParams::slabs): the pixel's work-buffer entry is slab * slab_px + crow * width + px
+// (work_index).  A padding block of a slab (its index past num_tiles) holds no pixel: px is
+// past every image width.
+DEV void tile_pixel(const RenderParams& P, int& px, int& py, int& crow, int& slab) {
+    slab = (int)(blockIdx.x / (unsigned)P.slab_tiles);
+    const int b = (int)blockIdx.x - slab * P.slab_tiles;
+    if (b >= P.num_tiles) {
+        px = 1 << 24;
+        crow = 0;
+        py = P.row_end;
+        return;
+    }
+    const int tile = P.tile_map[b];
     const int tx = tile % P.tiles_x, ty = tile / P.tiles_x;
     const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
     px = tx * 16 + (w & 1) * 8 + (l & 7);
@@ -2965,8 +2341,16 @@ DEV void tile_pixel(const RenderParams& P, int& px, int& py, int& crow) {
     py = part_row(P, crow);
 }
 DEV void tile_pixel(const RenderParams& P, int& px, int& py) {
-    int crow;
-    tile_pixel(P, px, py, crow);
+    int crow, slab;
+    tile_pixel(P, px, py, crow, slab);
+}
+DEV int work_index(const RenderParams& P, int width, int slab, int crow, int px) {
+    return slab * P.slab_px + crow * width + px;
+}
+// The image pixel of work-buffer entry i of sample slab `slab` (inverse of work_index).
+DEV int work_pixel(const RenderParams& P, int width, int slab, int i) {
+    const int r = i - slab * P.slab_px, crow = r / width;
+    return part_row(P, crow) * width + (r - crow * width);
 }
 
 template <bool STATS>
@@ -3017,21 +2401,7 @@ DEV bool shadow_occluded(const DevScene& S, const WaveBufs& W, size_t q, float4 
     r.d = mk(d.x, d.y, d.z);
     int res = -1;
     if constexpr (FAST) {
-#if RTG_SHADOW_MODE == 1
-        Hit h;
-        res = trace<true, STATS, FEAT, true>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
-#elif RTG_SHADOW_MODE == 2
-        const int slot = W.q_slot[q];
-        const int src = W.num_slots == 1 ? slot : slot / W.num_slots;
-        const int sobj = W.hit_obj ? W.hit_obj[src] : -1;
-        const int sface = sobj >= 0 ? W.hit_face[src] : -1;
-        res = trace_any_up<STATS, FEAT>(S, r, o.w, d.w, sobj, sface, cn);
-#elif RTG_SHADOW_MODE == 3
         res = trace_any_wide<STATS, FEAT>(S, r, o.w, d.w, cn);
-#else
-        Hit h;
-        res = trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
-#endif
         if (res < 0) {                               // undecided: the reference walk
             cn.fallback();
             Hit h;
@@ -3044,23 +2414,9 @@ DEV bool shadow_occluded(const DevScene& S, const WaveBufs& W, size_t q, float4 
     return res > 0;
 }
 
-// Large-leaf scenes pick the shadow walk per pass on the device (GATE): the deferring any-hit
-// walk (GATE 1) when the pass's camera walk reached large leaves with at least defer_any_min
-// lanes (queued, dq_count[0], or tested in the walk, dq_count[3]), else the cooperative
-// reference walk (GATE -1); the other kernel's blocks return at once.  Measured: C3-ton
-// 3 900 -> 5 333 Mrays/s and C4 2 377 -> 2 494 with the deferring walk, C3 5 035 -> 4 400: its
-// cooperative walk stays (profiles/r04p_any_walk_ab.txt).
-DEV bool any_defer_on(const WaveBufs& W) { return W.dq_count[0] + W.dq_count[3] >= W.defer_any_min; }
-template <int GATE>
-DEV bool gate_skip(const WaveBufs& W) {
-    if constexpr (GATE == 0) return false;
-    else return any_defer_on(W) != (GATE > 0);
-}
-
-template <bool STATS, int FEAT, bool FAST, bool DEFER = false, int GATE = 0>
+template <bool STATS, int FEAT, bool FAST, bool DEFER = false>
 __global__ __launch_bounds__(256, FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(FEAT)) void k_shadow(
     const DevScene S, const WaveBufs W, DevCounters* counters) {
-    if (gate_skip<GATE>(W)) return;
     const int k = blockIdx.y * 256 + threadIdx.x;
     const size_t q = ((size_t)blockIdx.x * W.num_slots) * 256 + k;
     Cnt<STATS> cn;
@@ -3072,34 +2428,6 @@ __global__ __launch_bounds__(256, FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(
         } else if (shadow_occluded<STATS, FEAT, FAST>(S, W, q, W.q_o[q], W.q_d[q], cn)) {
             W.occ[W.q_slot[q]] = 1;
         }
-    }
-    flush_counters<STATS>(cn, counters);
-}
-
-// The ray trees' shadow rays on the any-hit tree walked per lane (walk_wide_any: LDS stack per
-// lane; incoherent rays -- the levels below the camera's -- make the wave packet's union of
-// walks large), the reference walk for an undecided ray.  Exact as k_shadow's fast walk.
-#ifndef RTG_LANE_ANY_WAVES
-#define RTG_LANE_ANY_WAVES 5
-#endif
-template <bool STATS, int FEAT>
-__global__ __launch_bounds__(256, RTG_LANE_ANY_WAVES) void k_shadow_lane(const DevScene S, const WaveBufs W,
-                                                                         DevCounters* counters) {
-    const int k = blockIdx.y * 256 + threadIdx.x;
-    const size_t q = ((size_t)blockIdx.x * W.num_slots) * 256 + k;
-    Cnt<STATS> cn;
-    if (k < W.q_count[blockIdx.x]) {
-        const float4 o = W.q_o[q], d = W.q_d[q];
-        Ray r;
-        r.o = mk(o.x, o.y, o.z);
-        r.d = mk(d.x, d.y, d.z);
-        int res = trace_any_wide<STATS, FEAT, false, false>(S, r, o.w, d.w, cn);
-        if (res < 0) {                               // undecided: the reference walk
-            cn.fallback();
-            Hit h;
-            res = trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
-        }
-        if (res > 0) W.occ[W.q_slot[q]] = 1;
     }
     flush_counters<STATS>(cn, counters);
 }

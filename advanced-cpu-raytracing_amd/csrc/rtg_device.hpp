@@ -40,37 +40,27 @@ struct DevObject {
     double baseInvT[12];            // base mesh's inverseTransposeTransform
     int id;                         // Shape::id (XML id; spheres: never a light's id)
     int group_end;                  // first object of an instance group: one past its last member
-    int wroot;                      // (base) mesh's root in the collapsed reference BVH (WNode; ordered walk), -1: none
     int aroot;                      // (base) mesh's root in the any-hit tree (anodes; shadow rays), -1: none
 };
 
 // 4-wide BVH node, 128 B (one cache line pair): the four child boxes as SoA float4 rows, then
-// the child references.  Two trees use it:
-//   * wnodes: the reference's own BVH collapsed to 4 wide -- every child slot a reference node
-//     with its box copied exactly, leaf slots the reference's leaves (child <= -2: reference
-//     node -2 - child, leaf = its (first << 8) | count or LEAF_EXT) -- for the opt-in ordered
-//     closest-hit walk (trace_ordered);
-//   * anodes: the any-hit tree of shadow rays (rtg_ahb.cpp: binned SAH over the reference's
-//     small leaves and the faces of its large ones); leaf slots (child <= -2) hold a range of
-//     ahtris entries, leaf = (first << 8) | count, count <= 255.
+// the child references -- the any-hit tree of shadow rays (anodes; rtg_ahb.cpp: binned SAH over
+// the reference's small leaves and the faces of its large ones); leaf slots (child <= -2) hold a
+// range of ahtris entries, leaf = (first << 8) | count, count <= 255.
 struct WNode {
     float4 lox, hix, loy, hiy, loz, hiz;
     int4 child;                     // >= 0: wide node; WCHILD_EMPTY; <= -2: leaf
     int4 leaf;                      // leaf slots: see above
 };
 enum : int { WCHILD_EMPTY = -1 };
-// Shadow-ray walk of the wavefront pipeline's k_shadow (rtg_common.hpp): 3 = any-hit on the
-// any-hit tree (trace_any_wide; undecided rays take the reference walk: default), 0 = the
-// reference walk per lane, 1 = the same walks as a wave packet (walk_bvh_packet), 2 = any-hit
-// climb from the ray's origin leaf (trace_any_up).  (Round 2's mode 4, the collapsed tree on
-// compressed 64-B nodes, measured slower -- 0.311 vs 0.273 ms -- and was removed.)  The ray-tree pipeline's k_shadow always
-// uses the per-lane reference walk (its secondary rays are incoherent: modes 1-3 measured
-// slower on C5).  Camera rays: RTG_PRIMARY_PACKET -- 2 (default): the reference walk as wave
+// Shadow rays of the wavefront pipeline walk the any-hit tree as wave packets (trace_any_wide;
+// undecided rays take the reference walk); the ray-tree pipeline's k_shadow keeps the per-lane
+// reference walk (its secondary rays are incoherent: the packet walk measured slower on C5).
+// (Rejected shadow walks, removed in round 6: the reference walk as wave packets, an any-hit
+// climb from the ray's origin leaf, round 2's collapsed tree on compressed 64-B nodes.)
+// Camera rays: RTG_PRIMARY_PACKET -- 2 (default): the reference walk as wave
 // packets with scalar-cache records and select face tests (k_primary 0.227 -> 0.205 ms on the
 // headline, profiles/r04c_packet_ab.txt); 1: round 2's packet form; 0: per lane.  DESIGN.md §5.
-#ifndef RTG_SHADOW_MODE
-#define RTG_SHADOW_MODE 3
-#endif
 #ifndef RTG_PRIMARY_PACKET
 #define RTG_PRIMARY_PACKET 2
 #endif
@@ -170,14 +160,12 @@ struct DevScene {
     float ambient[3];
     int background[3];
     int coop;                        // the scene has large leaves (FEAT_BIGLEAF)
-    const WNode* __restrict__ wnodes;  // collapsed reference BVH (ordered walk; null: none)
     const WNode* __restrict__ anodes;  // any-hit tree (null: shadow rays take the reference walk)
     const float4* __restrict__ ahtris; // its leaf entries: face record, reference leaf node in [0].w
-    const int2* __restrict__ node_up;  // per node: (parent, parent's skip); null: no up-walk
     const int* __restrict__ face_leaf; // per face: its leaf node
     int exact_shadow;                  // RTG_RENDER_EXACT_SHADOW: shadow rays take the reference walk
     int ahb_split;                     // the any-hit tree splits large leaves (AHB_SPLIT)
-    int ordered;                       // RTG_RENDER_ORDERED (plain mesh scenes with a wide BVH)
+    int ordered;                       // RTG_RENDER_ORDERED (plain mesh scenes with an any-hit tree)
     // RTG_GUARD builds (fault hunting): table sizes and a violation bit mask (rtg_common.hpp GIDX)
     int* guard;
     int num_faces, num_textures, num_images, num_materials;
@@ -204,6 +192,16 @@ struct RenderParams {
     int part_index, part_count, part_rows;
     unsigned long long seed;
     const int* __restrict__ tile_map;   // block -> 16x16 tile of this part (host-built, XCD-aware)
+    // Multi-sample passes (wavefront and ray-tree pipelines): one pass carries `slabs`
+    // consecutive samples of the part's pixels, so a small part still fills the GPU.  Sample
+    // slab j of a pass is blocks [j * slab_tiles, (j + 1) * slab_tiles) of the tile grids
+    // (slab_tiles = num_tiles rounded up to the 8 XCDs, so a tile keeps its XCD in every slab;
+    // the padding blocks hold no pixels) and work-buffer entries [j * slab_px, (j + 1) * slab_px)
+    // (slab_px = 16 * tiles_y * width; the ray trees' level 0: j * width * part_rows).  A pass's
+    // colours go to a per-(slab, pixel) buffer and k_accum adds them to the pixel in sample
+    // order, so the image is the one-sample passes' bit for bit.  slabs = 1: one sample per pass
+    // (no colour buffer; tile grids of num_tiles blocks).
+    int slabs, slab_tiles, slab_px;
 };
 
 // Wavefront pipeline buffers (rtg_wave.hip), one entry per pixel of the rendered rows
@@ -222,6 +220,7 @@ struct WaveBufs {
     int* __restrict__ q_slot;           // light slot it decides
     int* __restrict__ q_count;          // per block: entries in its segment
     float4* __restrict__ accum;         // multi-sample: sum w*c, sum w
+    float4* __restrict__ col;           // multi-sample passes: colour per (slab, pixel) entry (k_accum)
     // one-slot scenes (at most one light): per queue entry the pixel's base colour + flags
     // and its light term + pixel index, so k_shadow finishes the pixel itself (no k_resolve)
     float4* __restrict__ q_pay;
@@ -230,9 +229,7 @@ struct WaveBufs {
     // leaf it reaches to a queue of (ray, leaf, minT at entry) entries, 3 float4 each, tested by
     // k_bigleaf; per pixel the 64-bit (t, object, face) key of the best hit so far
     float4* __restrict__ dq_e;
-    int* __restrict__ dq_count;         // [0] camera entries, [1] unsettled pixels, [2] shadow entries,
-                                        // [3] camera lanes testing large leaves in the walk
-    int defer_any_min;                  // shadow walk choice (GATE): large-leaf lanes of the camera pass
+    int* __restrict__ dq_count;         // [0] camera entries, [1] unsettled pixels, [2] shadow entries
     unsigned long long* __restrict__ hit_key;
     int* __restrict__ shadow_state;     // per shadow queue entry: SS_* bits (deferred any-hit)
     int dq_cap;

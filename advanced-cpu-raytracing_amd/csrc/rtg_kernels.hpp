@@ -10,7 +10,6 @@ namespace rtg {
 int max_supported_depth();
 // large leaves of the camera walk deferred to k_bigleaf (rtg_wave_shade.hip; RTG_DEFER=0: off)
 bool defer_leaves();
-int defer_any_gate();
 // FNV-1a of a camera's device record (view, image size, samples, renderer flags): the ray-tree and
 // path plans are kept per frame part of one camera
 inline unsigned long long camera_hash(const DevCamera& C) {

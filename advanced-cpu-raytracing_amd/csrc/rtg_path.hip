@@ -20,20 +20,12 @@
 // The node steps are rtg_node.hpp's, the same code the fused kernel runs, with the same RNG
 // keys, so the image is bit-identical to the fused kernel's.
 //
-// Split step (opt-in, RTG_PATH_SPLIT=1; the default is the single k_path_step above): the step is
-// three kernels by node kind, so none carries all of the shading --
-//     k_path_hit     a traced path's hit node up to shade_rest (surface, the GI ray: spawned
-//                    and pushed), or its miss; nodes needing shade_rest go to the rest queue,
-//                    finished values to the unwind queue
-//     k_path_rest    shade_rest (ambient + direct lighting with its shadow walk + the material's
-//                    first child) from the stored RestArgs
-//     k_path_unwind  hands finished values up the stack (resume_pre), a frame that needs
-//                    shade_rest goes to the next iteration's rest queue; a finished path writes
-//                    its pixel
-// Every path sits in one queue at a time (trace T, rest R, unwind U); its RestArgs (112 B) or
-// ChildVal (32 B) wait in HBM by path index.
+// (Round 4's split step -- three kernels by node kind at two waves per SIMD each -- was
+// bit-identical and slower, pt_cornell 2 588 -> 1 441 Mrays/s, profiles/r04v_ptwave_split.txt:
+// every unwinding level that needs shade_rest cost an iteration of four launches where the single
+// kernel unwinds in place; removed in round 6.)
 //
-// Path regeneration (single step kernel, cameras with Russian roulette; RTG_PATH_REGEN=1 / 0
+// Path regeneration (cameras with Russian roulette; RTG_PATH_REGEN=1 / 0
 // forces it on / off): a pass covers all of the render's samples.  Path slot i is pixel i of the chunk; when
 // its sample finishes, the step kernel accumulates it and starts the slot's next sample (its
 // camera ray) in the same iteration, so the queue stays full until the last samples and each
@@ -88,15 +80,8 @@ struct PathBufs {
     float* ht;          // closest hits by queue position
     int* hobj;
     int* hface;
-    float4* rest;       // split step: RestArgs + frame level by path (kRestChunks planes)
-    float4* val;        // split step: ChildVal + stack depth + miss flag by path (2 planes)
-    int* ract0;         // split step: rest queues (even / odd iterations)
-    int* ract1;
-    int* uact;          // split step: unwind queue (one iteration)
-    int* rcnt;          // per iteration: rest queue sizes; [kPathMaxIter + 2 ...]: unwind queue sizes
     int cap;            // paths per pass
 };
-constexpr int kRestChunks = 7;
 
 DEV size_t chunk_at(const PathBufs& B, int lv, int k, int i) {
     return ((size_t)lv * kFrameChunks + k) * (size_t)B.cap + i;
@@ -341,276 +326,9 @@ __global__ __launch_bounds__(256, RTG_PATH_STEP_WAVES) void k_path_step(
     flush_counters<STATS>(cn, counters);
 }
 
-// ---------------------------------------------------------------------------
-// Split step (RTG_PATH_SPLIT=1)
-// ---------------------------------------------------------------------------
-#ifndef RTG_PATH_HIT_WAVES
-#define RTG_PATH_HIT_WAVES 2
-#endif
-#ifndef RTG_PATH_REST_WAVES
-#define RTG_PATH_REST_WAVES 2
-#endif
-#ifndef RTG_PATH_UNWIND_WAVES
-#define RTG_PATH_UNWIND_WAVES 2
-#endif
-
-// wave-aggregated append of `path` to queue q (count *cnt) for the lanes with `on`; every
-// lane of the wave calls it
-DEV void q_append(int* q, int* cnt, bool on, int path) {
-    const unsigned long long mask = __ballot(on);
-    if (!mask) return;
-    const int lane = threadIdx.x & 63;
-    const int leader = __ffsll((long long)mask) - 1;
-    int qb = 0;
-    if (lane == leader) qb = atomicAdd(cnt, __popcll(mask));
-    qb = __shfl(qb, leader);
-    if (on) q[qb + __popcll(mask & ((1ull << lane) - 1ull))] = path;
-}
-
-DEV void rest_store(const DevScene& S, const PathBufs& B, int i, const RestArgs& a, int level) {
-    const size_t c = (size_t)B.cap;
-    float4* R = B.rest;
-    R[0 * c + i] = make_float4(a.c.s.p.x, a.c.s.p.y, a.c.s.p.z, a.c.s.u);
-    R[1 * c + i] = make_float4(a.c.s.n.x, a.c.s.n.y, a.c.s.n.z, a.c.s.v);
-    R[2 * c + i] = make_float4(a.w_o.x, a.w_o.y, a.w_o.z, a.medium);
-    R[3 * c + i] = make_float4(a.tp.x, a.tp.y, a.tp.z, a.t);
-    R[4 * c + i] = make_float4(a.color.x, a.color.y, a.color.z, a.mbTime);
-    R[5 * c + i] = make_float4(__uint_as_float((unsigned)a.key), __uint_as_float((unsigned)(a.key >> 32)),
-                               __int_as_float((int)(a.c.ob - S.objects)), __int_as_float((int)(a.c.mat - S.materials)));
-    R[6 * c + i] = make_float4(__int_as_float(a.depth), __int_as_float(a.skip), __int_as_float(level), 0.f);
-}
-
-DEV int rest_load(const DevScene& S, const PathBufs& B, int i, RestArgs& a) {
-    const size_t c = (size_t)B.cap;
-    const float4* R = B.rest;
-    const float4 r0 = R[0 * c + i], r1 = R[1 * c + i], r2 = R[2 * c + i], r3 = R[3 * c + i], r4 = R[4 * c + i];
-    const float4 r5 = R[5 * c + i], r6 = R[6 * c + i];
-    a.c.s.p = mk(r0.x, r0.y, r0.z);
-    a.c.s.u = r0.w;
-    a.c.s.n = mk(r1.x, r1.y, r1.z);
-    a.c.s.v = r1.w;
-    a.w_o = mk(r2.x, r2.y, r2.z);
-    a.medium = r2.w;
-    a.tp = mk(r3.x, r3.y, r3.z);
-    a.t = r3.w;
-    a.color = mk(r4.x, r4.y, r4.z);
-    a.mbTime = r4.w;
-    a.key = (uint64_t)__float_as_uint(r5.x) | ((uint64_t)__float_as_uint(r5.y) << 32);
-    a.c.ob = S.objects + __float_as_int(r5.z);
-    a.c.mat = S.materials + __float_as_int(r5.w);
-    a.depth = __float_as_int(r6.x);
-    a.skip = __float_as_int(r6.y);
-    return __float_as_int(r6.z);
-}
-
-// a finished value waiting for the unwind kernel: sp frames below it; miss: the pending ray of
-// the frame at sp - 1 missed (its value is the frame's miss_value, taken with the frame loaded)
-DEV void val_store(const PathBufs& B, int i, const ChildVal& v, int sp, bool miss) {
-    const size_t c = (size_t)B.cap;
-    B.val[i] = make_float4(v.value.x, v.value.y, v.value.z, v.t);
-    B.val[c + i] = make_float4(v.medium, __int_as_float((int)v.hit), __int_as_float(sp), __int_as_float((int)miss));
-}
-
-DEV void pending_store(const PathBufs& B, int path, const Pending& p, int sp) {
-    B.ro[path] = make_float4(p.R.o.x, p.R.o.y, p.R.o.z, p.medium);
-    B.rd[path] = make_float4(p.R.d.x, p.R.d.y, p.R.d.z, __int_as_float(p.depth));
-    B.key[path] = p.key;
-    B.tp[path] = make_float4(p.tp.x, p.tp.y, p.tp.z, __int_as_float(p.pend | (sp << 8)));
-}
-
-DEV int* rest_queue(const PathBufs& B, int it) { return (it & 1) ? B.ract1 : B.ract0; }
-DEV int* unwind_count(const PathBufs& B, int it) { return B.rcnt + (kPathMaxIter + 2) + it; }
-
-// The traced paths of iteration `it`: their hit nodes up to shade_rest, or their misses.
-template <bool STATS, int SK>
-__global__ __launch_bounds__(256, RTG_PATH_HIT_WAVES) void k_path_hit(const DevScene S, const DevCamera C,
-                                                                      const RenderParams P, const PathBufs B,
-                                                                      const int it, const int base, const int maxd,
-                                                                      DevCounters* counters) {
-    const int* act = (it & 1) ? B.act1 : B.act0;
-    int* nact = (it & 1) ? B.act0 : B.act1;
-    const int n = B.cnt[it];
-    const f3 cpos = ld3(C.pos);
-    Cnt<STATS> cn;
-    for (int i0 = blockIdx.x * 256; i0 < n; i0 += gridDim.x * 256) {
-        const int i = i0 + threadIdx.x;
-        bool toT = false, toR = false, toU = false;
-        int path = 0;
-        if (i < n) {
-            path = act[i];
-            const float4 o = B.ro[path], d = B.rd[path], t4 = B.tp[path];
-            Pending p;
-            p.R.o = mk(o.x, o.y, o.z);
-            p.R.d = mk(d.x, d.y, d.z);
-            p.medium = o.w;
-            p.depth = __float_as_int(d.w);
-            p.key = B.key[path];
-            p.tp = mk(t4.x, t4.y, t4.z);
-            const int ps = __float_as_int(t4.w);
-            p.pend = ps & 255;
-            int sp = (ps >> 8) & 255;
-            Node cur;
-            cur.h.t = B.ht[i];
-            cur.h.obj = B.hobj[i];
-            cur.h.face = B.hface[i];
-            cur.h.o = p.R.o;
-            const bool hit = cur.h.obj >= 0;
-            ChildVal v;
-            v.t = 0.f;
-            v.medium = 1.f;
-            v.hit = false;
-            v.value = mk(0, 0, 0);
-            if (p.pend == 0 && !hit) {
-                const int pixel = part_pixel(P, C.width, base + path);
-                v.value = miss_color<SK>(S, C, pixel % C.width, pixel / C.width, p.R.d);
-                val_store(B, path, v, 0, false);
-                toU = true;
-            } else {
-                if (p.pend == 3) frame_store_skip(B, sp - 1, path, emissive_hit_id(S, cur.h, hit));
-                if (hit) {
-                    cur.r = p.R;
-                    cur.eye = p.pend == 0 ? cpos : p.R.o;
-                    cur.medium = p.medium;
-                    cur.mbTime = 0.f;
-                    cur.depth = p.depth;
-                    cur.key = p.key;
-                    cur.tp = p.tp;
-                    FramePT f;
-                    Child ch;
-                    RestArgs a;
-                    const int r = shade_node_pre<STATS, true, SK>(S, C, cur, sp, maxd, v.value, f, ch, a, cn);
-                    if (r == NS_SPAWN) {
-                        spawn_child<STATS, true>(f, ch, p, cn);
-                        frame_store(B, sp, path, f);
-                        pending_store(B, path, p, sp + 1);
-                        toT = true;
-                    } else if (r == NS_REST) {
-                        rest_store(S, B, path, a, sp);
-                        toR = true;
-                    } else {
-                        v.hit = true;
-                        v.t = cur.h.t;
-                        v.medium = cur.medium;
-                        val_store(B, path, v, sp, false);
-                        toU = true;
-                    }
-                } else {
-                    val_store(B, path, v, sp, true);              // the frame's miss_value, in k_path_unwind
-                    toU = true;
-                }
-            }
-        }
-        q_append(nact, B.cnt + it + 1, toT, path);
-        q_append(rest_queue(B, it), B.rcnt + it, toR, path);
-        q_append(B.uact, unwind_count(B, it), toU, path);
-    }
-    flush_counters<STATS>(cn, counters);
-}
-
-// shade_rest for the rest queue of iteration `it`.
-template <bool STATS, int SK, int FEAT>
-__global__ __launch_bounds__(256, RTG_PATH_REST_WAVES) void k_path_rest(const DevScene S, const DevCamera C,
-                                                                        const PathBufs B, const int it,
-                                                                        DevCounters* counters) {
-    const int* rq = rest_queue(B, it);
-    int* nact = (it & 1) ? B.act0 : B.act1;
-    const int n = B.rcnt[it];
-    Cnt<STATS> cn;
-    for (int i0 = blockIdx.x * 256; i0 < n; i0 += gridDim.x * 256) {
-        const int i = i0 + threadIdx.x;
-        bool toT = false, toU = false;
-        int path = 0;
-        if (i < n) {
-            path = rq[i];
-            RestArgs a;
-            const int level = rest_load(S, B, path, a);
-            FramePT f;
-            Child ch;
-            f3 out;
-            const bool spawned = rest_call<STATS, true, SK, FEAT>(S, C, a, out, f, ch, cn);
-            Pending p;
-            ChildVal v;
-            rest_done<STATS, true>(spawned, a, f, ch, out, p, v, cn);
-            if (spawned) {
-                frame_store(B, level, path, f);
-                pending_store(B, path, p, level + 1);
-                toT = true;
-            } else {
-                val_store(B, path, v, level, false);
-                toU = true;
-            }
-        }
-        q_append(nact, B.cnt + it + 1, toT, path);
-        q_append(B.uact, unwind_count(B, it), toU, path);
-    }
-    flush_counters<STATS>(cn, counters);
-}
-
-// Finished values of iteration `it` handed up their stacks.
-template <bool STATS, int SK>
-__global__ __launch_bounds__(256, RTG_PATH_UNWIND_WAVES) void k_path_unwind(
-    const DevScene S, const DevCamera C, const RenderParams P, const PathBufs B, const int it, const int sample,
-    const int first, const int last, const int base, float* __restrict__ hdr, unsigned char* __restrict__ ldrOut,
-    float4* __restrict__ accum, DevCounters* counters) {
-    int* nact = (it & 1) ? B.act0 : B.act1;
-    const int n = *unwind_count(B, it);
-    Cnt<STATS> cn;
-    for (int i0 = blockIdx.x * 256; i0 < n; i0 += gridDim.x * 256) {
-        const int i = i0 + threadIdx.x;
-        bool toT = false, toR = false;
-        int path = 0;
-        if (i < n) {
-            path = B.uact[i];
-            const float4 v0 = B.val[path], v1 = B.val[(size_t)B.cap + path];
-            ChildVal v;
-            v.value = mk(v0.x, v0.y, v0.z);
-            v.t = v0.w;
-            v.medium = v1.x;
-            v.hit = __float_as_int(v1.y) != 0;
-            int sp = __float_as_int(v1.z);
-            FramePT f;
-            bool have = false;
-            if (__float_as_int(v1.w)) {                          // the pending ray of frame sp - 1 missed
-                frame_load(B, sp - 1, path, f);
-                have = true;
-                const float4 d = B.rd[path];
-                v.value = miss_value<true, SK>(S, f, mk(d.x, d.y, d.z));
-                v.hit = false;
-            }
-            while (true) {
-                if (sp == 0) {
-                    path_pixel(C, P, sample, first, last, part_pixel(P, C.width, base + path), v.value, hdr, ldrOut,
-                               accum);
-                    break;
-                }
-                if (!have) frame_load(B, sp - 1, path, f);
-                have = false;
-                Pending p;
-                RestArgs a;
-                const int r = resume_pre<STATS, true, SK>(S, C, f, v, p, a, cn);
-                if (r == NS_SPAWN) {
-                    frame_store(B, sp - 1, path, f);
-                    pending_store(B, path, p, sp);
-                    toT = true;
-                    break;
-                }
-                if (r == NS_REST) {
-                    rest_store(S, B, path, a, sp - 1);
-                    toR = true;
-                    break;
-                }
-                --sp;
-            }
-        }
-        q_append(nact, B.cnt + it + 1, toT, path);
-        q_append(rest_queue(B, it + 1), B.rcnt + it + 1, toR, path);
-    }
-    flush_counters<STATS>(cn, counters);
-}
-
 // paths left after a planned pass's last iteration: the plan was too short
-__global__ void k_path_check(int* cnt, int* rcnt, int last_it) {
-    if (threadIdx.x == 0 && (cnt[last_it] != 0 || (rcnt && rcnt[last_it] != 0))) cnt[kPathMaxIter + 1] = 1;
+__global__ void k_path_check(int* cnt, int last_it) {
+    if (threadIdx.x == 0 && cnt[last_it] != 0) cnt[kPathMaxIter + 1] = 1;
 }
 
 // ---------------------------------------------------------------------------
@@ -620,15 +338,14 @@ struct PathState {
     PathBufs B{};
     size_t cap = 0;                 // paths the buffers hold
     int levels = 0;                 // frame levels the buffers hold
-    int* h = nullptr;               // pinned host words: [0] a queue size, [1] the overflow flag, [2] a rest queue size
+    int* h = nullptr;               // pinned host words: [0] a queue size, [1] the overflow flag
     std::vector<int> plan;          // grid paths per iteration of planned passes
-    std::vector<int> rplan;         // split step: rest-queue entries carried into each iteration
     std::vector<long long> plan_key;
     ~PathState() { release(); if (h) (void)hipHostFree(h); }
     void release() {
         auto f = [](void* p) { if (p) (void)hipFree(p); };
         f(B.ro); f(B.rd); f(B.key); f(B.tp); f(B.frames); f(B.act0); f(B.act1); f(B.cnt); f(B.ht); f(B.hobj);
-        f(B.hface); f(B.rest); f(B.val); f(B.ract0); f(B.ract1); f(B.uact); f(B.rcnt);
+        f(B.hface);
         B = PathBufs{};
         cap = 0;
         levels = 0;
@@ -654,9 +371,6 @@ static hipError_t ensure_paths(PathState& T, size_t n, int levels) {
     A_(T.B.frames, n * (size_t)levels * kFrameChunks * 16);
     A_(T.B.act0, n * 4); A_(T.B.act1, n * 4); A_(T.B.cnt, (kPathMaxIter + 2) * sizeof(int));
     A_(T.B.ht, n * 4); A_(T.B.hobj, n * 4); A_(T.B.hface, n * 4);
-    A_(T.B.rest, n * kRestChunks * 16); A_(T.B.val, n * 2 * 16);
-    A_(T.B.ract0, n * 4); A_(T.B.ract1, n * 4); A_(T.B.uact, n * 4);
-    A_(T.B.rcnt, 2 * (kPathMaxIter + 2) * sizeof(int));
 #undef A_
     T.B.cap = (int)n;
     T.cap = n;
@@ -672,72 +386,55 @@ using TraceFn = void (*)(const DevScene, const PathBufs, const int, DevCounters*
 using StepFn = void (*)(const DevScene, const DevCamera, const RenderParams, const PathBufs, const int, const int,
                         const int, const int, const int, const int, const int, float*, unsigned char*, float4*,
                         DevCounters*);
-using HitFn = void (*)(const DevScene, const DevCamera, const RenderParams, const PathBufs, const int, const int,
-                      const int, DevCounters*);
-using RestFn = void (*)(const DevScene, const DevCamera, const PathBufs, const int, DevCounters*);
-using UnwindFn = void (*)(const DevScene, const DevCamera, const RenderParams, const PathBufs, const int, const int,
-                         const int, const int, const int, float*, unsigned char*, float4*, DevCounters*);
 struct PathKernels {
     GenFn gen;
     TraceFn trace;
-    StepFn step;          // single step kernel (split == false)
-    HitFn hit;            // split step
-    RestFn rest;
-    UnwindFn unwind;
-    bool split;
+    StepFn step;
 };
 
+// Iterations a pass may take: kPathMaxIter, or fewer with RTG_PATH_ITER_CAP (tests: the bound
+// reached by short passes)
+static int path_iter_cap() {
+    const char* v = std::getenv("RTG_PATH_ITER_CAP");
+    const int c = v ? std::atoi(v) : kPathMaxIter;
+    return c > 0 && c < kPathMaxIter ? c : kPathMaxIter;
+}
+
 // One pass over paths [base, base + n) of the frame part: samples [s, s + count) of each path
-// (count > 1: regeneration, single step kernel only).  plan == nullptr: host-driven (one
-// synchronisation per iteration; `seen` receives the queue sizes); otherwise the plan's
-// iterations, no synchronisation.
+// (count > 1: regeneration).  plan == nullptr: host-driven (one synchronisation per iteration;
+// `seen` receives the queue sizes); otherwise the plan's iterations, no synchronisation.
 static hipError_t path_pass(PathState& T, const PathKernels& K, const DevScene& S, const DevCamera& C,
                             const RenderParams& P, int maxd, int s, int count, int base, int n, float* hdr,
                             unsigned char* l, float4* accum, DevCounters* cnt, hipStream_t st, hipEvent_t* ev,
-                            const PathState* plan, std::vector<int>& seen, std::vector<int>& rseen) {
+                            const PathState* plan, std::vector<int>& seen) {
     hipError_t e;
     const PathBufs& B = T.B;
     if ((e = hipMemsetAsync(B.cnt, 0, (kPathMaxIter + 1) * sizeof(int), st)) != hipSuccess) return e;
-    if (K.split && (e = hipMemsetAsync(B.rcnt, 0, 2 * (kPathMaxIter + 2) * sizeof(int), st)) != hipSuccess) return e;
     if (ev) (void)hipEventRecord(ev[0], st);
     hipLaunchKernelGGL(K.gen, dim3((n + 255) / 256), dim3(256), 0, st, C, P, B, s, base, n, S.max_depth, cnt);
-    // paths: traced paths of the iteration; rpaths: rest entries carried into it (split step)
-    auto iteration = [&](int it, long long paths, long long rpaths) {
+    auto iteration = [&](int it, long long paths) {
         const int g = grid_for(paths);
         hipLaunchKernelGGL(K.trace, dim3(g), dim3(256), 0, st, S, B, it, cnt);
-        if (!K.split) {
-            hipLaunchKernelGGL(K.step, dim3(g), dim3(256), 0, st, S, C, P, B, it, s, P.sample_begin,
-                               P.sample_begin + P.sample_count - 1, count, base, maxd, hdr, l, accum, cnt);
-            return;
-        }
-        const int g2 = grid_for(std::min<long long>(n, paths + rpaths));
-        hipLaunchKernelGGL(K.hit, dim3(g), dim3(256), 0, st, S, C, P, B, it, base, maxd, cnt);
-        hipLaunchKernelGGL(K.rest, dim3(g2), dim3(256), 0, st, S, C, B, it, cnt);
-        hipLaunchKernelGGL(K.unwind, dim3(g2), dim3(256), 0, st, S, C, P, B, it, s, (int)(s == P.sample_begin),
-                           (int)(s == P.sample_begin + P.sample_count - 1), base, hdr, l, accum, cnt);
+        hipLaunchKernelGGL(K.step, dim3(g), dim3(256), 0, st, S, C, P, B, it, s, P.sample_begin,
+                           P.sample_begin + P.sample_count - 1, count, base, maxd, hdr, l, accum, cnt);
     };
     if (plan) {
         const int D = (int)plan->plan.size();
-        for (int it = 0; it < D; ++it) iteration(it, plan->plan[it], K.split ? plan->rplan[it] : 0);
-        hipLaunchKernelGGL(k_path_check, dim3(1), dim3(64), 0, st, B.cnt, K.split ? B.rcnt : nullptr, D);
+        if (D > path_iter_cap()) return hipErrorInvalidValue;   // (path_run caps its plans)
+        for (int it = 0; it < D; ++it) iteration(it, plan->plan[it]);
+        hipLaunchKernelGGL(k_path_check, dim3(1), dim3(64), 0, st, B.cnt, D);
     } else {
-        long long paths = n, rpaths = 0;
+        long long paths = n;
         seen.assign(1, n);
-        rseen.assign(1, 0);
         for (int it = 0;; ++it) {
-            if (it >= kPathMaxIter) return hipErrorNotSupported;   // the fused kernel takes the render
-            iteration(it, paths, rpaths);
+            if (it >= path_iter_cap()) return hipErrorNotSupported;   // the fused kernel takes the render
+            iteration(it, paths);
             if ((e = hipMemcpyAsync(T.h, B.cnt + it + 1, sizeof(int), hipMemcpyDeviceToHost, st)) != hipSuccess)
-                return e;
-            if (K.split && (e = hipMemcpyAsync(T.h + 2, B.rcnt + it + 1, sizeof(int), hipMemcpyDeviceToHost, st)) !=
-                               hipSuccess)
                 return e;
             if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
             paths = T.h[0];
-            rpaths = K.split ? T.h[2] : 0;
-            if (paths == 0 && rpaths == 0) break;
+            if (paths == 0) break;
             seen.push_back((int)paths);
-            rseen.push_back((int)rpaths);
         }
     }
     if (ev) (void)hipEventRecord(ev[1], st);
@@ -748,12 +445,11 @@ static hipError_t path_pass(PathState& T, const PathKernels& K, const DevScene& 
 static bool path_sync_only() { return std::getenv("RTG_PATH_SYNC") != nullptr; }
 
 // samples per pass: all of the render's with regeneration (Russian roulette, or
-// RTG_PATH_REGEN=1; the split step has none), at most 64 so a pass's iterations stay well inside
-// kPathMaxIter; one otherwise
+// RTG_PATH_REGEN=1), at most 64; one otherwise
 static int path_pass_samples(const PathKernels& K, const DevCamera& C, const RenderParams& P) {
     const char* v = std::getenv("RTG_PATH_REGEN");
     const bool regen = v ? std::strcmp(v, "0") != 0 : C.russian_roulette != 0;
-    if (K.split || !regen) return 1;
+    if (!regen) return 1;
     return std::max(1, std::min(P.sample_count, 64));
 }
 
@@ -765,7 +461,7 @@ static hipError_t path_run(PathState& T, const PathKernels& K, bool stats, const
     const int npix = P.part_rows * C.width;
     // paths per pass: up to 2^20, and at most half the device memory free now (the frame stacks:
     // 208 B x maxd levels per path -- 6.9 GB at 2^20 paths x 32 levels)
-    const size_t per_path = (size_t)maxd * kFrameChunks * 16 + 96 + (kRestChunks + 2) * 16 + 12;
+    const size_t per_path = (size_t)maxd * kFrameChunks * 16 + 96;
     size_t mem_free = 0, mem_total = 0;
     if (hipMemGetInfo(&mem_free, &mem_total) != hipSuccess) {
         (void)hipGetLastError();
@@ -778,7 +474,7 @@ static hipError_t path_run(PathState& T, const PathKernels& K, bool stats, const
     if ((e = ensure_paths(T, (size_t)chunk, maxd)) != hipSuccess) return e;
     const std::vector<long long> key = {P.row_begin, P.row_end, P.part_index, P.part_count, C.width, C.height,
                                         (long long)(size_t)S.objects, S.max_depth, (long long)chunk, maxd,
-                                        (long long)camera_hash(C), (long long)K.split, (long long)per_pass};
+                                        (long long)camera_hash(C), (long long)per_pass};
     for (int attempt = 0; attempt < 2; ++attempt) {
         // attempt 0: planned passes when this frame part has a plan (the first pass otherwise
         // host-driven, planning the rest); attempt 1 (a plan was too short): host-driven.
@@ -787,16 +483,16 @@ static hipError_t path_run(PathState& T, const PathKernels& K, bool stats, const
         bool planned = adapt && T.plan_key == key && !T.plan.empty();
         bool any_planned = false;
         if ((e = hipMemsetAsync(T.B.cnt + kPathMaxIter + 1, 0, sizeof(int), st)) != hipSuccess) return e;
-        std::vector<int> seen_max, rseen_max;
+        std::vector<int> seen_max;
         for (int base = 0; base < npix; base += chunk) {
             const int n = std::min(chunk, npix - base);
             const int s_end = P.sample_begin + P.sample_count;
             for (int s = P.sample_begin; s < s_end; s += per_pass) {
                 const int count = std::min(per_pass, s_end - s);
                 hipEvent_t* pev = (s + count == s_end && base + chunk >= npix) ? ev : nullptr;
-                std::vector<int> seen, rseen;
+                std::vector<int> seen;
                 e = path_pass(T, K, S, C, P, maxd, s, count, base, n, hdr, l, accum, cnt, st, pev,
-                              planned ? &T : nullptr, seen, rseen);
+                              planned ? &T : nullptr, seen);
                 if (e != hipSuccess) return e;
                 if (planned) {
                     any_planned = true;
@@ -804,8 +500,6 @@ static hipError_t path_run(PathState& T, const PathKernels& K, bool stats, const
                 }
                 if (seen.size() > seen_max.size()) seen_max.resize(seen.size(), 0);
                 for (size_t k = 0; k < seen.size(); ++k) seen_max[k] = std::max(seen_max[k], seen[k]);
-                if (rseen.size() > rseen_max.size()) rseen_max.resize(rseen.size(), 0);
-                for (size_t k = 0; k < rseen.size(); ++k) rseen_max[k] = std::max(rseen_max[k], rseen[k]);
                 if (adapt) {
                     // the queue sizes seen with a margin, and a few more iterations (sampled
                     // trees vary between passes; an empty iteration costs two short launches).
@@ -813,19 +507,23 @@ static hipError_t path_run(PathState& T, const PathKernels& K, bool stats, const
                     // every planned pass leaves paths and the render is redone host-driven
                     const bool tight = std::getenv("RTG_PATH_PLAN_TIGHT") != nullptr;
                     T.plan.clear();
-                    T.rplan.clear();
                     for (size_t k = 0; k < seen_max.size(); ++k) {
                         T.plan.push_back((int)std::min<long long>(n, seen_max[k] + seen_max[k] / 4 + 1024));
-                        T.rplan.push_back((int)std::min<long long>(n, rseen_max[k] + rseen_max[k] / 4 + 1024));
                     }
                     const int extra = tight ? 0 : std::max(4, (int)seen_max.size() / 4);
                     for (int k = 0; k < extra; ++k) {
                         T.plan.push_back(T.plan.back());
-                        T.rplan.push_back(T.rplan.back());
                     }
                     if (tight && T.plan.size() > 1) {
                         T.plan.pop_back();
-                        T.rplan.pop_back();
+                    }
+                    // at most kPathMaxIter iterations: the per-iteration counters (cnt) end
+                    // there.  A pass that needs more leaves paths after the last planned
+                    // iteration; k_path_check flags it and the render is redone host-driven,
+                    // which hands a pass that long to the fused kernel (hipErrorNotSupported)
+                    const size_t cap = (size_t)path_iter_cap();
+                    if (T.plan.size() > cap) {
+                        T.plan.resize(cap);
                     }
                     T.plan_key = key;
                     planned = true;
@@ -871,63 +569,19 @@ static StepFn step_kernel(int sk, int feat) {
     return step_kernel_sk<SK_ALL>(feat);
 }
 
-// split step kernels: the same feature variants as step_kernel
-template <int SK>
-static RestFn rest_kernel_sk(int feat) {
-    if (feat & (FEAT_INSTANCE | FEAT_XFORM)) return k_path_rest<false, SK, FEAT_ALL>;
-    return (feat & FEAT_BIGLEAF) ? k_path_rest<false, SK, FEAT_SPHERE | FEAT_BIGLEAF> : k_path_rest<false, SK, FEAT_SPHERE>;
-}
-static int split_sk(int sk) {
-    if ((sk & ~SK_BRDF) == 0) return SK_BRDF;
-    if ((sk & ~(SK_BRDF | SK_XLIGHT)) == 0) return SK_BRDF | SK_XLIGHT;
-    return SK_ALL;
-}
-static void split_kernels(PathKernels& K, int sk, int feat) {
-    switch (split_sk(sk)) {
-        case SK_BRDF:
-            K.hit = k_path_hit<false, SK_BRDF>;
-            K.rest = rest_kernel_sk<SK_BRDF>(feat);
-            K.unwind = k_path_unwind<false, SK_BRDF>;
-            break;
-        case SK_BRDF | SK_XLIGHT:
-            K.hit = k_path_hit<false, SK_BRDF | SK_XLIGHT>;
-            K.rest = rest_kernel_sk<SK_BRDF | SK_XLIGHT>(feat);
-            K.unwind = k_path_unwind<false, SK_BRDF | SK_XLIGHT>;
-            break;
-        default:
-            K.hit = k_path_hit<false, SK_ALL>;
-            K.rest = rest_kernel_sk<SK_ALL>(feat);
-            K.unwind = k_path_unwind<false, SK_ALL>;
-    }
-}
-
-// RTG_PATH_SPLIT=1: the step split by node kind (opt-in: bit-identical and at two waves per
-// SIMD, but slower -- pt_cornell 2 588 -> 1 441, pt_nee 3 588 -> 2 984, pt_rr 1 004 -> 1 002
-// Mrays/s, profiles/r04v_ptwave_split.txt: every unwinding level that needs shade_rest costs an
-// iteration of four launches where the single kernel unwinds in place)
-static bool path_split() {
-    const char* v = std::getenv("RTG_PATH_SPLIT");
-    return v && std::strcmp(v, "0") != 0;
-}
-
 hipError_t launch_path(PathState*& T, const DevScene& S, const DevCamera& C, const RenderParams& P, float* hdr,
                        unsigned char* l, float4* accum, DevCounters* cnt, bool stats, int feat, int sk,
                        hipStream_t st, hipEvent_t* ev) {
     if (!T) T = new PathState();
     PathKernels K{};
-    K.split = path_split();
     if (stats) {
         K.gen = k_path_gen<true>;
         K.trace = trace_kernel<true>(feat);
         K.step = k_path_step<true, SK_ALL, FEAT_ALL>;
-        K.hit = k_path_hit<true, SK_ALL>;
-        K.rest = k_path_rest<true, SK_ALL, FEAT_ALL>;
-        K.unwind = k_path_unwind<true, SK_ALL>;
     } else {
         K.gen = k_path_gen<false>;
         K.trace = trace_kernel<false>(feat);
-        if (K.split) split_kernels(K, sk, feat);
-        else K.step = step_kernel(sk, feat);
+        K.step = step_kernel(sk, feat);
     }
     return path_run(*T, K, stats, S, C, P, path_max_depth(S, C), hdr, l, accum, cnt, st, ev);
 }

@@ -39,13 +39,23 @@ enum : int { TK_FINAL = 0, TK_LEAF = 1, TK_ADDZERO = 2, TK_MIRROR = 3, TK_CONDUC
 enum : int { TK_LIT = 16 };
 enum : int { TM_ZERO = 0, TM_ENV = 1 };
 
-__global__ __launch_bounds__(256) void k_tree_gen(const DevCamera C, const RenderParams P, const int sample,
+// Level 0 of a pass of P.slabs samples: ray i is sample sample0 + i / npix of the part's pixel
+// tree_pixel(i mod npix) (npix = width * part_rows), so each slab is one sample's camera rays in
+// the 8x8-tile order.
+DEV int level0_pixel(const RenderParams& P, int width, int i, int& slab) {
+    const int npix = width * P.part_rows;
+    slab = i / npix;
+    return tree_pixel(P, width, i - slab * npix);
+}
+
+__global__ __launch_bounds__(256) void k_tree_gen(const DevCamera C, const RenderParams P, const int sample0,
                                                   const TreeLevel L0) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     if (i >= L0.n) return;
-    const int pixel = tree_pixel(P, C.width, i);
+    int slab;
+    const int pixel = level0_pixel(P, C.width, i, slab);
     const int px = pixel % C.width, py = pixel / C.width;
-    const uint64_t key = root_key(P.seed, pixel, sample);
+    const uint64_t key = root_key(P.seed, pixel, sample0 + slab);
     float mbTime;
     Ray r = camera_ray(C, px, py, key, mbTime);
     L0.o[i] = make_float4(r.o.x, r.o.y, r.o.z, 1.0f);
@@ -53,15 +63,13 @@ __global__ __launch_bounds__(256) void k_tree_gen(const DevCamera C, const Rende
     L0.key[i] = key;
 }
 
-// PK: the wave-packet form of the reference walk (k_primary's; coherent rays -- level 0, whose
-// rays are consecutive pixels of a row).  CL: the checked closest-hit walk of the any-hit tree
-// per lane (trace_closest_lane; plain meshes and spheres), the reference walk where it checks out
-#ifndef RTG_CL_WAVES
-#define RTG_CL_WAVES 4
-#endif
-template <bool STATS, int FEAT, bool PK = false, bool CL = false>
-__global__ __launch_bounds__(256, CL ? RTG_CL_WAVES : RTG_TRACE_WAVES(FEAT)) void k_tree_trace(const DevScene S, const TreeLevel L, const int level,
-                                                    DevCounters* counters) {
+// Closest hit of every ray of the level: the per-lane reference walk (the levels below the
+// camera's are incoherent -- round 5 measured packets on level 0 or on every level, the checked
+// closest-hit walk of the any-hit tree and a persistent refilling walk, all slower:
+// profiles/r05g_c5_tree_walks_ab.txt, r05y_c5_closest_ab.txt, r05z_c5_persistent_ab.txt)
+template <bool STATS, int FEAT>
+__global__ __launch_bounds__(256, RTG_TRACE_WAVES(FEAT)) void k_tree_trace(const DevScene S, const TreeLevel L,
+                                                                           const int level, DevCounters* counters) {
     const int i = blockIdx.x * 256 + threadIdx.x;
     Cnt<STATS> cn;
     if (i < level_n(L)) {
@@ -72,12 +80,7 @@ __global__ __launch_bounds__(256, CL ? RTG_CL_WAVES : RTG_TRACE_WAVES(FEAT)) voi
         if (level == 0) cn.cam();
         else cn.sec();
         Hit h;
-        bool done = false;
-        if constexpr (CL && (FEAT & ~FEAT_SPHERE) == 0) {
-            done = trace_closest_lane<STATS, FEAT>(S, r, h, cn);
-            if (!done) cn.efallback();
-        }
-        if (!done) trace<false, STATS, FEAT, PK && !(FEAT & FEAT_BIGLEAF)>(S, r, 0.f, INFINITY, INFINITY, h, cn);
+        trace<false, STATS, FEAT>(S, r, 0.f, INFINITY, INFINITY, h, cn);
         L.t[i] = h.t;
         L.obj[i] = h.obj;
         L.face[i] = h.face;
@@ -135,7 +138,8 @@ __global__ __launch_bounds__(256, SK == SK_ALL ? RTG_TREE_SHADE_WAVES : RTG_TREE
         if (obj < 0) {
             f3 v;
             if (level == 0) {
-                const int pixel = tree_pixel(P, C.width, i);
+                int slab;
+                const int pixel = level0_pixel(P, C.width, i, slab);
                 v = miss_color<SK>(S, C, pixel % C.width, pixel / C.width, r.d);
             } else {
                 const float4 m = L.miss[i];
@@ -357,17 +361,16 @@ __global__ __launch_bounds__(1024) void k_tree_scan(const int* __restrict__ cnt,
     }
 }
 
-// SORT (RTG_TREE_SORT, A/B): the block's children grouped by the octant of their direction
-// (stable: octant, then the order they were appended in), so that a wave of the next level holds
-// rays from one small image area going the same general way.  Positions within a level change
-// nothing but the walks' coherence: every ray's value depends only on its own record and key,
-// and the parents' links follow the rays.
-template <bool SORT>
+// Child rays into the next level's dense arrays in append order (round 5 measured grouping a
+// block's children by direction octant: no change, profiles/r05g_c5_tree_walks_ab.txt), and
+// the parents' child links.
 __global__ __launch_bounds__(256) void k_tree_compact(const TreeSegs G, const int* __restrict__ offs,
                                                       const TreeLevel cur, const TreeLevel nxt, const int cap) {
     const int b = blockIdx.x;
     const int n = G.c_count[b], base = offs[b];
-    auto move = [&](int k, int dst) {
+    for (int k = threadIdx.x; k < n; k += 256) {
+        const int dst = base + k;
+        if (dst >= cap) break;                       // over the planned capacity (k_tree_scan flagged it)
         const size_t q = (size_t)b * 512 + k;
         nxt.o[dst] = G.c_o[q];
         nxt.d[dst] = G.c_d[q];
@@ -377,58 +380,7 @@ __global__ __launch_bounds__(256) void k_tree_compact(const TreeSegs G, const in
         const int parent = p & 0x3FFFFFFF, slot = p >> 30;
         int* ext = reinterpret_cast<int*>(&cur.ext[parent]);
         ext[2 + slot] = dst;
-    };
-    if constexpr (SORT) {
-        __shared__ int wc[2][4][8];                  // per (round, wave, octant): count, then offset
-        const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-        int oc[2], rk[2];
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            const int k = r * 256 + (int)threadIdx.x;
-            int o = -1;
-            if (k < n) {
-                const float4 d = G.c_d[(size_t)b * 512 + k];
-                o = (d.x < 0.f ? 1 : 0) | (d.y < 0.f ? 2 : 0) | (d.z < 0.f ? 4 : 0);
-            }
-            oc[r] = o;
-            rk[r] = 0;
-            for (int c = 0; c < 8; ++c) {
-                const uint64_t m = __ballot(o == c);
-                if (o == c) rk[r] = __popcll(m & ((1ull << lane) - 1ull));
-                if (lane == 0) wc[r][w][c] = __popcll(m);
-            }
-        }
-        __syncthreads();
-        if (threadIdx.x == 0) {
-            int run = 0;
-            for (int c = 0; c < 8; ++c)
-                for (int r = 0; r < 2; ++r)
-                    for (int v = 0; v < 4; ++v) {
-                        const int t = wc[r][v][c];
-                        wc[r][v][c] = run;
-                        run += t;
-                    }
-        }
-        __syncthreads();
-#pragma unroll
-        for (int r = 0; r < 2; ++r) {
-            if (oc[r] < 0) continue;
-            const int dst = base + wc[r][w][oc[r]] + rk[r];
-            if (dst < cap) move(r * 256 + (int)threadIdx.x, dst);   // (over capacity: k_tree_scan flagged it)
-        }
-    } else {
-        for (int k = threadIdx.x; k < n; k += 256) {
-            const int dst = base + k;
-            if (dst >= cap) break;                   // over the planned capacity (k_tree_scan flagged it)
-            move(k, dst);
-        }
     }
-}
-
-// RTG_TREE_SORT=1 (A/B): k_tree_compact groups each block's children by direction octant
-static bool tree_sort() {
-    const char* v = std::getenv("RTG_TREE_SORT");
-    return v && std::strcmp(v, "0") != 0;
 }
 
 __global__ __launch_bounds__(256) void k_tree_resolve(const DevScene S, const DevCamera C, const RenderParams P,
@@ -507,7 +459,7 @@ __global__ __launch_bounds__(256) void k_tree_resolve(const DevScene S, const De
             value = add(color, term);
         }
     }
-    if (level > 0) {
+    if (level > 0 || P.slabs > 1) {     // (a multi-sample pass: k_tree_accum adds level 0's values)
         L.value[i] = make_float4(value.x, value.y, value.z, __int_as_float(L.obj[i] >= 0 ? 1 : 0));
         return;
     }
@@ -521,6 +473,7 @@ __global__ __launch_bounds__(256) void k_tree_resolve(const DevScene S, const De
     }
     const float gw = sample_weight(C.spp, sample, root_key(P.seed, pixel, sample));
     float4 a = first ? make_float4(0.f, 0.f, 0.f, 0.f) : accum[pixel];
+    // (accum_samples, rtg_common.hpp: the same operations over a multi-sample pass's slabs)
     a.x += value.x * gw;
     a.y += value.y * gw;
     a.z += value.z * gw;
@@ -532,6 +485,19 @@ __global__ __launch_bounds__(256) void k_tree_resolve(const DevScene S, const De
         if (hdr) { hdr[idx] = cc.x; hdr[idx + 1] = cc.y; hdr[idx + 2] = cc.z; }
         if (ldrOut) { ldrOut[idx] = ldr(cc.x); ldrOut[idx + 1] = ldr(cc.y); ldrOut[idx + 2] = ldr(cc.z); }
     }
+}
+
+// The end of a multi-sample pass: every pixel's level-0 values of the pass's slabs added to its
+// accumulation in sample order (accum_samples) -- the one-sample passes' operations bit for bit.
+__global__ __launch_bounds__(256) void k_tree_accum(const DevCamera C, const RenderParams P, const int sample0,
+                                                    const int first, const int last, const TreeLevel L0,
+                                                    float* __restrict__ hdr, unsigned char* __restrict__ ldrOut,
+                                                    float4* __restrict__ accum) {
+    const int npix = C.width * P.part_rows;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    if (i >= npix) return;
+    accum_samples(C, P, sample0, P.slabs, first != 0, last != 0, tree_pixel(P, C.width, i), L0.value + i,
+                  (size_t)npix, accum, hdr, ldrOut);
 }
 
 // ---------------------------------------------------------------------------
@@ -615,43 +581,15 @@ static hipError_t ensure_segs(TreeState& T, size_t blocks, int ns) {
 void tree_destroy(TreeState* t) { delete t; }
 
 // One level's trace / shade / shadow / scan launches (rays: L's count, on the host or device).
-// Levels whose closest hits take the packet walk (RTG_TREE_PK_LEVELS, A/B; default 0: every
-// level per lane)
-static int tree_packet_levels() {
-    const char* v = std::getenv("RTG_TREE_PK_LEVELS");
-    return v ? std::atoi(v) : 0;
-}
-
-// The levels' shadow rays (RTG_TREE_SHADOW_FAST, A/B): 1 the any-hit packet walk, 2 the any-hit
-// tree walked per lane (k_shadow_lane), both exact as in the wavefront pipeline; 0 the reference
-// walk per lane (round 3 measured the packet walk slower on the incoherent levels)
-static int tree_shadow_fast() {
-    const char* v = std::getenv("RTG_TREE_SHADOW_FAST");
-    return v ? std::atoi(v) : 0;
-}
-
-// (Round 5 measured an XCD-aware block order for the levels' trace / shade / shadow grids --
-// runs of 2^c consecutive blocks per XCD dealt round-robin, so a block's rays, hits and shadow
-// queue stay in one XCD's L2: C5 1 726 / 1 722 / 1 718 / 1 721 Mrays/s for block order and
-// c = 4 / 2 / 6; the levels' misses are not a matter of which XCD walks which rays --
-// profiles/r05s_tree_xcd_ab.txt.)
-// RTG_TREE_CLOSEST=1 (A/B): the levels not on the packet walk take the checked closest-hit walk
-// of the any-hit tree per lane
-static bool tree_closest() { return std::getenv("RTG_TREE_CLOSEST") != nullptr; }
-
+// (Round 5 measured an XCD-aware block order for the levels' grids -- no change,
+// profiles/r05s_tree_xcd_ab.txt -- and the levels' shadow rays on the any-hit tree as packets
+// or per lane -- slower, r05g_c5_tree_walks_ab.txt: they keep the per-lane reference walk.)
 template <bool STATS, int FEAT>
 static void level_launches(TreeState& T, const DevScene& S, const DevCamera& C, const RenderParams& P, int s,
                            int level, TreeLevel& L, int blocks, int ns, int* next_n, int cap_next, DevCounters* cnt,
                            hipStream_t st) {
     if (level == 0) hipLaunchKernelGGL(k_tree_gen, dim3(blocks), dim3(256), 0, st, C, P, s, L);
-    const int pkl = tree_packet_levels();
-    const bool cl = tree_closest() && (FEAT & ~FEAT_SPHERE) == 0 && S.anodes && !S.ahb_split;
-    if (level < pkl)
-        hipLaunchKernelGGL((k_tree_trace<STATS, FEAT, true>), dim3(blocks), dim3(256), 0, st, S, L, level, cnt);
-    else if (cl)
-        hipLaunchKernelGGL((k_tree_trace<STATS, FEAT, false, true>), dim3(blocks), dim3(256), 0, st, S, L, level, cnt);
-    else
-        hipLaunchKernelGGL((k_tree_trace<STATS, FEAT>), dim3(blocks), dim3(256), 0, st, S, L, level, cnt);
+    hipLaunchKernelGGL((k_tree_trace<STATS, FEAT>), dim3(blocks), dim3(256), 0, st, S, L, level, cnt);
     if ((T.sk & ~SK_TEX) == 0)
         hipLaunchKernelGGL((k_tree_shade<STATS, SK_TEX>), dim3(blocks), dim3(256), 0, st, S, C, L, level, P, T.G, cnt);
     else
@@ -663,14 +601,7 @@ static void level_launches(TreeState& T, const DevScene& S, const DevCamera& C, 
         W.num_slots = ns;
         W.hit_obj = L.obj;              // the hits the shadow rays leave (their origin leaf)
         W.hit_face = L.face;
-        const int sf = tree_shadow_fast();
-        if (sf && S.anodes && !S.exact_shadow && !(FEAT & FEAT_BIGLEAF) && !S.ahb_split) {
-            if (sf == 2)
-                hipLaunchKernelGGL((k_shadow_lane<STATS, FEAT>), dim3(blocks, ns), dim3(256), 0, st, S, W, cnt);
-            else
-                hipLaunchKernelGGL((k_shadow<STATS, FEAT, true>), dim3(blocks, ns), dim3(256), 0, st, S, W, cnt);
-        } else
-            hipLaunchKernelGGL((k_shadow<STATS, FEAT, false>), dim3(blocks, ns), dim3(256), 0, st, S, W, cnt);
+        hipLaunchKernelGGL((k_shadow<STATS, FEAT, false>), dim3(blocks, ns), dim3(256), 0, st, S, W, cnt);
     }
     hipLaunchKernelGGL(k_tree_scan, dim3(1), dim3(1024), 0, st, T.G.c_count, blocks, T.offs, next_n, cap_next,
                        T.d_counts ? T.d_counts + kMaxLevels : nullptr);
@@ -686,7 +617,7 @@ static hipError_t tree_pass_sync(TreeState& T, const DevScene& S, const DevCamer
     const int ns = S.num_point + S.num_area + S.num_env + S.num_dir + S.num_spot + S.num_mesh;
     const int npix = P.part_rows * C.width;
     hipError_t e;
-    size_t n = (size_t)npix;
+    size_t n = (size_t)npix * P.slabs;
     int level = 0;
     sizes.assign(1, n);
     if (ev) (void)hipEventRecord(ev[0], st);
@@ -706,12 +637,8 @@ static hipError_t tree_pass_sync(TreeState& T, const DevScene& S, const DevCamer
         sizes.push_back(nn);
         if ((int)T.levels.size() <= level + 1) T.levels.emplace_back();
         if ((e = ensure_level(T.levels[level + 1], nn, ns)) != hipSuccess) return e;
-        if (tree_sort())
-            hipLaunchKernelGGL(k_tree_compact<true>, dim3(blocks), dim3(256), 0, st, T.G, T.offs, T.levels[level].L,
-                               T.levels[level + 1].L, (int)nn);
-        else
-            hipLaunchKernelGGL(k_tree_compact<false>, dim3(blocks), dim3(256), 0, st, T.G, T.offs, T.levels[level].L,
-                               T.levels[level + 1].L, (int)nn);
+        hipLaunchKernelGGL(k_tree_compact, dim3(blocks), dim3(256), 0, st, T.G, T.offs, T.levels[level].L,
+                           T.levels[level + 1].L, (int)nn);
         n = nn;
     }
     if (ev) (void)hipEventRecord(ev[1], st);
@@ -722,6 +649,9 @@ static hipError_t tree_pass_sync(TreeState& T, const DevScene& S, const DevCamer
         hipLaunchKernelGGL(k_tree_resolve, dim3(blocks), dim3(256), 0, st, S, C, P, s, (int)first, (int)last, L,
                            Lc, lv, ns, hdr, l, accum);
     }
+    if (P.slabs > 1)
+        hipLaunchKernelGGL(k_tree_accum, dim3((npix + 255) / 256), dim3(256), 0, st, C, P, s, (int)first, (int)last,
+                           T.levels[0].L, hdr, l, accum);
     if (ev) (void)hipEventRecord(ev[2], st);
     return hipGetLastError();
 }
@@ -750,11 +680,7 @@ static hipError_t tree_pass_async(TreeState& T, const DevScene& S, const DevCame
             TreeLevel& Ln = T.levels[level + 1].L;
             Ln.n = (int)T.plan[level + 1];
             Ln.nd = T.d_counts + level + 1;
-            if (tree_sort())
-                hipLaunchKernelGGL(k_tree_compact<true>, dim3(blocks), dim3(256), 0, st, T.G, T.offs, L, Ln,
-                               (int)T.plan[level + 1]);
-            else
-                hipLaunchKernelGGL(k_tree_compact<false>, dim3(blocks), dim3(256), 0, st, T.G, T.offs, L, Ln,
+            hipLaunchKernelGGL(k_tree_compact, dim3(blocks), dim3(256), 0, st, T.G, T.offs, L, Ln,
                                (int)T.plan[level + 1]);
         }
     }
@@ -765,6 +691,11 @@ static hipError_t tree_pass_async(TreeState& T, const DevScene& S, const DevCame
         const int blocks = (int)((T.plan[lv] + 255) / 256);
         hipLaunchKernelGGL(k_tree_resolve, dim3(blocks), dim3(256), 0, st, S, C, P, s, (int)first, (int)last, L,
                            Lc, lv, ns, hdr, l, accum);
+    }
+    if (P.slabs > 1) {
+        const int npix = P.part_rows * C.width;
+        hipLaunchKernelGGL(k_tree_accum, dim3((npix + 255) / 256), dim3(256), 0, st, C, P, s, (int)first, (int)last,
+                           T.levels[0].L, hdr, l, accum);
     }
     if (ev) (void)hipEventRecord(ev[2], st);
     return hipGetLastError();
@@ -785,7 +716,7 @@ static hipError_t tree_run(TreeState& T, const DevScene& S, const DevCamera& C, 
     // the plan belongs to one frame part of one camera (its view and samples decide the level
     // sizes): two cameras of a scene at the same size keep apart
     const std::vector<long long> key = {P.row_begin, P.row_end, P.part_index, P.part_count, C.width, C.height,
-                                        (long long)(size_t)S.objects, S.max_depth, (long long)camera_hash(C)};
+                                        (long long)(size_t)S.objects, S.max_depth, (long long)camera_hash(C), P.slabs};
     auto prepare = [&]() -> hipError_t {
         // capacities and block segments of the plan; the overflow flag cleared
         hipError_t r;
@@ -818,15 +749,25 @@ static hipError_t tree_run(TreeState& T, const DevScene& S, const DevCamera& C, 
         bool any_async = false;
         if (planned && (e = prepare()) != hipSuccess) return e;
         std::vector<size_t> seen;
-        for (int s = P.sample_begin; s < P.sample_begin + P.sample_count; ++s) {
-            const bool first = s == P.sample_begin, last = s == P.sample_begin + P.sample_count - 1;
+        // passes of P.slabs consecutive samples; a shorter last pass (what is left) runs
+        // host-driven: its level sizes are not the plan's
+        const int s_end = P.sample_begin + P.sample_count;
+        for (int s = P.sample_begin; s < s_end; s += P.slabs) {
+            RenderParams Pp = P;
+            Pp.slabs = s_end - s < P.slabs ? s_end - s : P.slabs;
+            const bool first = s == P.sample_begin, last = s + Pp.slabs == s_end;
             hipEvent_t* pev = last ? ev : nullptr;
-            if (planned) {
-                e = tree_pass_async<STATS, FEAT>(T, S, C, P, s, first, last, hdr, l, accum, cnt, st, pev);
+            if (planned && Pp.slabs == P.slabs) {
+                e = tree_pass_async<STATS, FEAT>(T, S, C, Pp, s, first, last, hdr, l, accum, cnt, st, pev);
                 any_async = true;
+            } else if (planned) {
+                // (the render's last pass: the planned passes before it are untouched -- buffers
+                // only grow -- and the next render re-prepares the plan)
+                std::vector<size_t> sizes;
+                e = tree_pass_sync<STATS, FEAT>(T, S, C, Pp, s, first, last, hdr, l, accum, cnt, st, pev, sizes);
             } else {
                 std::vector<size_t> sizes;
-                e = tree_pass_sync<STATS, FEAT>(T, S, C, P, s, first, last, hdr, l, accum, cnt, st, pev, sizes);
+                e = tree_pass_sync<STATS, FEAT>(T, S, C, Pp, s, first, last, hdr, l, accum, cnt, st, pev, sizes);
                 if (sizes.size() > seen.size()) seen.resize(sizes.size(), 0);
                 for (size_t k = 0; k < sizes.size(); ++k) seen[k] = std::max(seen[k], sizes[k]);
                 if (e == hipSuccess && adapt) {

@@ -23,59 +23,39 @@
 
 namespace rtg {
 
-// k_shade register-pressure variants (A/B): RTG_SHADE_REFS the hit point / normal by reference
-// and the RNG key recomputed where used (no scratch in the headline's fused kernel),
-// RTG_FUSED_SWITCH one light by branch instead of the light loops (no VGPR spills either, but
-// SGPR spills into the shadow walk: measured slower), RTG_FUSED_STASH the pixel's colour terms
-// in LDS across the shadow walk
-#ifndef RTG_FUSED_STASH
-#define RTG_FUSED_STASH 0
-#endif
-#ifndef RTG_FUSED_SWITCH
-#define RTG_FUSED_SWITCH 0
-#endif
-#ifndef RTG_SHADE_REFS
-#define RTG_SHADE_REFS 1
-#endif
-
 enum { BASE_FINAL = 1, BASE_ADD_ZERO = 2 };
 
-// ORD: RTG_RENDER_ORDERED (plain mesh scenes): the checked closest-hit walk -- on the any-hit
-// tree as wave packets (trace_closest_pk, ordered mode 2) or nearest-first per lane on the
-// collapsed reference tree (trace_ordered, mode 1) -- the reference walk where its check fails
+// ORD: RTG_RENDER_ORDERED (plain mesh scenes): the checked closest-hit walk on the any-hit tree
+// as wave packets (trace_closest_pk), the reference walk where its check fails
 #ifndef RTG_ORD_WAVES
 #define RTG_ORD_WAVES RTG_WIDE_WAVES_PLAIN
 #endif
-template <bool STATS, int FEAT, int ORD = 0, bool DEFER = false>
+template <bool STATS, int FEAT, bool ORD = false, bool DEFER = false>
 __global__ __launch_bounds__(256, ORD ? RTG_ORD_WAVES : RTG_TRACE_WAVES(FEAT)) void k_primary(
-    const DevScene S, const DevCamera C, const RenderParams P, const int sample, const WaveBufs W,
+    const DevScene S, const DevCamera C, const RenderParams P, const int sample0, const WaveBufs W,
     DevCounters* counters) {
-    int px, py, crow;
-    tile_pixel(P, px, py, crow);
+    int px, py, crow, slab;
+    tile_pixel(P, px, py, crow, slab);
+    const int sample = sample0 + slab;
     Cnt<STATS> cn;
     if (px < C.width && py < P.row_end) {
         const int pixel = px + py * C.width;
+        const int i = work_index(P, C.width, slab, crow, px);
         const uint64_t key = root_key(P.seed, pixel, sample);
         float mbTime;
         Ray ray = camera_ray(C, px, py, key, mbTime);
         cn.cam();
         Hit h;
         if constexpr (ORD) {
-            bool sure;
-            if constexpr (ORD == 2) sure = trace_closest_pk<STATS, FEAT>(S, ray, h, cn);
-            else sure = trace_ordered<STATS>(S, ray, h, cn);
-            if (!sure) {
+            if (!trace_closest_pk<STATS, FEAT>(S, ray, h, cn)) {
                 cn.efallback();
                 trace<false, STATS, FEAT>(S, ray, mbTime, INFINITY, INFINITY, h, cn);
             }
         } else if constexpr (DEFER) {
             // large leaves deferred to k_bigleaf; k_hitfix settles the pixel (rtg_common.hpp DeferCtx)
-            DeferCtx dc{W.dq_e, W.dq_count, W.dq_cap, crow * C.width + px, false, 0};
+            DeferCtx dc{W.dq_e, W.dq_count, W.dq_cap, i, false};
             trace<false, STATS, FEAT, true, true>(S, ray, mbTime, INFINITY, INFINITY, h, cn, &dc);
-            const int big = __builtin_amdgcn_readfirstlane(dc.big);
-            if (big && (int)(threadIdx.x & 63) == __ffsll((long long)__ballot(1)) - 1) atomicAdd(W.dq_count + 3, big);
             if (dc.deferred) {
-                const int i = crow * C.width + px;
                 W.hit_key[i] = h.obj >= 0 ? obj_key(h.t, h.obj, h.face) : ~0ull;
                 W.hit_obj[i] = -2;                         // pending
                 flush_counters<STATS>(cn, counters);
@@ -85,7 +65,6 @@ __global__ __launch_bounds__(256, ORD ? RTG_ORD_WAVES : RTG_TRACE_WAVES(FEAT)) v
             trace<false, STATS, FEAT, RTG_PRIMARY_PACKET != 0 && !(FEAT & FEAT_BIGLEAF)>(S, ray, mbTime, INFINITY,
                                                                                        INFINITY, h, cn);
         }
-        const int i = crow * C.width + px;
         W.hit_t[i] = h.t;
         W.hit_obj[i] = h.obj;
         W.hit_face[i] = h.face;
@@ -129,10 +108,11 @@ __global__ __launch_bounds__(256) void k_bigleaf(const DevScene S, const WaveBuf
 // the pending pixels and extend_fallbacks those the check sent to the reference walk)
 template <int FEAT>
 __global__ __launch_bounds__(256) void k_hitfix(const DevScene S, const DevCamera C, const RenderParams P,
-                                                const int sample, const WaveBufs W, DevCounters* counters) {
-    int px, py, crow;
-    tile_pixel(P, px, py, crow);
-    const int i = crow * C.width + px;
+                                                const int sample0, const WaveBufs W, DevCounters* counters) {
+    int px, py, crow, slab;
+    tile_pixel(P, px, py, crow, slab);
+    const int sample = sample0 + slab;
+    const int i = work_index(P, C.width, slab, crow, px);
     const bool pending = px < C.width && py < P.row_end && W.hit_obj[i] == -2;
     const uint64_t pm = __ballot(pending);
     if (counters && pm && (threadIdx.x & 63) == __ffsll((long long)pm) - 1)
@@ -261,13 +241,15 @@ DEV bool trace_wave(const DevScene& S, Ray& r, float mbTime, Hit& h) {
 
 template <int FEAT>
 __global__ __launch_bounds__(256) void k_refwalk(const DevScene S, const DevCamera C, const RenderParams P,
-                                                 const int sample, const WaveBufs W) {
+                                                 const int sample0, const WaveBufs W) {
     const int n = W.dq_count[1];
     for (int e = (int)((blockIdx.x * 256u + threadIdx.x) >> 6); e < n; e += gridDim.x * 4) {
         const int i = reinterpret_cast<const int*>(W.dq_e)[e];
-        const int crow = i / C.width, px = i - crow * C.width, py = part_row(P, crow);
+        const int slab = i / P.slab_px;
+        const int pixel = work_pixel(P, C.width, slab, i);
+        const int py = pixel / C.width, px = pixel - py * C.width;
         float mbTime;
-        Ray ray = camera_ray(C, px, py, root_key(P.seed, px + py * C.width, sample), mbTime);
+        Ray ray = camera_ray(C, px, py, root_key(P.seed, pixel, sample0 + slab), mbTime);
         Hit h;
         trace_wave<FEAT>(S, ray, mbTime, h);
         if ((threadIdx.x & 63) == 0) {
@@ -292,30 +274,39 @@ DEV int queue_append(bool want, int* lds_count) {
     return want ? base + rank : -1;
 }
 
-// Output of a sample pass: final image (spp 1) or the multi-sample accumulator.
+// Output of a sample pass: final image (spp 1) or the multi-sample accumulator; a pass of
+// several sample slabs (RenderParams::slabs > 1) writes each colour to `col` (work-buffer
+// index) and k_accum adds them to the accumulator in sample order.
 struct PassOut {
     float* hdr;
     unsigned char* ldr;
     float4* accum;
     int first, last;
+    float4* col;
 };
 
 // renderThreadMain's per-pixel end of a sample pass (main.cpp:80-121): the colour itself at
-// 1 spp, else the Gaussian-weighted accumulation, divided out after the last sample.
-DEV void finish_pixel(const DevCamera& C, const RenderParams& P, int sample, const PassOut& O, int pixel, f3 color) {
+// 1 spp, else the Gaussian-weighted accumulation, divided out after the last sample.  A
+// multi-sample pass stores the colour in the pixel's entry of its sample slab (work_index,
+// derived from the pixel here: the callers keep only the pixel live across their walks).
+DEV void finish_pixel(const DevCamera& C, const RenderParams& P, int sample, const PassOut& O, int pixel, int slab,
+                      f3 color) {
+    if (O.col) {
+        const int py = pixel / C.width, px = pixel - py * C.width;
+        const int r = py - P.row_begin;
+        const int crow = ((r >> 3) / P.part_count) * 8 + (r & 7);   // part_row's inverse
+        O.col[work_index(P, C.width, slab, crow, px)] = make_float4(color.x, color.y, color.z, 0.f);
+        return;
+    }
     if (C.spp <= 1 && !P.accum_only) {
         const size_t idx = 3 * (size_t)pixel;
         if (O.hdr) { O.hdr[idx] = color.x; O.hdr[idx + 1] = color.y; O.hdr[idx + 2] = color.z; }
         if (O.ldr) { O.ldr[idx] = ldr(color.x); O.ldr[idx + 1] = ldr(color.y); O.ldr[idx + 2] = ldr(color.z); }
         return;
     }
-#if RTG_SHADE_REFS
     int pk = pixel;                  // (recomputed, not merged with the caller's key: see area_light)
     asm volatile("" : "+v"(pk));
     const float gw = sample_weight(C.spp, sample, root_key(P.seed, pk, sample));
-#else
-    const float gw = sample_weight(C.spp, sample, root_key(P.seed, pixel, sample));
-#endif
     float4 a = O.first ? make_float4(0.f, 0.f, 0.f, 0.f) : O.accum[pixel];
     a.x += color.x * gw;
     a.y += color.y * gw;
@@ -370,20 +361,21 @@ template <bool STATS, int SK, int MODE, int FEAT = 0, bool FAST = false, bool FR
 __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(FEAT))
                                                    : RTG_SHADE_WAVES) void k_shade(const DevScene S, const DevCamera C,
                                                                                    const RenderParams P,
-                                                                                   const int sample, const WaveBufs W,
+                                                                                   const int sample0, const WaveBufs W,
                                                                                    const PassOut O,
                                                                                    DevCounters* counters) {
     constexpr bool ONE = MODE != SH_GENERAL;
     __shared__ int seg_count;
     if (threadIdx.x == 0) seg_count = 0;
     __syncthreads();
-    int px, py, crow;
-    tile_pixel(P, px, py, crow);
+    int px, py, crow, slab;
+    tile_pixel(P, px, py, crow, slab);
+    const int sample = sample0 + slab;
     const size_t seg = (size_t)blockIdx.x * 256 * W.num_slots;
     Cnt<STATS> cn;
     const bool valid = px < C.width && py < P.row_end;
     const int pixel = valid ? px + py * C.width : 0;
-    const int i = valid ? crow * C.width + px : 0;
+    const int i = valid ? work_index(P, C.width, slab, crow, px) : 0;
     const uint64_t key = root_key(P.seed, pixel, sample);
     static_assert(!FRAME || MODE >= SH_FUSED, "the frame kernel is the fused layout's");
     Hit fh;                          // FRAME: the camera ray's hit
@@ -443,14 +435,10 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
     }
     // ---- lights, in SampleDirectLighting's order (raytracer.cpp:706-803)
     int slot = i * W.num_slots;
-#if RTG_SHADE_REFS
     // the hit point and normal by reference: a lane that is not lit never reads them (every use
     // is behind `lit` / push's `want`), and selected copies kept a second set of six VGPRs live
-    // next to the surface record through the light loops
+    // next to the surface record through the light loops (36 B of scratch per lane at seven waves)
     const f3 &p = c.s.p, &n = c.s.n;
-#else
-    const f3 p = lit ? c.s.p : mk(0, 0, 0), n = lit ? c.s.n : mk(0, 0, 1);
-#endif
     if constexpr (MODE == SH_FUSED_N) {
         // SK 0: point, area and directional lights only, in that order; one shadow-walk call site
         f3 sum = mk(0, 0, 0);
@@ -501,7 +489,7 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
             }
             if (!shadow_occluded<STATS, FEAT, FAST>(S, W, 0, qo, qd, cn)) sum = add(sum, term);
         }
-        if (valid) finish_pixel(C, P, sample, O, pixel, resolve_sum(base, bflags, sum));
+        if (valid) finish_pixel(C, P, sample, O, pixel, slab, resolve_sum(base, bflags, sum));
     } else {
     auto push = [&](bool want, f3 target_dir_or_pos, bool directional) {
         // IsInShadow / IsInShadowDirectional shadow-ray set-up (raytracer.cpp:555-584)
@@ -557,16 +545,12 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
         f3 sp = mk(0, 0, 0);
         if (lit) {
             const DevAreaLight& L = S.area_lights[l];
-#if RTG_SHADE_REFS
             // the pixel's RNG key again (a few integer ops) rather than two VGPRs kept through the
             // point lights' shading; the laundered pixel index stops the compiler from merging it
             // with the first computation
             int pk = pixel;
             asm volatile("" : "+v"(pk));
             const uint64_t akey = root_key(P.seed, pk, sample);
-#else
-            const uint64_t akey = key;
-#endif
             float offU = rnd(akey, RP_AREA, 2 * l) - 0.5f;
             float offV = rnd(akey, RP_AREA, 2 * l + 1) - 0.5f;
             sp = add(add(ld3(L.pos), muls(ld3(L.u), L.extent * offU)), muls(ld3(L.v), L.extent * offV));
@@ -585,15 +569,6 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
         if (lit) put(shade<false, SK>(S, c, neg(ldir), w_o, ld3(S.dir_lights[l].radiance)));
         push(lit, ldir, true);
     };
-    if constexpr (MODE == SH_FUSED && RTG_FUSED_SWITCH) {
-        // the fused layout's scenes have exactly one light, a point, area or directional one:
-        // one branch instead of three loops, so nothing of one light kind stays live across
-        // another's code (the loops kept the RNG key and the hit point live through the point
-        // light's shading and spilled them to scratch at seven waves per SIMD)
-        if (S.num_point) point_light(0);
-        else if (S.num_area) area_light(0);
-        else dir_light(0);
-    } else {
     for (int l = 0; l < S.num_point; ++l, ++slot) point_light(l);
     for (int l = 0; l < S.num_area; ++l, ++slot) area_light(l);
     if constexpr ((SK & SK_XLIGHT) != 0) {
@@ -645,31 +620,15 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
             push(lit, sp, false);
         }
     }
-    }
     if constexpr (MODE == SH_FUSED) {
         if (pushed) {
-#if RTG_FUSED_STASH
-            // the pixel's base colour, flags, light term and index wait in LDS while the shadow
-            // walk runs: eight VGPRs fewer across the walk, which at seven waves per SIMD (72
-            // VGPRs) had spilled to scratch
-            __shared__ float4 stash[2][256];
-            stash[0][threadIdx.x] = make_float4(base.x, base.y, base.z, __int_as_float(bflags));
-            stash[1][threadIdx.x] = make_float4(term1.x, term1.y, term1.z, __int_as_float(pixel));
-            asm volatile("" ::: "memory");
             const bool occluded = shadow_occluded<STATS, FEAT, FAST>(S, W, 0, ro, rd, cn);
-            asm volatile("" ::: "memory");
-            const float4 sb = stash[0][threadIdx.x], st = stash[1][threadIdx.x];
-            finish_pixel(C, P, sample, O, __float_as_int(st.w),
-                         resolve_one(mk(sb.x, sb.y, sb.z), __float_as_int(sb.w), true, mk(st.x, st.y, st.z), occluded));
-#else
-            const bool occluded = shadow_occluded<STATS, FEAT, FAST>(S, W, 0, ro, rd, cn);
-            finish_pixel(C, P, sample, O, pixel, resolve_one(base, bflags, true, term1, occluded));
-#endif
+            finish_pixel(C, P, sample, O, pixel, slab, resolve_one(base, bflags, true, term1, occluded));
         } else if (valid) {
-            finish_pixel(C, P, sample, O, pixel, resolve_one(base, bflags, has_term, term1, false));
+            finish_pixel(C, P, sample, O, pixel, slab, resolve_one(base, bflags, has_term, term1, false));
         }
     }
-    if (MODE == SH_ONE && valid && !pushed) finish_pixel(C, P, sample, O, pixel, resolve_one(base, bflags, has_term, term1, false));
+    if (MODE == SH_ONE && valid && !pushed) finish_pixel(C, P, sample, O, pixel, slab, resolve_one(base, bflags, has_term, term1, false));
     }
     __syncthreads();
     if (threadIdx.x == 0) W.q_count[blockIdx.x] = seg_count;
@@ -678,11 +637,11 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
 
 // One-light scenes: CastShadowRay for a queued pixel, then its PerformShading sum and the end
 // of the sample pass (what k_resolve does for the general case).
-template <bool STATS, int FEAT, bool FAST, bool DEFER = false, int GATE = 0>
+template <bool STATS, int FEAT, bool FAST, bool DEFER = false>
 __global__ __launch_bounds__(256, FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(FEAT)) void k_shadow_one(
-    const DevScene S, const DevCamera C, const RenderParams P, const int sample, const WaveBufs W, const PassOut O,
+    const DevScene S, const DevCamera C, const RenderParams P, const int sample0, const WaveBufs W, const PassOut O,
     DevCounters* counters) {
-    if (gate_skip<GATE>(W)) return;
+    const int slab = (int)(blockIdx.x / (unsigned)P.slab_tiles);    // the k_shade block's sample slab
     const int k = threadIdx.x;
     const size_t q = (size_t)blockIdx.x * 256 + k;
     Cnt<STATS> cn;
@@ -702,17 +661,17 @@ __global__ __launch_bounds__(256, FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(
         }
         const float4 b = W.q_pay[2 * q], t = W.q_pay[2 * q + 1];
         const f3 color = resolve_one(mk(b.x, b.y, b.z), __float_as_int(b.w), true, mk(t.x, t.y, t.z), occluded);
-        finish_pixel(C, P, sample, O, __float_as_int(t.w), color);
+        finish_pixel(C, P, sample0 + slab, O, __float_as_int(t.w), slab, color);
     }
     flush_counters<STATS>(cn, counters);
 }
 
 // Pending shadow rays after k_bigleaf_any: occluded by a queued leaf, undecided (the reference
 // walk decides), else unoccluded -- then the pixel is finished as k_shadow_one would have.
-template <int FEAT, int GATE>
+template <int FEAT>
 __global__ __launch_bounds__(256) void k_shadow_fin_one(const DevScene S, const DevCamera C, const RenderParams P,
-                                                        const int sample, const WaveBufs W, const PassOut O) {
-    if (gate_skip<GATE>(W)) return;              // (shadow_state holds an older pass's states)
+                                                        const int sample0, const WaveBufs W, const PassOut O) {
+    const int slab = (int)(blockIdx.x / (unsigned)P.slab_tiles);
     const int k = threadIdx.x;
     const size_t q = (size_t)blockIdx.x * 256 + k;
     if (k >= W.q_count[blockIdx.x]) return;
@@ -730,13 +689,12 @@ __global__ __launch_bounds__(256) void k_shadow_fin_one(const DevScene S, const 
     }
     const float4 b = W.q_pay[2 * q], t = W.q_pay[2 * q + 1];
     const f3 color = resolve_one(mk(b.x, b.y, b.z), __float_as_int(b.w), true, mk(t.x, t.y, t.z), occluded);
-    finish_pixel(C, P, sample, O, __float_as_int(t.w), color);
+    finish_pixel(C, P, sample0 + slab, O, __float_as_int(t.w), slab, color);
 }
 
 // The same for the general layout: the answer goes to the light slot's occlusion byte.
-template <int FEAT, int GATE>
+template <int FEAT>
 __global__ __launch_bounds__(256) void k_shadow_fin(const DevScene S, const WaveBufs W) {
-    if (gate_skip<GATE>(W)) return;
     const int k = blockIdx.y * 256 + threadIdx.x;
     const size_t q = ((size_t)blockIdx.x * W.num_slots) * 256 + k;
     if (k >= W.q_count[blockIdx.x]) return;
@@ -763,10 +721,13 @@ hipError_t wave_shade(bool stats, int sk, bool one, const DevScene& S, const Dev
                       int sample, const WaveBufs& W, const PassOut& O, DevCounters* cnt, hipStream_t st);
 void wave_resolve(const DevCamera& C, const RenderParams& P, int sample, const WaveBufs& W, const PassOut& O,
                   hipStream_t st);
+// the end of a multi-sample pass: every pixel's slab colours into its accumulation (k_accum)
+void wave_accum(const DevCamera& C, const RenderParams& P, int sample, const WaveBufs& W, const PassOut& O,
+                hipStream_t st);
 bool no_fused_shade();
 bool frame_kernel();
 bool defer_leaves();
-int defer_any_leaves();
+bool defer_any_leaves();
 bool wide_bigleaf();
 bool defer_diag();
 int refwalk_blocks();
@@ -781,38 +742,35 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
     const bool one = W.num_slots <= 1 && W.q_pay != nullptr;
     const int scene_sk = sk;
     if (!one) sk = SK_ALL;
-    // fast any-hit walk (RTG_SHADOW_MODE) unless RTG_RENDER_EXACT_SHADOW asks for the
-    // reference walk
+    // the any-hit packet walk unless RTG_RENDER_EXACT_SHADOW asks for the reference walk
     // (large-leaf scenes: the split any-hit tree cuts their pole fans into small leaves; with
     // RTG_AHB=ref / exact they keep the cooperative reference walk unless RTG_WIDE_BIGLEAF)
     // large-leaf scenes (production renders): the any-hit walk with their large leaves queued
-    // (k_bigleaf_any; RTG_DEFER=0: the cooperative reference walk)
-    // (0 off; 1 always; 2 chosen per pass on the device -- GATE, rtg_common.hpp)
-    const int defer_any = !STATS && (FEAT & FEAT_BIGLEAF) && RTG_SHADOW_MODE == 3 && W.dq_e && W.shadow_state &&
-                                  S.anodes && !S.ahb_split && !S.exact_shadow
-                              ? defer_any_leaves()
-                              : 0;
-    const bool fast = (RTG_SHADOW_MODE == 3 ? S.anodes != nullptr
-                                            : RTG_SHADOW_MODE == 2 ? S.node_up != nullptr : S.nodes != nullptr) &&
-                      (!(FEAT & FEAT_BIGLEAF) || S.ahb_split || wide_bigleaf() || defer_any == 1) && !S.exact_shadow;
+    // (k_bigleaf_any; RTG_DEFER_ANY=0: the cooperative reference walk)
+    const bool defer_any = !STATS && (FEAT & FEAT_BIGLEAF) && W.dq_e && W.shadow_state &&
+                           S.anodes && !S.ahb_split && !S.exact_shadow && defer_any_leaves();
+    const bool fast = S.anodes != nullptr && (!(FEAT & FEAT_BIGLEAF) || S.ahb_split || wide_bigleaf() || defer_any) && !S.exact_shadow;
     // shading fused with the shadow ray: plain shading, the fast any-hit walk (RTG_NO_FUSED_SHADE=1
     // keeps the queue: experiments)
     const bool fused = scene_sk == 0 && fast && !(FEAT & FEAT_BIGLEAF) && nshadow > 0 && !no_fused_shade();
     *layout = fused ? (frame_kernel() && !(FEAT == 0 && S.ordered) ? LAYOUT_WAVE_FRAME : LAYOUT_WAVE_FUSED)
                     : (one ? LAYOUT_WAVE_ONE : LAYOUT_WAVE);
-    for (int s = P.sample_begin; s < P.sample_begin + P.sample_count; ++s) {
-        const int first = s == P.sample_begin, last = s == P.sample_begin + P.sample_count - 1;
-        const PassOut O{hdr, l, W.accum, first, last};
+    const int s_end = P.sample_begin + P.sample_count;
+    // passes of P.slabs consecutive samples (the last one what is left)
+    for (int s = P.sample_begin; s < s_end; s += P.slabs) {
+        RenderParams Pp = P;
+        Pp.slabs = s_end - s < P.slabs ? s_end - s : P.slabs;
+        const int nb = Pp.slab_tiles * Pp.slabs;       // blocks of the tile grids
+        const int first = s == P.sample_begin, last = s + Pp.slabs == s_end;
+        // several slabs: colours per (slab, pixel), k_accum adds them in sample order
+        const PassOut O{hdr, l, W.accum, first, last, Pp.slabs > 1 ? W.col : nullptr};
         hipEvent_t* e5 = last ? ev : nullptr;
         hipError_t e;
         if (e5) (void)hipEventRecord(e5[0], st);
         bool ordered = false;
         if constexpr (FEAT == 0) {
-            if (S.ordered == 2) {
-                hipLaunchKernelGGL((k_primary<STATS, 0, 2>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
-                ordered = true;
-            } else if (S.ordered) {
-                hipLaunchKernelGGL((k_primary<STATS, 0, 1>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
+            if (S.ordered) {
+                hipLaunchKernelGGL((k_primary<STATS, 0, true>), dim3(nb), dim3(256), 0, st, S, C, Pp, s, W, cnt);
                 ordered = true;
             }
         }
@@ -826,100 +784,80 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
         if (W.dq_e) (void)hipMemsetAsync(W.dq_count, 0, 4 * sizeof(int), st);
         if constexpr (!STATS && (FEAT & FEAT_BIGLEAF) != 0) {
             if (!ordered && !frame && W.dq_e && S.face_leaf && S.num_objects < 4096 && S.num_faces < (1 << 20)) {
-                hipLaunchKernelGGL((k_primary<STATS, FEAT, 0, true>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s,
-                                   W, cnt);
+                hipLaunchKernelGGL((k_primary<STATS, FEAT, false, true>), dim3(nb), dim3(256), 0, st, S, C, Pp, s, W, cnt);
                 hipLaunchKernelGGL((k_bigleaf<FEAT>), dim3(2048), dim3(256), 0, st, S, W);
-                hipLaunchKernelGGL((k_hitfix<FEAT>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W,
+                hipLaunchKernelGGL((k_hitfix<FEAT>), dim3(nb), dim3(256), 0, st, S, C, Pp, s, W,
                                    defer_diag() ? cnt : nullptr);
-                hipLaunchKernelGGL((k_refwalk<FEAT>), dim3(refwalk_blocks()), dim3(256), 0, st, S, C, P, s, W);
+                hipLaunchKernelGGL((k_refwalk<FEAT>), dim3(refwalk_blocks()), dim3(256), 0, st, S, C, Pp, s, W);
                 deferred = true;
             }
         }
         if (!ordered && !frame && !deferred)
-            hipLaunchKernelGGL((k_primary<STATS, FEAT>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, cnt);
+            hipLaunchKernelGGL((k_primary<STATS, FEAT>), dim3(nb), dim3(256), 0, st, S, C, Pp, s, W, cnt);
         if (e5 && !frame) (void)hipEventRecord(e5[1], st);
         if (frame) {
             if constexpr (!(FEAT & FEAT_BIGLEAF)) {
                 if (one)
-                    hipLaunchKernelGGL((k_shade<STATS, 0, SH_FUSED, FEAT, true, true>), dim3(P.num_tiles), dim3(256), 0,
-                                       st, S, C, P, s, W, O, cnt);
+                    hipLaunchKernelGGL((k_shade<STATS, 0, SH_FUSED, FEAT, true, true>), dim3(nb), dim3(256), 0, st, S, C,
+                                       Pp, s, W, O, cnt);
                 else
-                    hipLaunchKernelGGL((k_shade<STATS, 0, SH_FUSED_N, FEAT, true, true>), dim3(P.num_tiles), dim3(256),
-                                       0, st, S, C, P, s, W, O, cnt);
+                    hipLaunchKernelGGL((k_shade<STATS, 0, SH_FUSED_N, FEAT, true, true>), dim3(nb), dim3(256), 0, st, S,
+                                       C, Pp, s, W, O, cnt);
             }
             if (e5) (void)hipEventRecord(e5[1], st);             // LAYOUT_WAVE_FRAME: one stage
         } else if (fused) {
             if constexpr (!(FEAT & FEAT_BIGLEAF)) {
                 if (one)
-                    hipLaunchKernelGGL((k_shade<STATS, 0, SH_FUSED, FEAT, true>), dim3(P.num_tiles), dim3(256), 0, st, S,
-                                       C, P, s, W, O, cnt);
+                    hipLaunchKernelGGL((k_shade<STATS, 0, SH_FUSED, FEAT, true>), dim3(nb), dim3(256), 0, st, S, C, Pp,
+                                       s, W, O, cnt);
                 else
-                    hipLaunchKernelGGL((k_shade<STATS, 0, SH_FUSED_N, FEAT, true>), dim3(P.num_tiles), dim3(256), 0, st,
-                                       S, C, P, s, W, O, cnt);
+                    hipLaunchKernelGGL((k_shade<STATS, 0, SH_FUSED_N, FEAT, true>), dim3(nb), dim3(256), 0, st, S, C,
+                                       Pp, s, W, O, cnt);
             }
             if (e5) (void)hipEventRecord(e5[2], st);
         } else if (one) {
-            e = wave_shade(STATS, sk, true, S, C, P, s, W, O, cnt, st);
+            e = wave_shade(STATS, sk, true, S, C, Pp, s, W, O, cnt, st);
             if (e != hipSuccess) return e;
             if (e5) (void)hipEventRecord(e5[2], st);
             if (nshadow > 0) {
                 if (defer_any) {
                     if constexpr (!STATS && (FEAT & FEAT_BIGLEAF)) {
-                        if (defer_any == 1) {            // RTG_DEFER_ANY=1: always the deferring walk
-                            hipLaunchKernelGGL((k_shadow_one<STATS, FEAT, true, true>), dim3(P.num_tiles), dim3(256), 0,
-                                               st, S, C, P, s, W, O, cnt);
-                            hipLaunchKernelGGL((k_bigleaf_any<FEAT>), dim3(2048), dim3(256), 0, st, S, W);
-                            hipLaunchKernelGGL((k_shadow_fin_one<FEAT, 0>), dim3(P.num_tiles), dim3(256), 0, st, S, C,
-                                               P, s, W, O);
-                        } else {                         // chosen on the device (GATE)
-                            hipLaunchKernelGGL((k_shadow_one<STATS, FEAT, false, false, -1>), dim3(P.num_tiles),
-                                               dim3(256), 0, st, S, C, P, s, W, O, cnt);
-                            hipLaunchKernelGGL((k_shadow_one<STATS, FEAT, true, true, 1>), dim3(P.num_tiles), dim3(256),
-                                               0, st, S, C, P, s, W, O, cnt);
-                            hipLaunchKernelGGL((k_bigleaf_any<FEAT>), dim3(2048), dim3(256), 0, st, S, W);
-                            hipLaunchKernelGGL((k_shadow_fin_one<FEAT, 1>), dim3(P.num_tiles), dim3(256), 0, st, S, C,
-                                               P, s, W, O);
-                        }
+                        hipLaunchKernelGGL((k_shadow_one<STATS, FEAT, true, true>), dim3(nb), dim3(256), 0, st, S, C, Pp,
+                                           s, W, O, cnt);
+                        hipLaunchKernelGGL((k_bigleaf_any<FEAT>), dim3(2048), dim3(256), 0, st, S, W);
+                        hipLaunchKernelGGL((k_shadow_fin_one<FEAT>), dim3(nb), dim3(256), 0, st, S, C, Pp, s, W, O);
                     }
                 } else if (fast)
-                    hipLaunchKernelGGL((k_shadow_one<STATS, FEAT, true>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P,
-                                       s, W, O, cnt);
+                    hipLaunchKernelGGL((k_shadow_one<STATS, FEAT, true>), dim3(nb), dim3(256), 0, st, S, C, Pp, s, W, O,
+                                       cnt);
                 else
-                    hipLaunchKernelGGL((k_shadow_one<STATS, FEAT, false>), dim3(P.num_tiles), dim3(256), 0, st, S, C,
-                                       P, s, W, O, cnt);
+                    hipLaunchKernelGGL((k_shadow_one<STATS, FEAT, false>), dim3(nb), dim3(256), 0, st, S, C, Pp, s, W,
+                                       O, cnt);
             }
             if (e5) (void)hipEventRecord(e5[3], st);
         } else {
-            e = wave_shade(STATS, SK_ALL, false, S, C, P, s, W, O, cnt, st);
+            e = wave_shade(STATS, SK_ALL, false, S, C, Pp, s, W, O, cnt, st);
             if (e != hipSuccess) return e;
             if (e5) (void)hipEventRecord(e5[2], st);
             if (nshadow > 0) {
+                const dim3 g(nb, nshadow);
                 if (defer_any) {
                     if constexpr (!STATS && (FEAT & FEAT_BIGLEAF)) {
-                        const dim3 g(P.num_tiles, nshadow);
-                        if (defer_any == 1) {
-                            hipLaunchKernelGGL((k_shadow<STATS, FEAT, true, true>), g, dim3(256), 0, st, S, W, cnt);
-                            hipLaunchKernelGGL((k_bigleaf_any<FEAT>), dim3(2048), dim3(256), 0, st, S, W);
-                            hipLaunchKernelGGL((k_shadow_fin<FEAT, 0>), g, dim3(256), 0, st, S, W);
-                        } else {
-                            hipLaunchKernelGGL((k_shadow<STATS, FEAT, false, false, -1>), g, dim3(256), 0, st, S, W, cnt);
-                            hipLaunchKernelGGL((k_shadow<STATS, FEAT, true, true, 1>), g, dim3(256), 0, st, S, W, cnt);
-                            hipLaunchKernelGGL((k_bigleaf_any<FEAT>), dim3(2048), dim3(256), 0, st, S, W);
-                            hipLaunchKernelGGL((k_shadow_fin<FEAT, 1>), g, dim3(256), 0, st, S, W);
-                        }
+                        hipLaunchKernelGGL((k_shadow<STATS, FEAT, true, true>), g, dim3(256), 0, st, S, W, cnt);
+                        hipLaunchKernelGGL((k_bigleaf_any<FEAT>), dim3(2048), dim3(256), 0, st, S, W);
+                        hipLaunchKernelGGL((k_shadow_fin<FEAT>), g, dim3(256), 0, st, S, W);
                     }
                 } else if (fast) {
-                    hipLaunchKernelGGL((k_shadow<STATS, FEAT, true>), dim3(P.num_tiles, nshadow), dim3(256), 0, st, S,
-                                       W, cnt);
+                    hipLaunchKernelGGL((k_shadow<STATS, FEAT, true>), g, dim3(256), 0, st, S, W, cnt);
                 } else {
-                    hipLaunchKernelGGL((k_shadow<STATS, FEAT, false>), dim3(P.num_tiles, nshadow), dim3(256), 0, st, S,
-                                       W, cnt);
+                    hipLaunchKernelGGL((k_shadow<STATS, FEAT, false>), g, dim3(256), 0, st, S, W, cnt);
                 }
             }
             if (e5) (void)hipEventRecord(e5[3], st);
-            wave_resolve(C, P, s, W, O, st);
+            wave_resolve(C, Pp, s, W, O, st);
             if (e5) (void)hipEventRecord(e5[4], st);
         }
+        if (O.col) wave_accum(C, Pp, s, W, O, st);
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }

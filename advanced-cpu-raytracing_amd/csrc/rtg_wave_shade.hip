@@ -5,12 +5,13 @@
 
 namespace rtg {
 
-__global__ __launch_bounds__(256) void k_resolve(const DevCamera C, const RenderParams P, const int sample,
+__global__ __launch_bounds__(256) void k_resolve(const DevCamera C, const RenderParams P, const int sample0,
                                                  const WaveBufs W, const PassOut O) {
+    // entries of the pass's slabs (work_index): slab, compact row, column
     const int i = blockIdx.x * 256 + threadIdx.x;
-    const int npix = P.part_rows * C.width;
-    if (i >= npix) return;
-    const int pixel = part_pixel(P, C.width, i);
+    const int slab = i / P.slab_px, r = i - slab * P.slab_px, crow = r / C.width;
+    if (slab >= P.slabs || crow >= P.part_rows) return;
+    const int pixel = part_row(P, crow) * C.width + (r - crow * C.width);
     const float4 b = W.base[i];
     const int flags = __float_as_int(b.w);
     f3 color = mk(b.x, b.y, b.z);
@@ -25,7 +26,19 @@ __global__ __launch_bounds__(256) void k_resolve(const DevCamera C, const Render
         color = add(color, sum);
         if (flags & BASE_ADD_ZERO) color = add(color, mk(0, 0, 0));   // depth-0 mirror/dielectric/conductor
     }
-    finish_pixel(C, P, sample, O, pixel, color);
+    finish_pixel(C, P, sample0 + slab, O, pixel, slab, color);
+}
+
+// A multi-sample pass's colours (O.col, one per slab and pixel) into the pixels' accumulation,
+// in sample order (accum_samples): the image of one-sample passes, bit for bit.
+__global__ __launch_bounds__(256) void k_accum(const DevCamera C, const RenderParams P, const int sample0,
+                                               const PassOut O) {
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int crow = i / C.width;
+    if (crow >= P.part_rows) return;
+    const int pixel = part_row(P, crow) * C.width + (i - crow * C.width);
+    accum_samples(C, P, sample0, P.slabs, O.first, O.last, pixel, O.col + i, (size_t)P.slab_px, O.accum, O.hdr,
+                  O.ldr);
 }
 
 // RTG_WIDE_BIGLEAF=1: shadow rays of large-leaf scenes also take the any-hit wide walk
@@ -57,21 +70,14 @@ bool defer_leaves() {
     return !v || std::strcmp(v, "0") != 0;
 }
 
-// RTG_DEFER_ANY: shadow rays of large-leaf scenes -- 0 the cooperative reference walk, 1 or
-// unset the deferring any-hit walk, 2 chosen per pass on the device (GATE, rtg_common.hpp).
-// Round 5, with the lean any-hit walk, the deferring walk wins on every large-leaf config
-// (C3 5 527 -> 5 872, C3-ton 5 517 -> 5 602, C4 3 165 -> 3 164 Mrays/s against the per-pass
-// choice; profiles/r05q_deferany_ab.txt)
-// RTG_DEFER_ANY_GATE=g: the deferring walk when the camera pass reached large leaves with at
-// least pixels / g lanes (default 50: 2 %)
-int defer_any_gate() {
-    const char* v = std::getenv("RTG_DEFER_ANY_GATE");
-    return v && std::atoi(v) > 0 ? std::atoi(v) : 50;
-}
-
-int defer_any_leaves() {
+// RTG_DEFER_ANY: shadow rays of large-leaf scenes -- 0 the cooperative reference walk (A/B,
+// exactness cross-check), unset or 1 the deferring any-hit walk.  Round 5, with the lean
+// any-hit walk, the deferring walk won on every large-leaf config against round 4's per-pass
+// choice on the device (C3 5 527 -> 5 872, C3-ton 5 517 -> 5 602, C4 3 165 -> 3 164 Mrays/s;
+// profiles/r05q_deferany_ab.txt), which was then removed
+bool defer_any_leaves() {
     const char* v = std::getenv("RTG_DEFER_ANY");
-    return !v ? 1 : std::strcmp(v, "0") == 0 ? 0 : std::strcmp(v, "2") == 0 ? 2 : 1;
+    return !v || std::strcmp(v, "0") != 0;
 }
 
 // The fused layout's two kernels as one (k_shade<..., FRAME>, default since round 5;
@@ -90,13 +96,14 @@ template <bool STATS>
 static hipError_t wave_shade_t(int sk, bool one, const DevScene& S, const DevCamera& C, const RenderParams& P,
                                int s, const WaveBufs& W, const PassOut& O, DevCounters* cnt, hipStream_t st) {
     if (!one) {
-        hipLaunchKernelGGL((k_shade<STATS, SK_ALL, SH_GENERAL>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, O,
-                           cnt);
+        hipLaunchKernelGGL((k_shade<STATS, SK_ALL, SH_GENERAL>), dim3(P.slab_tiles * P.slabs), dim3(256), 0, st, S, C,
+                           P, s, W, O, cnt);
         return hipGetLastError();
     }
 #define RTG_SK(K)                                                                                                  \
     case K:                                                                                                        \
-        hipLaunchKernelGGL((k_shade<STATS, K, SH_ONE>), dim3(P.num_tiles), dim3(256), 0, st, S, C, P, s, W, O, cnt); \
+        hipLaunchKernelGGL((k_shade<STATS, K, SH_ONE>), dim3(P.slab_tiles * P.slabs), dim3(256), 0, st, S, C, P, s, W, \
+                           O, cnt);                                                                                 \
         break
     switch (sk & SK_ALL) {
         RTG_SK(0); RTG_SK(1); RTG_SK(2); RTG_SK(3); RTG_SK(4); RTG_SK(5); RTG_SK(6);
@@ -114,8 +121,14 @@ hipError_t wave_shade(bool stats, int sk, bool one, const DevScene& S, const Dev
 
 void wave_resolve(const DevCamera& C, const RenderParams& P, int sample, const WaveBufs& W, const PassOut& O,
                   hipStream_t st) {
+    const long long n = P.slabs > 1 ? (long long)P.slabs * P.slab_px : (long long)P.part_rows * C.width;
+    hipLaunchKernelGGL(k_resolve, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, C, P, sample, W, O);
+}
+
+void wave_accum(const DevCamera& C, const RenderParams& P, int sample, const WaveBufs& W, const PassOut& O,
+                hipStream_t st) {
     const int npix = P.part_rows * C.width;
-    hipLaunchKernelGGL(k_resolve, dim3((npix + 255) / 256), dim3(256), 0, st, C, P, sample, W, O);
+    hipLaunchKernelGGL(k_accum, dim3((npix + 255) / 256), dim3(256), 0, st, C, P, sample, O);
 }
 
 hipError_t launch_wave(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W, float* hdr,

@@ -31,6 +31,7 @@ RTG_RENDER_TIMING = 8
 RTG_RENDER_TREE = 16
 RTG_RENDER_EXACT_SHADOW = 32
 RTG_RENDER_ORDERED = 64
+RTG_RENDER_SAMPLE_PASSES = 128
 RTG_LOAD_DEVICE_BVH = 1
 RTG_CAMERA_SIZE = 392   # sizeof(rtg_camera), checked against the C compiler by tests/test_abi.py
 
@@ -91,7 +92,7 @@ EXPORTED = [
     "rtg_scene_export_bvh",
     "rtg_desc_camera_info", "rtg_desc_counts", "rtg_desc_anyhit_check", "rtg_scene_create", "rtg_scene_destroy",
     "rtg_device_count", "rtg_render", "rtg_render_device", "rtg_resolve_accum",
-    "rtg_scene_stats", "rtg_scene_reset_stats", "rtg_scene_timings", "rtg_tonemap_device", "rtg_tonemap",
+    "rtg_scene_stats", "rtg_scene_reset_stats", "rtg_scene_timings", "rtg_scene_timed_samples", "rtg_tonemap_device", "rtg_tonemap",
     "rtg_tonemap_log_average",
     "rtg_write_png", "rtg_write_hdr",
     "rtg_last_error", "rtg_abi_version",
@@ -141,6 +142,7 @@ def lib() -> ctypes.CDLL:
     L.rtg_scene_stats.argtypes = [vp, P(Stats)]
     L.rtg_scene_reset_stats.argtypes = [vp]
     L.rtg_scene_timings.argtypes = [vp, P(ctypes.c_float), P(ctypes.c_char_p), i32, P(i32)]
+    L.rtg_scene_timed_samples.argtypes = [vp, P(i32)]
     L.rtg_tonemap_device.argtypes = [vp, i32, i32, P(TonemapParams), vp, i32, vp]
     L.rtg_tonemap.argtypes = [vp, i32, i32, P(TonemapParams), vp, i32]
     L.rtg_tonemap_log_average.argtypes = [vp, i32, i32, i32, P(ctypes.c_double), i32]
@@ -312,6 +314,13 @@ class DeviceScene:
         n = ctypes.c_int32()
         _check(lib().rtg_scene_timings(self._s, ms, names, 8, ctypes.byref(n)))
         return {names[k].decode(): float(ms[k]) for k in range(n.value)}
+
+    def timed_samples(self) -> int:
+        """Samples per pixel the stages of timings() covered (the last pass of a multi-sample
+        render carries several, RTG_RENDER_SAMPLE_PASSES)."""
+        n = ctypes.c_int32()
+        _check(lib().rtg_scene_timed_samples(self._s, ctypes.byref(n)))
+        return n.value
 
     def close(self):
         if getattr(self, "_s", None):

@@ -139,43 +139,66 @@ def _median(v):
     return v[len(v) // 2]
 
 
-def cpu_baseline(xml_dir, xml, rays_per_frame, reps):
+# The CPU leg's sample per configuration: the whole frame, or a band of rows where the whole
+# frame would take minutes (C5: 2.2 G rays; C4: 59 M rays through the restatement) -- about
+# 10-30 s of CPU work per run.  C4 takes the restatement ("port"): the reference itself is
+# undefined behaviour on MeshInstance scenes (instancedMesh.hpp:23 + raytracer.cpp:590) and
+# crashes on C4.
+CPU_SAMPLE = {"c4": {"rows": (404, 676), "reps": 2, "kind": "port"},
+              "c5": {"rows": (1048, 1112), "reps": 1}}
+
+
+def cpu_baseline(xml_dir, xml, count_rays, reps, rows=None, kind=None):
     """The reference's CPU path (oracle/_ref/refdriver: its own sources, row-band threads
-    exactly as main.cpp:38-39,164-185) on this host, in SURVEY §8d's two modes: A = the
-    reference's THREAD_COUNT (8), B = every core of this box's share.  Per mode: the
-    render alone (thread spawn -> join) and the reference-equivalent span main.cpp:138->199
-    (Raytracer copy + render + PNG encode).  Falls back to the CPU restatement ("port") when
-    the reference build is absent."""
+    exactly as main.cpp:38-39,164-185 and each pixel's spp loop as renderThreadMain,
+    main.cpp:42-121) on this host, in SURVEY §8d's two modes: A = the reference's THREAD_COUNT
+    (8), B = every core of this box's share.  Per mode: the render alone (thread spawn -> join)
+    and the reference-equivalent span main.cpp:138->199 (Raytracer copy + render + PNG encode).
+    `rows`: a band of the frame (the rows each mode's threads cover exactly as main.cpp deals
+    them); `count_rays(r0, r1)` gives the rays of those rows from the GPU's counting render.
+    The CPU restatement ("port") when the reference build is absent or `kind` asks for it."""
     drv = os.path.join(ROOT, "oracle", "_ref", "refdriver")
     modes = {}
-    kind = "reference" if os.path.exists(drv) else "port"
+    kind = kind or ("reference" if os.path.exists(drv) else "port")
     for label, threads in (("A", 8), ("B", box_threads())):
         if kind == "reference":
-            out = subprocess.run([drv, "bench", os.path.basename(xml), str(threads), str(reps), "0",
-                                  os.path.join(xml_dir, "refdriver_bench.png")], cwd=xml_dir,
-                                 capture_output=True, text=True, timeout=900, check=True).stdout
+            cmd = [drv, "bench", os.path.basename(xml), str(threads), str(reps), "0",
+                   os.path.join(xml_dir, "refdriver_bench.png")]
+            if rows:
+                cmd += [str(rows[0]), str(rows[1])]
+            out = subprocess.run(cmd, cwd=xml_dir, capture_output=True, text=True, timeout=900, check=True).stdout
             rec = json.loads([ln for ln in out.splitlines() if ln.startswith("{")][-1])
             render_s, span_s = _median(rec["seconds"]), _median(rec["span_seconds"])
+            r0, r1 = rec["rows"]
         else:
             sys.path.insert(0, os.path.join(ROOT, "tests"))
             import oracle_bind as ob
             import rtgpu
             hs = rtgpu.HostScene(xml)
+            h = hs.camera(0)["height"]
+            r0, r1 = rows or (0, h)
+            r1 = r0 + (r1 - r0) // threads * threads       # the rows main.cpp's threads would cover
             secs = []
             for _ in range(reps):
                 t0 = time.perf_counter()
-                ob.render(hs, threads=threads)
+                ob.render(hs, rows=(r0, r1), threads=threads)
                 secs.append(time.perf_counter() - t0)
             render_s = span_s = _median(secs)
-        modes[label] = {"threads": threads, "render_s": round(render_s, 4), "span_s": round(span_s, 4),
-                        "mrays_s": round(rays_per_frame / render_s / 1e6, 3),
-                        "span_mrays_s": round(rays_per_frame / span_s / 1e6, 3)}
-        log(f"cpu baseline mode {label}: {threads} threads, {modes[label]['mrays_s']} Mrays/s")
+            hs.close()
+        rays = count_rays(r0, r1)
+        modes[label] = {"threads": threads, "rows": [r0, r1], "rays": int(rays), "render_s": round(render_s, 4),
+                        "span_s": round(span_s, 4), "mrays_s": round(rays / render_s / 1e6, 3),
+                        "span_mrays_s": round(rays / span_s / 1e6, 3)}
+        log(f"cpu baseline mode {label}: {threads} threads, rows {r0}-{r1}, {modes[label]['mrays_s']} Mrays/s")
     a = modes["A"]
+    what = "the reference itself (oracle/_ref/refdriver)" if kind == "reference" else \
+        "the CPU restatement (oracle/cpu_oracle.cpp, liboracle.so)"
+    band = (f"rows {a['rows'][0]}-{a['rows'][1]} of the frame" if rows else "full frame")
     return {"value": a["mrays_s"], "unit": "Mrays/s", "cores": a["threads"], "kind": kind,
-            "sample": f"full {os.path.basename(xml)} frame x {reps} reps per mode; value = mode A (the reference's "
-                      f"THREAD_COUNT=8, render only: spawn->join, main.cpp:164-185); mode B = the box's "
-                      f"{modes['B']['threads']} cores; span = main.cpp:138->199 (Raytracer copy + render + PNG)",
+            "sample": f"{band} of {os.path.basename(xml)} ({a['rays']} rays, every sample per pixel) x {reps} reps "
+                      f"per mode, {what}; value = mode A (THREAD_COUNT=8, render only: spawn->join, "
+                      f"main.cpp:164-185); mode B = the box's {modes['B']['threads']} cores; span = "
+                      f"main.cpp:138->199 (Raytracer copy + render + PNG)",
             "cpu_model": cpu_model(), "host_cpus_visible": os.cpu_count(), "modes": modes}
 
 
@@ -527,8 +550,10 @@ def main():
         s_el = reduce_max(s_el)
 
         ktimes = kernel_times(ds, torch, lambda: render(rtgpu.RTG_RENDER_TIMING), args.steps)
-        # the library times the kernels of the last sample pass: bytes of this rank's pass
-        kbytes = {k: v / max(1, cam["spp"]) for k, v in kernel_bytes(part_st, W, H).items()}
+        # the library times the kernels of the last pass (its samples: several per pass in the
+        # wavefront and ray-tree pipelines): bytes of this rank's pass
+        pass_samples = ds.timed_samples()
+        kbytes = {k: v * pass_samples / max(1, cam["spp"]) for k, v in kernel_bytes(part_st, W, H).items()}
         dom = max((k for k in ktimes if k in kbytes), key=lambda k: ktimes[k])
         K = int(args.K) if args.config == "headline" else None
         share = part_rays / max(rays, 1)
@@ -657,9 +682,21 @@ def main():
                 sweep[str(Ks)] = sweep_point(args, torch, rtgpu, local, Ks, hdr, ldr)
             result["sweep_K"] = sweep
         # the reference's CPU path on this host, rank 0 only, outside the timed region, at every N
-        # (the same whole frame: its rate does not depend on how the GPUs split it)
-        if rank == 0 and not args.no_cpu_baseline and args.config == "headline":
-            result["cpu_baseline"] = cpu_baseline(tmp, xml, rays, args.cpu_reps)
+        # (the same frame or row band: its rate does not depend on how the GPUs split it); the
+        # rays of the rows it renders from this GPU's counting render of those rows
+        if rank == 0 and not args.no_cpu_baseline:
+            def count_rays(r0, r1):
+                if (r0, r1) == (0, H) and world == 1:
+                    return rays
+                ds.reset_stats()
+                ds.render_device(hdr.data_ptr(), ldr.data_ptr(), sptr, seed=seed, rows=(r0, r1),
+                                 flags=rtgpu.RTG_RENDER_COUNT_STATS)
+                torch.cuda.synchronize()
+                s_ = ds.stats()
+                return s_["camera_rays"] + s_["secondary_rays"] + s_["shadow_rays"]
+            cs = CPU_SAMPLE.get(args.config, {})
+            result["cpu_baseline"] = cpu_baseline(tmp, xml, count_rays, cs.get("reps", args.cpu_reps),
+                                                  rows=cs.get("rows"), kind=cs.get("kind"))
         if rank == 0:
             print(json.dumps(result), flush=True)
         barrier()     # the other ranks wait for rank 0's CPU leg before tearing the group down

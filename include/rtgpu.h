@@ -26,7 +26,7 @@
 extern "C" {
 #endif
 
-#define RTG_ABI_VERSION 5
+#define RTG_ABI_VERSION 6
 
 enum rtg_status {
     RTG_OK = 0,
@@ -308,11 +308,18 @@ enum rtg_render_flags {
                                      fused kernel bit for bit)                         */
     RTG_RENDER_EXACT_SHADOW = 32, /* shadow rays walk the reference BVH instead of the
                                      any-hit wide BVH (same answers; for cross-checks)  */
-    RTG_RENDER_ORDERED = 64       /* opt-in (ABI 4): camera rays of plain mesh scenes walk
+    RTG_RENDER_ORDERED = 64,      /* opt-in (ABI 4): camera rays of plain mesh scenes walk
                                      the 4-wide BVH nearest child first with a checked
                                      result (the reference walk where the check fails);
                                      agreement with the reference order is measured, not
                                      proven -- DESIGN.md §5                          */
+    RTG_RENDER_SAMPLE_PASSES = 128 /* ABI 6: one sample per pass.  By default the wavefront
+                                     and ray-tree pipelines carry several consecutive
+                                     samples of the rendered pixels in one pass (about
+                                     8 Mi camera rays per pass; env RTG_PASS_RAYS) and
+                                     add each pixel's samples in sample order, so the image
+                                     is the same bit for bit; this flag restores one
+                                     sample per pass (for cross-checks)               */
 };
 
 typedef struct {
@@ -414,6 +421,10 @@ int rtg_scene_reset_stats(rtg_scene* scene);
  * kernel: "k_render"; ray-tree pipeline: "tree_levels" (all levels' trace / shade /
  * shadow kernels), "tree_resolve".  Writes up to `cap` entries; *count = number of stages. */
 int rtg_scene_timings(rtg_scene* scene, float* ms, const char** names, int32_t cap, int32_t* count);
+/* ABI 6: samples per pixel the stages rtg_scene_timings reports covered -- the last pass's
+ * samples (a pass carries several, RTG_RENDER_SAMPLE_PASSES), or the whole render's for the
+ * fused kernel. */
+int rtg_scene_timed_samples(const rtg_scene* scene, int32_t* samples);
 
 /* ------------------------------------------------------------------------- */
 /* Tonemapping (tonemapper.h, main.cpp:187-192)                               */

@@ -12,11 +12,15 @@
 //       Stochastic scenes (path tracing, area / environment lights): n RenderPixel calls per
 //       pixel, single-threaded.  Writes "RTGV" int32 w, h, n, then the per-pixel mean and
 //       the variance of that mean (w*h*3 float32 each) -- the statistical golden.
-//   refdriver bench <scene.xml> <threads> <reps> [camera] [png]
+//   refdriver bench <scene.xml> <threads> <reps> [camera] [png] [row_begin row_end]
 //       Times the reference's row-band render exactly as main.cpp:164-185 partitions it
-//       (rows [t*(H/T), (t+1)*(H/T)) per thread; spawn -> join), spp==1 per pixel via
-//       RenderPixel, and the reference-equivalent span main.cpp:138-199 (Raytracer copy +
-//       render + PNG encode); prints one JSON line with the per-rep seconds of both.
+//       (rows [t*(H/T), (t+1)*(H/T)) per thread; spawn -> join), each pixel as
+//       renderThreadMain does it (main.cpp:42-121: one RenderPixel, or for spp > 1 the
+//       stratified jitter from the thread's mt19937, spp RenderPixel calls and the Gaussian2D
+//       weighting of gaussian.h), and the reference-equivalent span main.cpp:138-199
+//       (Raytracer copy + render + PNG encode); prints one JSON line with the per-rep seconds
+//       of both.  With row_begin / row_end only those rows are rendered (a bounded sample of a
+//       long frame), dealt to the threads the same way.
 //   refdriver imgdump <image file> <out.bin>
 //       The reference's own image classes as parser.cpp:103-110 picks them: HDRImage (tinyexr
 //       LoadEXR) for a ".exr" name, else LDRImage (stbi_load).  Writes "RTGI" int32 w, h,
@@ -38,9 +42,12 @@
 #include <algorithm>
 #include <vector>
 
+#include <random>
+
 #include "raytracer.hpp"
 #undef STB_IMAGE_IMPLEMENTATION          // emitted once above (raytracer.hpp -> image.h)
 #include "LDRImage.h"
+#include "gaussian.h"
 
 using namespace DorkTracer;
 
@@ -139,11 +146,46 @@ static int dumpavg(const char* xml, const char* out, int n, int ci) {
 // main.cpp:138 -> 199 for one camera: Raytracer copy-construction (main.cpp:140), the
 // LDR frame buffer, the threaded render with the clamp of main.cpp:118-124, and the PNG
 // encode of main.cpp:197 (written to png_out, "" = /dev/null-like temp name).
-static int bench(const char* xml, int threads, int reps, int ci, const char* png_out) {
+// One pixel as renderThreadMain computes it (main.cpp:57-101), the thread's generator and
+// sample vector passed in.
+static Vec3f bench_pixel(Raytracer& renderer, Camera& cam, int x, int y, std::mt19937& gen,
+                         std::uniform_real_distribution<>& u01, std::vector<Vec2f>& samples, Gaussian2D& g) {
+    const int spp = cam.samplesPerPixel;
+    if (spp <= 1) return renderer.RenderPixel(x, y, cam);
+    const int n = (int)std::sqrt(spp);
+    int i = 0;
+    for (int r = 0; r < n; ++r)
+        for (int c = 0; c < n; ++c) {
+            const float p1 = u01(gen), p2 = u01(gen);
+            samples[i].x = (c + p1) / n;
+            samples[i].y = (r + p2) / n;
+            ++i;
+        }
+    Vec3f col{0.0f, 0.0f, 0.0f};
+    float wsum = 0.0f;
+    for (i = 0; i < spp; ++i) {
+        // (RenderPixel takes int coordinates: the jitter only moves the Gaussian weight)
+        const Vec3f v = renderer.RenderPixel(samples[i].x + x, samples[i].y + y, cam);
+        const float gw = g.GetWeight(samples[i].x - 0.5f, samples[i].y - 0.5f);
+        col.x += v.x * gw;
+        col.y += v.y * gw;
+        col.z += v.z * gw;
+        wsum += gw;
+    }
+    col.x = col.x / wsum;
+    col.y = col.y / wsum;
+    col.z = col.z / wsum;
+    return col;
+}
+
+static int bench(const char* xml, int threads, int reps, int ci, const char* png_out, int rb, int re) {
     Scene scene;
     scene.loadFromXml(xml);
     Camera& cam = scene.cameras[ci];
     const int w = cam.imageWidth, h = cam.imageHeight;
+    if (re <= 0 || re > h) re = h;
+    if (rb < 0 || rb >= re) rb = 0;
+    const int band = re - rb;
     std::vector<float> img((size_t)w * h * 3);
     std::vector<double> render_s, span_s;
     for (int r = 0; r < reps; ++r) {
@@ -155,10 +197,14 @@ static int bench(const char* xml, int threads, int reps, int ci, const char* png
         std::vector<std::thread> th;
         for (int t = 0; t < threads; ++t) {
             th.emplace_back([&, t]() {
-                int y0 = t * (h / threads), y1 = y0 + h / threads;
+                int y0 = rb + t * (band / threads), y1 = y0 + band / threads;
+                std::mt19937 gen(rand());
+                std::uniform_real_distribution<> u01(0.0f, 1.0f);
+                std::vector<Vec2f> samples(std::max(1, cam.samplesPerPixel));
+                Gaussian2D g(1.0f / 6.0f);
                 for (int y = y0; y < y1; ++y)
                     for (int x = 0; x < w; ++x) {
-                        Vec3f c = renderer.RenderPixel(x, y, cam);
+                        Vec3f c = bench_pixel(renderer, cam, x, y, gen, u01, samples, g);
                         size_t i = 3 * ((size_t)x + (size_t)y * w);
                         img[i] = c.x; img[i + 1] = c.y; img[i + 2] = c.z;
                         Vec3i q = clamp(c);
@@ -175,7 +221,8 @@ static int bench(const char* xml, int threads, int reps, int ci, const char* png
     }
     double checksum = 0;
     for (float v : img) checksum += v;
-    std::printf("{\"threads\": %d, \"width\": %d, \"height\": %d, \"seconds\": [", threads, w, h);
+    std::printf("{\"threads\": %d, \"width\": %d, \"height\": %d, \"spp\": %d, \"rows\": [%d, %d], \"seconds\": [",
+                threads, w, h, cam.samplesPerPixel, rb, rb + (band / threads) * threads);
     for (size_t r = 0; r < render_s.size(); ++r) std::printf("%s%.6f", r ? ", " : "", render_s[r]);
     std::printf("], \"span_seconds\": [");
     for (size_t r = 0; r < span_s.size(); ++r) std::printf("%s%.6f", r ? ", " : "", span_s[r]);
@@ -213,7 +260,8 @@ int main(int argc, char** argv) {
         return dumpavg(argv[2], argv[3], std::atoi(argv[4]), argc > 5 ? std::atoi(argv[5]) : 0);
     if (argc >= 5 && !std::strcmp(argv[1], "bench"))
         return bench(argv[2], std::atoi(argv[3]), std::atoi(argv[4]), argc > 5 ? std::atoi(argv[5]) : 0,
-                     argc > 6 ? argv[6] : "refdriver_bench.png");
+                     argc > 6 ? argv[6] : "refdriver_bench.png", argc > 8 ? std::atoi(argv[7]) : 0,
+                     argc > 8 ? std::atoi(argv[8]) : 0);
     std::fprintf(stderr, "usage: refdriver dump <scene.xml> <out.bin> [camera] | bench <scene.xml> <threads> <reps> [camera]\n");
     return 2;
 }

@@ -37,7 +37,7 @@ def test_library_exports_every_declared_symbol():
 
 
 def test_abi_version():
-    assert rtgpu.lib().rtg_abi_version() == 5
+    assert rtgpu.lib().rtg_abi_version() == 6
 
 
 def test_struct_layouts_are_plain_c(tmp_path):

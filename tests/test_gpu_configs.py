@@ -159,8 +159,7 @@ def test_large_leaf_cooperative_walk_small(cfg, in_tmp):
 def test_deferred_large_leaves(name, in_tmp, monkeypatch):
     """Large-leaf scenes: the camera walk defers its large leaves to k_bigleaf and settles each
     pixel in k_hitfix (the winner's leaf box checked at next_up(t), rtg_common.hpp DeferCtx), the
-    shadow walk queues its large leaves to k_bigleaf_any (AnyDefer; by default always,
-    RTG_DEFER_ANY=2 when the camera pass queued enough of them) -- bit for bit the image of the cooperative
+    shadow walk queues its large leaves to k_bigleaf_any (AnyDefer) -- bit for bit the image of the cooperative
     reference walk (RTG_DEFER=0), of camera deferral alone (RTG_DEFER_ANY=0) and of the counting
     render (which never defers)."""
     if name == "c3_small":
@@ -175,9 +174,6 @@ def test_deferred_large_leaves(name, in_tmp, monkeypatch):
     hs0, ds0 = _scene(xml0)
     a, la = ds0.render(0, seed=9)
     c, lc = ds0.render(0, seed=9, flags=rtgpu.RTG_RENDER_COUNT_STATS)
-    monkeypatch.setenv("RTG_DEFER_ANY", "2")   # shadow rays: the walk chosen per pass on the device
-    e, le = ds0.render(0, seed=9)
-    assert np.array_equal(a.view(np.uint32), e.view(np.uint32)) and np.array_equal(la, le)
     monkeypatch.setenv("RTG_DEFER_ANY", "0")   # shadow rays: the cooperative walk
     d, ld = ds0.render(0, seed=9)
     monkeypatch.setenv("RTG_DEFER", "0")

@@ -212,11 +212,9 @@ def test_cli_devices(tmp_path):
 @pytest.mark.parametrize("part,rows", [((0, 1), (0, 0)), ((1, 2), (0, 0)), ((2, 3), (0, 0)), ((5, 8), (0, 0)),
                                        ((0, 1), (100, 1000)), ((3, 4), (37, 1080))])
 def test_host_path_variants_equal_one_launch(part, rows, tmp_path, monkeypatch):
-    """rtg_render's host-path variants write exactly the rows and bits of the default one-launch
-    path (render + copy), for whole frames, parts of a partition and row ranges: the chunked
-    path (RTG_HOST_CHUNKS: row chunks of whole band rounds on two streams, each chunk's rows
-    copied while the next renders) and direct writes into a page-locked frame
-    (RTG_HOST_DIRECT)."""
+    """rtg_render's host paths write exactly the rows and bits of the one-launch render + copy,
+    for whole frames, parts of a partition and row ranges: into pageable frames (render + copy)
+    and straight into a page-locked frame (RTG_HOST_DIRECT, the default for such frames)."""
     import scenes
     xml = scenes.synthetic_heightfield(str(tmp_path), K=10082, width=1920, height=1080)
     old = os.getcwd()
@@ -226,9 +224,7 @@ def test_host_path_variants_equal_one_launch(part, rows, tmp_path, monkeypatch):
         ds = rtgpu.DeviceScene(hs, 0)
         init = lambda: (np.full((1080, 1920, 3), -1.0, np.float32), np.full((1080, 1920, 3), 7, np.uint8))  # noqa: E731
         b = ds.render(0, rows=rows, part=part, seed=3, out=init())
-        monkeypatch.setenv("RTG_HOST_CHUNKS", "8")
         a = ds.render(0, rows=rows, part=part, seed=3, out=init())
-        monkeypatch.delenv("RTG_HOST_CHUNKS")
         monkeypatch.delenv("RTG_HOST_DIRECT", raising=False)        # the default for page-locked frames
         ph, pl = rtgpu.PinnedArray((1080, 1920, 3), "float32"), rtgpu.PinnedArray((1080, 1920, 3), "uint8")
         ph.array[...] = -1.0

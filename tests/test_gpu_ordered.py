@@ -1,5 +1,5 @@
 """Ordered closest hit (RTG_RENDER_ORDERED: rtg_common.hpp trace_closest_pk on the any-hit tree
-as wave packets, or round 3's trace_ordered with RTG_ORDERED_WALK=collapsed) against the
+as wave packets) against the
 reference-order walk it replaces for camera rays of plain mesh scenes.
 
 The reference's IntersectObjects (raytracer.cpp:625-643) walks each BVH left child first
@@ -65,12 +65,8 @@ def test_ordered_equals_reference_order(name):
     _check(ds, name)
 
 
-@pytest.mark.parametrize("walk", ["sah_packet", "collapsed"])
-def test_ordered_headline_full_size(tmp_path, walk, monkeypatch):
-    """Both ordered walks on the full headline: the any-hit tree as wave packets (mode 2, the
-    default) and round 3's per-lane walk of the collapsed reference tree (RTG_ORDERED_WALK)."""
-    if walk == "collapsed":
-        monkeypatch.setenv("RTG_ORDERED_WALK", "collapsed")
+def test_ordered_headline_full_size(tmp_path):
+    """The ordered walk (the any-hit tree as wave packets) on the full headline."""
     import scenes
     xml = scenes.synthetic_heightfield(str(tmp_path), K=100352)
     old = os.getcwd()

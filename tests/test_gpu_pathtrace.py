@@ -123,11 +123,9 @@ def _bits(a):
     return a.view(np.uint32)
 
 
-# step kernel modes: split by node kind; one kernel as chosen by the camera (regeneration with
-# Russian roulette), with path regeneration forced, and with a pass per sample
-MODES = {"split": {"RTG_PATH_SPLIT": "1"}, "default": {"RTG_PATH_SPLIT": "0"},
-         "regen": {"RTG_PATH_SPLIT": "0", "RTG_PATH_REGEN": "1"},
-         "noregen": {"RTG_PATH_SPLIT": "0", "RTG_PATH_REGEN": "0"}}
+# step kernel modes: as chosen by the camera (regeneration with Russian roulette), with path
+# regeneration forced, and with a pass per sample
+MODES = {"default": {}, "regen": {"RTG_PATH_REGEN": "1"}, "noregen": {"RTG_PATH_REGEN": "0"}}
 
 
 @pytest.mark.parametrize("mode", list(MODES))
@@ -137,9 +135,8 @@ def test_path_wavefront_equals_fused(name, spp, mode, tmp_path, monkeypatch):
     """The wavefront path tracer (rtg_path.hip, forced with RTG_RENDER_TREE) gives the fused
     kernel's image bit for bit: the same node steps (rtg_node.hpp) on the same RNG keys -- with
     the step as one kernel (the default), with or without path regeneration (a finished sample's
-    slot starting the pixel's next sample inside the pass; by default with Russian roulette), and
-    split by node kind
-    (RTG_PATH_SPLIT=1: k_path_hit / k_path_rest / k_path_unwind).  The first render plans its
+    slot starting the pixel's next sample inside the pass; by default with Russian roulette).
+    The first render plans its
     later passes from its first; the second runs planned throughout."""
     for k, v in MODES[mode].items():
         monkeypatch.setenv(k, v)
@@ -154,14 +151,12 @@ def test_path_wavefront_equals_fused(name, spp, mode, tmp_path, monkeypatch):
     assert "path_iterations" in ds.timings()
 
 
-@pytest.mark.parametrize("split", ["1", "0"])
 @pytest.mark.parametrize("env", ["RTG_PATH_SYNC", "RTG_PATH_PLAN_TIGHT"])
-def test_path_wavefront_host_driven_and_overflow(env, split, tmp_path, monkeypatch):
+def test_path_wavefront_host_driven_and_overflow(env, tmp_path, monkeypatch):
     """Every pass host-driven (RTG_PATH_SYNC), and plans one iteration short
     (RTG_PATH_PLAN_TIGHT: every planned pass leaves paths, the render is redone host-driven):
     the same image as the fused kernel."""
     monkeypatch.setenv(env, "1")
-    monkeypatch.setenv("RTG_PATH_SPLIT", split)
     hs = _scene(tmp_path, "pt_nee", 4)
     ds = rtgpu.DeviceScene(hs, 0)
     b, _ = ds.render(0, seed=5, flags=rtgpu.RTG_RENDER_FUSED)
@@ -171,11 +166,9 @@ def test_path_wavefront_host_driven_and_overflow(env, split, tmp_path, monkeypat
 
 
 @pytest.mark.parametrize("name", ["pt_cornell", "pt_nee"])
-@pytest.mark.parametrize("split", ["1", "0"])
-def test_path_wavefront_stats_and_bands(name, split, tmp_path, monkeypatch):
+def test_path_wavefront_stats_and_bands(name, tmp_path, monkeypatch):
     """Ray counts of the wavefront path tracer equal the fused kernel's; row bands rendered
     separately give the whole frame (part_pixel mapping of the path queues)."""
-    monkeypatch.setenv("RTG_PATH_SPLIT", split)
     hs = _scene(tmp_path, name, 2)
     ds = rtgpu.DeviceScene(hs, 0)
     ds.reset_stats()
@@ -199,7 +192,6 @@ def test_path_regeneration_passes_and_sample_ranges(regen, tmp_path, monkeypatch
     with sample ranges accumulated separately (RTG_RENDER_ACCUM_ONLY, samples [0, 3) and
     [3, 7)): the fused kernel's bits, so each pixel's samples are still summed in sample order."""
     torch = pytest.importorskip("torch")
-    monkeypatch.setenv("RTG_PATH_SPLIT", "0")
     monkeypatch.setenv("RTG_PATH_REGEN", regen)
     hs = _scene(tmp_path, "pt_rr", 70)
     ds = rtgpu.DeviceScene(hs, 0)
@@ -218,3 +210,22 @@ def test_path_regeneration_passes_and_sample_ranges(regen, tmp_path, monkeypatch
             torch.cuda.synchronize()
             accs.append(acc.cpu().numpy())
         assert np.array_equal(_bits(accs[0]), _bits(accs[1]))
+
+
+@pytest.mark.parametrize("cap", ["8", "48", "4096"])
+def test_path_regeneration_iteration_bound(cap, tmp_path, monkeypatch):
+    """Passes with path regeneration run many iterations (up to 64 samples per slot, Russian
+    roulette chains); a plan grown from a long first pass (its iterations + a quarter) must stay
+    within the per-pass bound the iteration counters are sized for (kPathMaxIter, lowered here
+    with RTG_PATH_ITER_CAP): capped, a pass that needs more leaves paths, the render is redone
+    host-driven and a pass past the bound falls back to the fused kernel -- the fused kernel's
+    bits whichever happens (rtg_path.hip path_run)."""
+    monkeypatch.setenv("RTG_PATH_REGEN", "1")
+    monkeypatch.setenv("RTG_PATH_ITER_CAP", cap)
+    hs = _scene(tmp_path, "pt_rr", 64)
+    ds = rtgpu.DeviceScene(hs, 0)
+    b, lb = ds.render(0, seed=29, flags=rtgpu.RTG_RENDER_FUSED)
+    for _ in range(3):
+        a, la = ds.render(0, seed=29, flags=rtgpu.RTG_RENDER_TREE)
+        assert np.array_equal(_bits(a), _bits(b)), ob.compare(a, b)
+        assert np.array_equal(la, lb)

@@ -33,6 +33,20 @@ def test_adapter_description_equals_loader(name):
     assert r.returncode == 0 and report[-1] == "IDENTICAL", "\n".join(report)
 
 
+@needs_dorkrt
+def test_dorkrt_cannot_reach_the_reference_trace_path():
+    """dorkrt links the reference's parser and object model but not its trace / shade entry
+    (integration/Makefile leaves out raytracer.o): no Raytracer symbol -- RenderPixel,
+    PerformShading, CastShadowRay, IntersectObjects -- is defined or referenced, so every pixel
+    it writes comes from rtg_render."""
+    out = subprocess.run(["nm", "-C", DORKRT], capture_output=True, text=True, check=True).stdout
+    hits = [ln for ln in out.splitlines() if "Raytracer" in ln]
+    assert not hits, hits[:5]
+    dyn = subprocess.run(["nm", "-C", "-D", "--undefined-only", DORKRT], capture_output=True, text=True,
+                         check=True).stdout
+    assert "rtg_render" in dyn
+
+
 def _stage(tmp_path, name):
     """A working directory with the scene's assets (PLY paths and inputs/ are relative to the
     CWD, parser.cpp:107-110,1404) so the outputs land in tmp_path."""
