@@ -1,6 +1,8 @@
 // C-ABI implementation (include/rtgpu.h): scene ingest, device upload, render.
 #include <hip/hip_runtime.h>
 
+#include <cfloat>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <algorithm>
@@ -85,6 +87,7 @@ struct WaveWork {
     size_t pixels = 0, tiles = 0;
     int slots = 0;
     bool col = false;                 // with the multi-sample colour buffer
+    int pay = 0;                      // one-layout payload float4s per queue entry
     void* mem = nullptr;
     void* dq = nullptr;               // deferred-leaf queue + per-pixel hit keys (ensure_defer)
     size_t dq_nq = 0;                 // its shadow-state entries
@@ -123,6 +126,7 @@ struct rtg_scene {
     DevBuf<rtg::DevSpotLight> spot_lights;
     DevBuf<rtg::DevCounters> counters;
     DevBuf<rtg::WNode> anodes;
+    DevBuf<float4> nodes64;
     DevBuf<float4> ahtris;
     DevBuf<int> face_leaf;
     DevBuf<int> guard;                // RTG_GUARD builds: index-violation bits
@@ -434,6 +438,55 @@ static bool anyhit_trees(const rtg_scene_desc* d, const std::vector<float4>& nd,
     return ahbOk;
 }
 
+// The 64-B node records of the per-lane walk walk_bvh_q (rtg_common.hpp): per node its own
+// 32-B record, then for an inner node its children's boxes quantised conservatively relative to
+// its own box -- per axis the largest lo code and the smallest hi code whose decoded bound
+// (lo + q * (hi - lo) * 2^-16 in float, exactly as the device decodes it; q = 0 / 65535 the box's
+// own bound) still contains the child's -- packed lo | hi << 16, the right child's index (skip of
+// the left child) and a validity bit per child (0: no usable code -- non-finite or tiny boxes, a
+// child outside its parent -- the child is then always fetched).
+static float qdec_lo(float lo, float s, uint32_t q) { return q == 0 ? lo : lo + (float)q * s; }
+static float qdec_hi(float lo, float hi, float s, uint32_t q) { return q == 0xFFFFu ? hi : lo + (float)q * s; }
+static bool quantise_axis(float lo, float hi, float clo, float chi, uint32_t& out) {
+    const float s = (hi - lo) * 0x1p-16f;
+    if (!std::isfinite(lo) || !std::isfinite(hi) || !std::isfinite(clo) || !std::isfinite(chi)) return false;
+    if (!(s >= FLT_MIN) || clo < lo || chi > hi || clo > chi) return false;
+    double ql = std::floor(((double)clo - lo) / s), qh = std::ceil(((double)chi - lo) / s);
+    uint32_t a = (uint32_t)std::min(65535.0, std::max(0.0, ql)), b = (uint32_t)std::min(65535.0, std::max(0.0, qh));
+    while (a > 0 && qdec_lo(lo, s, a) > clo) --a;
+    while (b < 0xFFFFu && qdec_hi(lo, hi, s, b) < chi) ++b;
+    if (qdec_lo(lo, s, a) > clo || qdec_hi(lo, hi, s, b) < chi) return false;
+    out = a | (b << 16);
+    return true;
+}
+static std::vector<float4> child_records(const std::vector<float4>& nd) {
+    const size_t nn = nd.size() / 2;
+    std::vector<float4> out(4 * nn, make_float4(0.f, 0.f, 0.f, 0.f));
+    auto iv = [](float f) { int v; std::memcpy(&v, &f, 4); return v; };
+    auto fv = [](uint32_t v) { float f; std::memcpy(&f, &v, 4); return f; };
+    for (size_t i = 0; i < nn; ++i) {
+        const float4 a = nd[2 * i], b = nd[2 * i + 1];
+        out[4 * i] = a;
+        out[4 * i + 1] = b;
+        if (iv(b.w) >= 0 || i + 1 >= nn) continue;        // a leaf (or the pad node)
+        const int L = (int)i + 1, R = iv(nd[2 * L + 1].z);
+        if (R <= L || (size_t)R >= nn) continue;
+        const float lo[3] = {a.x, a.y, a.z}, hi[3] = {a.w, b.x, b.y};
+        uint32_t code[2][3] = {};
+        bool ok[2] = {true, true};
+        const int child[2] = {L, R};
+        for (int k = 0; k < 2; ++k) {
+            const float4 ca = nd[2 * child[k]], cb = nd[2 * child[k] + 1];
+            const float clo[3] = {ca.x, ca.y, ca.z}, chi[3] = {ca.w, cb.x, cb.y};
+            for (int ax = 0; ax < 3; ++ax) ok[k] = ok[k] && quantise_axis(lo[ax], hi[ax], clo[ax], chi[ax], code[k][ax]);
+        }
+        out[4 * i + 2] = make_float4(fv(code[0][0]), fv(code[0][1]), fv(code[0][2]), fv((uint32_t)R));
+        out[4 * i + 3] = make_float4(fv(code[1][0]), fv(code[1][1]), fv(code[1][2]),
+                                     fv((ok[0] ? 1u : 0u) | (ok[0] && ok[1] ? 2u : 0u)));
+    }
+    return out;
+}
+
 int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     if (!d || !out) return set_err(RTG_ERR_INVALID, "null argument");
     *out = nullptr;
@@ -574,6 +627,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     std::vector<float4> ahtris;
     int ahbMode = rtg::AHB_EXACT;
     std::vector<int> faceLeaf;
+    std::vector<float4> nodes64;
     for (int i = 0; i < d->num_objects; ++i) objs[i].aroot = -1;
     if (!std::getenv("RTG_NO_FAST_SHADOW") && d->num_meshes > 0) {
         std::vector<float4> dn;
@@ -596,6 +650,9 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
                 if (l == rtg::LEAF_EXT) { first = nx[p].x; cnt = nx[p].y; }
                 for (int f = first; f < first + cnt; ++f) faceLeaf[f] = p;
             }
+        // the per-lane walk's records with quantised child boxes (walk_bvh_q; RTG_QNODES=0: none)
+        const char* qn = std::getenv("RTG_QNODES");
+        if (!qn || std::strcmp(qn, "0") != 0) nodes64 = child_records(nd);
 
         // any-hit tree per mesh (anyhit_trees, rtg_ahb.cpp)
         std::vector<float4> ht;
@@ -800,6 +857,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     HIP_TRY(sc->anodes.upload(anodes));
     HIP_TRY(sc->ahtris.upload(ahtris));
     HIP_TRY(sc->face_leaf.upload(faceLeaf));
+    HIP_TRY(sc->nodes64.upload(nodes64));
     std::vector<rtg::DevCounters> zero(1);
     std::memset(zero.data(), 0, sizeof(rtg::DevCounters));
     HIP_TRY(sc->counters.upload(zero));
@@ -842,6 +900,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     HIP_TRY(hipMemset(sc->guard.p, 0, sizeof(int)));
     S.guard = sc->guard.p;
     S.face_leaf = faceLeaf.empty() ? nullptr : sc->face_leaf.p;
+    S.nodes64 = nodes64.empty() ? nullptr : sc->nodes64.p;
     HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&sc->done, hipEventDisableTiming));
     HIP_TRY(hipDeviceSynchronize());
@@ -1017,22 +1076,36 @@ static int prepare(rtg_scene* s, const rtg_render_opts* o, rtg::DevCamera& C, rt
     return RTG_OK;
 }
 
+// The wavefront pipeline's one-shadow-light layout (rtg_wave.hpp SH_ONE): payload float4s per
+// queued shadow ray -- 2 with at most one light, 3 with one point / area light followed by one
+// environment light (its term travels with the shadow ray: C4), 0 otherwise (general layout)
+static int one_payload(const rtg_scene* s) {
+    const rtg::DevScene& S = s->ds;
+    if (s->num_slots <= 1) return 2;
+    if (s->num_slots == 2 && S.num_env == 1 && S.num_point + S.num_area == 1 && S.num_dir + S.num_spot + S.num_mesh == 0)
+        return 3;
+    return 0;
+}
+
 // Sizes the wavefront buffers for `pixels` pixel entries x `slots` light slots and `tiles`
-// shade blocks (queue segments of 256 * slots entries), one allocation; `col`: with the colour
-// buffer of multi-sample passes (one float4 per entry).
-static int ensure_wave(WaveWork& ww, size_t pixels, int slots, size_t tiles, bool col = false) {
-    if (ww.mem && ww.pixels >= pixels && ww.slots >= slots && ww.tiles >= tiles && (ww.col || !col)) return RTG_OK;
+// shade blocks (queue segments of 256 * slots entries), one allocation; `pay`: one-layout
+// payload float4s per queue entry (one_payload); `col`: with the colour buffer of multi-sample
+// passes (one float4 per entry).
+static int ensure_wave(WaveWork& ww, size_t pixels, int slots, size_t tiles, int pay, bool col = false) {
+    if (ww.mem && ww.pixels >= pixels && ww.slots >= slots && ww.tiles >= tiles && ww.pay >= pay && (ww.col || !col))
+        return RTG_OK;
     if (ww.dq) { (void)hipFree(ww.dq); ww.dq = nullptr; }
     if (ww.mem) { (void)hipFree(ww.mem); ww.mem = nullptr; }
     pixels = std::max(pixels, ww.pixels);
     tiles = std::max(tiles, ww.tiles);
     col = col || ww.col;
+    pay = std::max(pay, ww.pay);
     const size_t ns = pixels * (size_t)std::max(slots, 1);
     const size_t nq = tiles * 256 * (size_t)std::max(slots, 1);
     auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
     size_t off[13], total = 0;
     const size_t sz[13] = {pixels * 4, pixels * 4, pixels * 4, pixels * 16, ns * 16, ns, nq * 16, nq * 16, nq * 4,
-                           tiles * 4, pixels * 16, slots <= 1 ? nq * 32 : 0, col ? pixels * 16 : 0};
+                           tiles * 4, pixels * 16, (size_t)tiles * 256 * 16 * pay, col ? pixels * 16 : 0};
     for (int k = 0; k < 13; ++k) { off[k] = total; total += al(sz[k]); }
     HIP_TRY(hipMalloc(&ww.mem, total));
     char* b = (char*)ww.mem;
@@ -1041,7 +1114,9 @@ static int ensure_wave(WaveWork& ww, size_t pixels, int slots, size_t tiles, boo
     W.base = (float4*)(b + off[3]); W.term = (float4*)(b + off[4]); W.occ = (unsigned char*)(b + off[5]);
     W.q_o = (float4*)(b + off[6]); W.q_d = (float4*)(b + off[7]); W.q_slot = (int*)(b + off[8]);
     W.q_count = (int*)(b + off[9]); W.accum = (float4*)(b + off[10]);
-    W.q_pay = slots <= 1 ? (float4*)(b + off[11]) : nullptr;
+    W.q_pay = pay ? (float4*)(b + off[11]) : nullptr;
+    W.pay3 = pay == 3;
+    ww.pay = pay;
     W.col = col ? (float4*)(b + off[12]) : nullptr;
     ww.col = col;
     ww.pixels = pixels;
@@ -1145,7 +1220,7 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
     if (pipe == PIPE_PATH) {
         float4* acc = (float4*)d_accum;
         if (!P.accum_only && C.spp > 1) {   // internal accumulator indexed by absolute pixel
-            int rc = ensure_wave(ww, (size_t)C.width * C.height, s->num_slots, (size_t)P.num_tiles);
+            int rc = ensure_wave(ww, (size_t)C.width * C.height, s->num_slots, (size_t)P.num_tiles, 0);
             if (rc) return rc;
             acc = ww.W.accum;
         }
@@ -1173,7 +1248,7 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
     if (pipe == PIPE_TREE) {
         float4* acc = (float4*)d_accum;
         if (!P.accum_only && C.spp > 1) {   // internal accumulator indexed by absolute pixel
-            int rc = ensure_wave(ww, (size_t)C.width * C.height, s->num_slots, (size_t)P.num_tiles);
+            int rc = ensure_wave(ww, (size_t)C.width * C.height, s->num_slots, (size_t)P.num_tiles, 0);
             if (rc) return rc;
             acc = ww.W.accum;
         }
@@ -1186,7 +1261,7 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
         // work-buffer entries and shade blocks of a pass (all its sample slabs)
         const size_t entries = P.slabs > 1 ? (size_t)P.slabs * P.slab_px : (size_t)P.part_rows * C.width;
         const size_t blocks = (size_t)P.slab_tiles * P.slabs;
-        int rc = ensure_wave(ww, entries, s->num_slots, blocks, P.slabs > 1);
+        int rc = ensure_wave(ww, entries, s->num_slots, blocks, one_payload(s), P.slabs > 1);
         if (rc) return rc;
 
         rtg::WaveBufs W = ww.W;
@@ -1195,7 +1270,7 @@ static int launch(rtg_scene* s, const rtg_render_opts* o, const rtg::DevCamera& 
         else if (C.spp > 1) {   // internal accumulator indexed by absolute pixel
             size_t need = (size_t)C.width * C.height;
             if (need > ww.pixels) {
-                int rc2 = ensure_wave(ww, need, s->num_slots, blocks, P.slabs > 1);
+                int rc2 = ensure_wave(ww, need, s->num_slots, blocks, one_payload(s), P.slabs > 1);
                 if (rc2) return rc2;
                 W = ww.W;
                 W.num_slots = s->num_slots;

@@ -596,6 +596,111 @@ DEV bool walk_bvh_seq(const DevScene& S, int i, const int end, const Ray& r, flo
     return hit;
 }
 
+// Conservative slab test: accepts every box the exact test (box_hit) accepts at minT.  The
+// fast slab distances (m - o) * rcp(d) are within 2^-22 |t| of the exact quotients (RayRcp,
+// q.fast), so exact tmax > 0, tmax >= tmin, tmin < minT imply the tests below on the fast
+// values (minTc = minT (1 + 2^-21); the 1e-30 terms cover subnormal products).  (An fma form
+// m * rcp - o * rcp saves six instructions but its error scales with |o * rcp|, which loosens
+// the test badly for rays with a small direction component: measured 2x slower.)
+
+struct SlabRay {
+    f3 o;
+    float ix, iy, iz;
+};
+DEV SlabRay slab_ray(const Ray& r, const RayRcp& q) {
+    SlabRay s;
+    s.o = r.o;
+    s.ix = q.ix; s.iy = q.iy; s.iz = q.iz;
+    return s;
+}
+DEV bool slab_cons(float lx, float ly, float lz, float hx, float hy, float hz, const SlabRay& s, float minTc,
+                   float& tnear) {
+    const float tx1 = (lx - s.o.x) * s.ix, tx2 = (hx - s.o.x) * s.ix;
+    const float ty1 = (ly - s.o.y) * s.iy, ty2 = (hy - s.o.y) * s.iy;
+    const float tz1 = (lz - s.o.z) * s.iz, tz2 = (hz - s.o.z) * s.iz;
+    const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
+    const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
+    tnear = tmin;
+    return (tmax > -1e-30f) & (tmax >= fmaf(tmin, 1.0f - 0x1p-21f, -1e-30f)) & (tmin < minTc);
+}
+
+// The same walk on the 64-B records of S.nodes64 (the ray trees' closest hits, C5): each record
+// is the node's own 32-B record followed by its children's boxes, quantised conservatively
+// relative to its own box (rtg_api.cpp child_records: per axis two 16-bit bounds,
+// lo + q * ext * 2^-16 rounded down / up, q = 0 / 65535 the box's own bound), the right child's
+// index and two validity bits.  The reference tests the left child right after its parent, and
+// the right child right after a failing left child, at the same minT -- so at a passing inner
+// node a child whose quantised box fails the conservative slab test (slab_cons: never stricter
+// than the exact test, and the slab test is monotone in the box) is decided there, without
+// fetching its record: the reference's decision and its count, not its dependent fetch.  A right
+// child reached after its left sibling's subtree is tested on its own record as before.
+DEV float q_lo(float lo, float s, uint32_t q) { return q == 0 ? lo : lo + (float)q * s; }
+DEV float q_hi(float lo, float hi, float s, uint32_t q) { return q == 0xFFFFu ? hi : lo + (float)q * s; }
+DEV bool q_box_cons(float4 a, float4 b, int qx, int qy, int qz, const SlabRay& sr, float minTc) {
+    const float sx = (a.w - a.x) * 0x1p-16f, sy = (b.x - a.y) * 0x1p-16f, sz = (b.y - a.z) * 0x1p-16f;
+    const uint32_t ux = (uint32_t)qx, uy = (uint32_t)qy, uz = (uint32_t)qz;
+    float tn;
+    return slab_cons(q_lo(a.x, sx, ux & 0xFFFFu), q_lo(a.y, sy, uy & 0xFFFFu), q_lo(a.z, sz, uz & 0xFFFFu),
+                     q_hi(a.x, a.w, sx, ux >> 16), q_hi(a.y, b.x, sy, uy >> 16), q_hi(a.z, b.y, sz, uz >> 16), sr,
+                     minTc, tn);
+}
+template <bool ANY, bool STATS>
+DEV bool walk_bvh_q(const DevScene& S, int i, const int end, const Ray& r, float& minT, int& hitFace, float limit,
+                    Cnt<STATS>& c) {
+    bool hit = false;
+    const RayRcp q = ray_rcp(r);
+    const SlabRay sr = slab_ray(r, q);
+    while (i < end) {
+        const float4* R = S.nodes64 + 4 * (size_t)i;
+        const float4 a = R[0];
+        const float4 b = R[1];
+        c.template node<ANY>();
+        const int skip = __float_as_int(b.z);
+        if (!box_hit_fast<true>(a.x, a.y, a.z, a.w, b.x, b.y, r, q, minT)) {
+            i = skip;
+            continue;
+        }
+        const int leaf = __float_as_int(b.w);
+        if (leaf >= 0) {
+            int first = leaf >> 8, cnt = leaf & 255;
+            if (leaf == LEAF_EXT) {
+                const int2 e = S.node_ext[i];
+                first = e.x;
+                cnt = e.y;
+            }
+            for (int f = first; f < first + cnt; ++f) {
+                c.template tri<ANY>();
+                float t;
+                if (tri_test_sel(S.tris + 3 * f, r, minT, t)) {
+                    minT = t;
+                    hitFace = f;
+                    hit = true;
+                    if (ANY && t < limit) return true;
+                }
+            }
+            i = skip;
+            continue;
+        }
+        const int4 cl = reinterpret_cast<const int4*>(R)[2];      // left box, right child's index
+        const int4 cr = reinterpret_cast<const int4*>(R)[3];      // right box, validity bits
+        if (q.fast && (cr.w & 1)) {
+            const float minTc = minT * (1.0f + 0x1p-21f);
+            if (!q_box_cons(a, b, cl.x, cl.y, cl.z, sr, minTc)) {
+                c.template node<ANY>();                           // the left child's test: it fails
+                if ((cr.w & 2) && !q_box_cons(a, b, cr.x, cr.y, cr.z, sr, minTc)) {
+                    c.template node<ANY>();                       // the right child's: it fails too
+                    i = skip;
+                } else {
+                    i = cl.w;
+                }
+                continue;
+            }
+        }
+        i = i + 1;
+    }
+    return hit;
+}
+
 // One step's large leaves, tested by the whole wave at once.  Every lane that reached a
 // large leaf in this step (`coop`) posts an event -- its ray, minT and leaf -- to the wave's
 // table in LDS; the (event, face) pairs of all events are dealt over the wave's lanes, and
@@ -1028,7 +1133,9 @@ struct Hit {
 // bbox test fails leaves its offset on the ray origin (instancedMesh.cpp:18-60).
 // FEAT (scene features the caller guarantees absent when the bit is clear) lets the
 // traversal kernels drop whole code paths -- and their registers -- for plain scenes.
-template <bool ANY, bool STATS, int FEAT = FEAT_ALL, bool PK = false, bool DEFER = false>
+// QN: the per-lane walk on S.nodes64 (walk_bvh_q; the caller checks S.nodes64, scenes without
+// large leaves)
+template <bool ANY, bool STATS, int FEAT = FEAT_ALL, bool PK = false, bool DEFER = false, bool QN = false>
 DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit, Hit& h, Cnt<STATS>& c,
                DeferCtx* dc = nullptr) {
     h.t = minT;
@@ -1090,6 +1197,8 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
         if constexpr (PK)
             found = walk_bvh_packet<ANY, STATS, RTG_PRIMARY_PACKET == 2, DEFER>(S, ob.node_begin, ob.node_end, lr, t,
                                                                                   face, limit, c, dc, k);
+        else if constexpr (QN && !(FEAT & FEAT_BIGLEAF))
+            found = walk_bvh_q<ANY, STATS>(S, ob.node_begin, ob.node_end, lr, t, face, limit, c);
         else found = walk_bvh<ANY, STATS, (FEAT & FEAT_BIGLEAF) != 0>(S, ob.node_begin, ob.node_end, lr, t, face, limit, c);
         if (found) {
             h.t = t; h.obj = k; h.face = face; h.o = r.o;
@@ -1136,33 +1245,6 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
 #endif
 #define RTG_WIDE_WAVES(FEAT) (((FEAT) & FEAT_INSTANCE) ? RTG_INST_ANY_WAVES : RTG_WIDE_WAVES_PLAIN)
 
-
-// Conservative slab test: accepts every box the exact test (box_hit) accepts at minT.  The
-// fast slab distances (m - o) * rcp(d) are within 2^-22 |t| of the exact quotients (RayRcp,
-// q.fast), so exact tmax > 0, tmax >= tmin, tmin < minT imply the tests below on the fast
-// values (minTc = minT (1 + 2^-21); the 1e-30 terms cover subnormal products).  (An fma form
-// m * rcp - o * rcp saves six instructions but its error scales with |o * rcp|, which loosens
-// the test badly for rays with a small direction component: measured 2x slower.)
-struct SlabRay {
-    f3 o;
-    float ix, iy, iz;
-};
-DEV SlabRay slab_ray(const Ray& r, const RayRcp& q) {
-    SlabRay s;
-    s.o = r.o;
-    s.ix = q.ix; s.iy = q.iy; s.iz = q.iz;
-    return s;
-}
-DEV bool slab_cons(float lx, float ly, float lz, float hx, float hy, float hz, const SlabRay& s, float minTc,
-                   float& tnear) {
-    const float tx1 = (lx - s.o.x) * s.ix, tx2 = (hx - s.o.x) * s.ix;
-    const float ty1 = (ly - s.o.y) * s.iy, ty2 = (hy - s.o.y) * s.iy;
-    const float tz1 = (lz - s.o.z) * s.iz, tz2 = (hz - s.o.z) * s.iz;
-    const float tmin = fmaxf(fmaxf(fminf(tx1, tx2), fminf(ty1, ty2)), fminf(tz1, tz2));
-    const float tmax = fminf(fminf(fmaxf(tx1, tx2), fmaxf(ty1, ty2)), fmaxf(tz1, tz2));
-    tnear = tmin;
-    return (tmax > -1e-30f) & (tmax >= fmaf(tmin, 1.0f - 0x1p-21f, -1e-30f)) & (tmin < minTc);
-}
 
 // DEFER (large-leaf scenes, the packet walk): a leaf slot of more than RTG_DEFER_ANY_LEAF entries
 // that at most RTG_DEFER_ANY_LANES lanes reach is queued for those lanes (k_bigleaf_any) instead

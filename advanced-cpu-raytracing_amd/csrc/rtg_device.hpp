@@ -163,6 +163,7 @@ struct DevScene {
     const WNode* __restrict__ anodes;  // any-hit tree (null: shadow rays take the reference walk)
     const float4* __restrict__ ahtris; // its leaf entries: face record, reference leaf node in [0].w
     const int* __restrict__ face_leaf; // per face: its leaf node
+    const float4* __restrict__ nodes64; // per node 64 B: its record + quantised child boxes (walk_bvh_q); null: none
     int exact_shadow;                  // RTG_RENDER_EXACT_SHADOW: shadow rays take the reference walk
     int ahb_split;                     // the any-hit tree splits large leaves (AHB_SPLIT)
     int ordered;                       // RTG_RENDER_ORDERED (plain mesh scenes with an any-hit tree)
@@ -224,6 +225,7 @@ struct WaveBufs {
     // one-slot scenes (at most one light): per queue entry the pixel's base colour + flags
     // and its light term + pixel index, so k_shadow finishes the pixel itself (no k_resolve)
     float4* __restrict__ q_pay;
+    int pay3;                           // ... and a third: the environment light's term (one_layout_env)
     int num_slots;                      // lights per pixel
     // large-leaf scenes (FEAT_BIGLEAF), production renders: the camera walk defers each large
     // leaf it reaches to a queue of (ray, leaf, minT at entry) entries, 3 float4 each, tested by

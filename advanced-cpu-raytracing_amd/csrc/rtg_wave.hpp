@@ -332,6 +332,19 @@ DEV f3 resolve_one(f3 base, int flags, bool has_term, f3 term, bool occluded) {
     return color;
 }
 
+// The same with a second, unshadowed term after it (one shadow-casting point / area light
+// followed by an environment light, which casts no shadow ray, raytracer.cpp:741-755): k_resolve's
+// loop over the two slots -- (0 + term if unoccluded) + env term.
+DEV f3 resolve_two(f3 base, int flags, bool has_term, f3 term, bool occluded, bool has_term2, f3 term2) {
+    if (flags & BASE_FINAL) return base;
+    f3 sum = mk(0, 0, 0);
+    if (has_term && !occluded) sum = add(sum, term);
+    if (has_term2) sum = add(sum, term2);
+    f3 color = add(base, sum);
+    if (flags & BASE_ADD_ZERO) color = add(color, mk(0, 0, 0));   // depth-0 mirror/dielectric/conductor
+    return color;
+}
+
 // PerformShading's sum with the unoccluded light terms already summed in light order.
 DEV f3 resolve_sum(f3 base, int flags, f3 sum) {
     if (flags & BASE_FINAL) return base;
@@ -343,9 +356,10 @@ DEV f3 resolve_sum(f3 base, int flags, f3 sum) {
 // SK: shading variant (rtg_common.hpp SK_*).  MODE:
 //   SH_GENERAL  every light slot's term and occlusion flag to the per-pixel buffers, shadow
 //               rays to the block's queue segment (k_shadow, k_resolve follow);
-//   SH_ONE      at most one light: the pixel is finished here when it casts no shadow ray,
-//               else its base colour and light term travel with the shadow ray in the queue
-//               (q_pay) and k_shadow_one finishes it;
+//   SH_ONE      at most one light with a shadow ray, and at most one environment light after
+//               it (W.pay3; C4's point + environment light): the pixel is finished here when
+//               it casts no shadow ray, else its base colour and light term(s) travel with
+//               the shadow ray in the queue (q_pay) and k_shadow_one finishes it;
 //   SH_FUSED    at most one light, plain shading (SK 0): the lane casts its own shadow ray
 //               (any-hit walk of FEAT, FAST) and finishes its pixel -- no queue.  Almost
 //               every pixel of a scene that fills the frame casts one, and the ones that do
@@ -371,7 +385,7 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
     int px, py, crow, slab;
     tile_pixel(P, px, py, crow, slab);
     const int sample = sample0 + slab;
-    const size_t seg = (size_t)blockIdx.x * 256 * W.num_slots;
+    const size_t seg = (size_t)blockIdx.x * 256 * (ONE ? 1 : W.num_slots);   // (ONE: one shadow ray per pixel)
     Cnt<STATS> cn;
     const bool valid = px < C.width && py < P.row_end;
     const int pixel = valid ? px + py * C.width : 0;
@@ -398,6 +412,8 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
     int bflags = 0;
     f3 term1 = mk(0, 0, 0);
     bool has_term = false, pushed = false;
+    f3 term2 = mk(0, 0, 0);          // SH_ONE: the environment light's term after the shadowed one
+    bool has_term2 = false;
     float4 ro = make_float4(0.f, 0.f, 0.f, 0.f), rd = ro;      // SH_FUSED: the shadow ray
     auto put_base = [&](f3 col, int flags) {
         if (ONE) { base = col; bflags = flags; }
@@ -509,7 +525,8 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
                 qd = make_float4(d.x, d.y, d.z, lightT);
             }
         }
-        if constexpr (MODE == SH_FUSED) {
+        if constexpr (ONE) {
+            // (SH_ONE: queued after the light loops, with every term of the pixel)
             if (want) { ro = qo; rd = qd; pushed = true; }
             return;
         }
@@ -518,19 +535,20 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
             const size_t q = seg + qi;
             W.q_o[q] = qo;
             W.q_d[q] = qd;
-            if (ONE) {
-                W.q_pay[2 * q] = make_float4(base.x, base.y, base.z, __int_as_float(bflags));
-                W.q_pay[2 * q + 1] = make_float4(term1.x, term1.y, term1.z, __int_as_float(pixel));
-                pushed = true;
-            } else {
-                W.q_slot[q] = slot;
-                W.occ[slot] = 0;
-            }
+            W.q_slot[q] = slot;
+            W.occ[slot] = 0;
         }
     };
     auto put = [&](f3 t) {
-        if (ONE) { term1 = t; has_term = true; }
-        else W.term[slot] = make_float4(t.x, t.y, t.z, 0.f);
+        if constexpr (MODE == SH_ONE) {
+            if (has_term) { term2 = t; has_term2 = true; }   // the environment light after the shadowed one
+            else { term1 = t; has_term = true; }
+        } else if constexpr (ONE) {
+            term1 = t;
+            has_term = true;
+        } else {
+            W.term[slot] = make_float4(t.x, t.y, t.z, 0.f);
+        }
     };
     auto point_light = [&](int l) {
         const f3 lp = ld3(S.point_lights[l].pos);
@@ -628,15 +646,47 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
             finish_pixel(C, P, sample, O, pixel, slab, resolve_one(base, bflags, has_term, term1, false));
         }
     }
-    if (MODE == SH_ONE && valid && !pushed) finish_pixel(C, P, sample, O, pixel, slab, resolve_one(base, bflags, has_term, term1, false));
+    if constexpr (MODE == SH_ONE) {
+        // the shadow ray with the pixel's base colour and terms, or the pixel finished here
+        const int qi = queue_append(pushed, &seg_count);
+        if (pushed) {
+            const size_t q = seg + qi;
+            W.q_o[q] = ro;
+            W.q_d[q] = rd;
+            const size_t pq = (W.pay3 ? 3 : 2) * q;
+            W.q_pay[pq] = make_float4(base.x, base.y, base.z, __int_as_float(bflags));
+            W.q_pay[pq + 1] = make_float4(term1.x, term1.y, term1.z, __int_as_float(pixel));
+            if (W.pay3) W.q_pay[pq + 2] = make_float4(term2.x, term2.y, term2.z, __int_as_float(has_term2 ? 1 : 0));
+        } else if (valid) {
+            finish_pixel(C, P, sample, O, pixel, slab, resolve_two(base, bflags, has_term, term1, false, has_term2, term2));
+        }
+    }
     }
     __syncthreads();
     if (threadIdx.x == 0) W.q_count[blockIdx.x] = seg_count;
     flush_counters<STATS>(cn, counters);
 }
 
-// One-light scenes: CastShadowRay for a queued pixel, then its PerformShading sum and the end
-// of the sample pass (what k_resolve does for the general case).
+// The end of a queued pixel of the one-shadow-light layout: its PerformShading sum from the
+// payload k_shade queued with the shadow ray (base colour, the shadowed light's term, W.pay3:
+// the environment light's term after it) and the shadow ray's answer.
+DEV void finish_one(const DevCamera& C, const RenderParams& P, int sample, const PassOut& O, const WaveBufs& W,
+                    size_t q, int slab, bool occluded) {
+    const size_t pq = (W.pay3 ? 3 : 2) * q;
+    const float4 b = W.q_pay[pq], t = W.q_pay[pq + 1];
+    f3 color;
+    if (W.pay3) {
+        const float4 t2 = W.q_pay[pq + 2];
+        color = resolve_two(mk(b.x, b.y, b.z), __float_as_int(b.w), true, mk(t.x, t.y, t.z), occluded,
+                            __float_as_int(t2.w) != 0, mk(t2.x, t2.y, t2.z));
+    } else {
+        color = resolve_one(mk(b.x, b.y, b.z), __float_as_int(b.w), true, mk(t.x, t.y, t.z), occluded);
+    }
+    finish_pixel(C, P, sample, O, __float_as_int(t.w), slab, color);
+}
+
+// One-shadow-light scenes: CastShadowRay for a queued pixel, then its PerformShading sum and the
+// end of the sample pass (what k_resolve does for the general case).
 template <bool STATS, int FEAT, bool FAST, bool DEFER = false>
 __global__ __launch_bounds__(256, FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(FEAT)) void k_shadow_one(
     const DevScene S, const DevCamera C, const RenderParams P, const int sample0, const WaveBufs W, const PassOut O,
@@ -659,9 +709,7 @@ __global__ __launch_bounds__(256, FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(
         } else {
             occluded = shadow_occluded<STATS, FEAT, FAST>(S, W, q, W.q_o[q], W.q_d[q], cn);
         }
-        const float4 b = W.q_pay[2 * q], t = W.q_pay[2 * q + 1];
-        const f3 color = resolve_one(mk(b.x, b.y, b.z), __float_as_int(b.w), true, mk(t.x, t.y, t.z), occluded);
-        finish_pixel(C, P, sample0 + slab, O, __float_as_int(t.w), slab, color);
+        finish_one(C, P, sample0 + slab, O, W, q, slab, occluded);
     }
     flush_counters<STATS>(cn, counters);
 }
@@ -687,9 +735,7 @@ __global__ __launch_bounds__(256) void k_shadow_fin_one(const DevScene S, const 
         Hit h;
         occluded = trace<true, false, FEAT>(S, r, 0.f, o.w, d.w, h, cn);
     }
-    const float4 b = W.q_pay[2 * q], t = W.q_pay[2 * q + 1];
-    const f3 color = resolve_one(mk(b.x, b.y, b.z), __float_as_int(b.w), true, mk(t.x, t.y, t.z), occluded);
-    finish_pixel(C, P, sample0 + slab, O, __float_as_int(t.w), slab, color);
+    finish_one(C, P, sample0 + slab, O, W, q, slab, occluded);
 }
 
 // The same for the general layout: the answer goes to the light slot's occlusion byte.
@@ -737,9 +783,10 @@ template <bool STATS, int FEAT>
 hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderParams& P, const WaveBufs& W, float* hdr,
                          unsigned char* l, DevCounters* cnt, int sk, hipStream_t st, hipEvent_t* ev, int* layout) {
     const int nshadow = S.num_point + S.num_area + S.num_dir + S.num_spot + S.num_mesh;
-    // at most one light: k_shade / k_shadow_one finish the pixels (no k_resolve); shading
-    // variants for this case only (every other scene takes the general k_shade)
-    const bool one = W.num_slots <= 1 && W.q_pay != nullptr;
+    // at most one light with a shadow ray (and at most one environment light after it):
+    // k_shade / k_shadow_one finish the pixels (no k_resolve); shading variants for this case
+    // only (every other scene takes the general k_shade)
+    const bool one = W.q_pay != nullptr && (W.num_slots <= 1 || W.pay3);
     const int scene_sk = sk;
     if (!one) sk = SK_ALL;
     // the any-hit packet walk unless RTG_RENDER_EXACT_SHADOW asks for the reference walk
