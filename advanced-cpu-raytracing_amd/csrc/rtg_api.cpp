@@ -96,7 +96,7 @@ struct WaveWork {
 };
 constexpr int kWorkCtx = 1;
 struct TileMap {
-    int tx, ty, mode;
+    int tx, ty;
     DevBuf<int> map;
 };
 
@@ -146,7 +146,7 @@ struct rtg_scene {
     float* d_hdr = nullptr;
     unsigned char* d_ldr = nullptr;
     size_t d_pixels = 0;
-    // block -> tile tables, one per (tiles_x, tiles_y, mode) met (never re-uploaded: kernels of
+    // block -> tile tables, one per (tiles_x, tiles_y) met (never re-uploaded: kernels of
     // several streams may be reading them)
     std::vector<std::unique_ptr<TileMap>> tile_maps;
     // RTG_RENDER_TIMING events (stage k runs between ev[k] and ev[k+1])
@@ -719,7 +719,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     sc->num_slots = d->num_point_lights + d->num_area_lights + d->num_env_lights + d->num_dir_lights +
                     d->num_spot_lights + d->num_mesh_lights;
     // shading features: textures / maps (incl. a background texture), BRDFs, env / spot / mesh
-    // lights; RTG_SK_FORCE=<bits> ORs bits in (experiments: the general variant, same values)
+    // lights
     {
         int sk = 0;
         for (int i = 0; i < d->num_objects; ++i)
@@ -730,7 +730,6 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
         for (int i = 0; i < d->num_materials; ++i)
             if (d->materials[i].brdf >= 0) sk |= rtg::SK_BRDF;
         if (d->num_env_lights + d->num_spot_lights + d->num_mesh_lights > 0) sk |= rtg::SK_XLIGHT;
-        if (const char* e = std::getenv("RTG_SK_FORCE")) sk |= std::atoi(e) & rtg::SK_ALL;
         sc->shade_sk = sk;
     }
     // mesh lights (meshLight.h): their faces in MeshLight::faces order (the BVH-permuted one)
@@ -963,39 +962,23 @@ int rtg_part_runs(int32_t row_begin, int32_t row_end, int32_t part, int32_t part
 }
 
 // Block -> tile assignment.  The hardware deals workgroups to the 8 XCDs round-robin
-// (block b runs on XCD b % 8), and each XCD has its own L2.  Mode 2 (default) gives each
-// XCD whole 64x64-pixel super-tiles (4x4 tiles), dealt round-robin over the image, so an
-// XCD's blocks share BVH nodes in its L2 while every XCD sees a spread of the image
-// (traversal cost varies strongly with image position; contiguous bands would leave
-// XCDs idle).  Mode 1: one contiguous band per XCD.  Mode 0: row-major tiles.
-// RTG_TILE_MAP=<mode> overrides (experiments).
-static int tile_map_mode() {
-    static int mode = [] {
-        const char* e = std::getenv("RTG_TILE_MAP");
-        return e ? std::atoi(e) : 2;
-    }();
-    return mode;
-}
-
-static std::vector<int> build_tile_map(int tx, int ty, int mode) {
+// (block b runs on XCD b % 8), and each XCD has its own L2: each XCD gets whole 64x64-pixel
+// super-tiles (4x4 tiles), dealt round-robin over the image, so an XCD's blocks share BVH nodes
+// in its L2 while every XCD sees a spread of the image (traversal cost varies strongly with
+// image position: one contiguous band per XCD left XCDs idle, 3.1 -> 5.3 Grays/s on the headline
+// when this was fixed; super-tiles of 32 / 128 / 256 px and row-major tiles measured no better,
+// DESIGN.md §4).
+static std::vector<int> build_tile_map(int tx, int ty) {
     const int n = tx * ty;
     std::vector<int> order(n);
     for (int t = 0; t < n; ++t) order[t] = t;
-    if (mode == 2) {
-        // super-tile side in tiles (RTG_TILE_SUPER overrides, experiments)
-        static const int kSuper = [] {
-            const char* e = std::getenv("RTG_TILE_SUPER");
-            return e ? std::max(1, std::atoi(e)) : 4;
-        }();
-        const int S = kSuper, stx = (tx + S - 1) / S;
-        auto key = [&](int t) {
-            const int x = t % tx, y = t / tx;
-            const int st = (y / S) * stx + x / S;
-            return std::make_tuple(st % 8, st / 8, (y % S) * S + x % S);
-        };
-        std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return key(a) < key(b); });
-    }
-    if (mode == 0) return order;
+    const int S = 4, stx = (tx + S - 1) / S;
+    auto key = [&](int t) {
+        const int x = t % tx, y = t / tx;
+        const int st = (y / S) * stx + x / S;
+        return std::make_tuple(st % 8, st / 8, (y % S) * S + x % S);
+    };
+    std::stable_sort(order.begin(), order.end(), [&](int a, int b) { return key(a) < key(b); });
     // block 8k + x (XCD x) takes the k-th tile of XCD x's contiguous share of `order`
     std::vector<int> map(n);
     int prefix = 0;
@@ -1008,15 +991,14 @@ static std::vector<int> build_tile_map(int tx, int ty, int mode) {
 }
 
 static int ensure_tile_map(rtg_scene* s, int tx, int ty, const int** out) {
-    const int mode = tile_map_mode();
     for (auto& m : s->tile_maps)
-        if (m->tx == tx && m->ty == ty && m->mode == mode) {
+        if (m->tx == tx && m->ty == ty) {
             *out = m->map.p;
             return RTG_OK;
         }
     HIP_TRY(hipSetDevice(s->device));
-    std::unique_ptr<TileMap> m(new TileMap{tx, ty, mode, {}});
-    HIP_TRY(m->map.upload(build_tile_map(tx, ty, mode)));
+    std::unique_ptr<TileMap> m(new TileMap{tx, ty, {}});
+    HIP_TRY(m->map.upload(build_tile_map(tx, ty)));
     *out = m->map.p;
     s->tile_maps.push_back(std::move(m));
     return RTG_OK;
@@ -1307,10 +1289,9 @@ int rtg_render_device(rtg_scene* s, const rtg_render_opts* o, float* d_hdr, uint
     HIP_TRY(hipSetDevice(s->device));
     rc = launch(s, o, C, P, d_hdr, d_ldr, d_accum, (hipStream_t)stream);
     if (rc) return rc;
-    // (RTG_NO_DONE_EVENT=1, A/B: no completion marker; rtg_scene_stats then sees only renders
-    // whose stream was synchronised)
-    static const bool no_done = std::getenv("RTG_NO_DONE_EVENT") != nullptr;
-    if (!no_done || (o->flags & RTG_RENDER_COUNT_STATS)) HIP_TRY(hipEventRecord(s->done, (hipStream_t)stream));
+    // the completion marker rtg_scene_stats waits for (round 4 measured a render without it: the
+    // same part-frame time, profiles/r04f_parts_ab.jsonl)
+    HIP_TRY(hipEventRecord(s->done, (hipStream_t)stream));
     return RTG_OK;
 }
 

@@ -770,13 +770,10 @@ void wave_resolve(const DevCamera& C, const RenderParams& P, int sample, const W
 // the end of a multi-sample pass: every pixel's slab colours into its accumulation (k_accum)
 void wave_accum(const DevCamera& C, const RenderParams& P, int sample, const WaveBufs& W, const PassOut& O,
                 hipStream_t st);
-bool no_fused_shade();
 bool frame_kernel();
 bool defer_leaves();
 bool defer_any_leaves();
-bool wide_bigleaf();
 bool defer_diag();
-int refwalk_blocks();
 
 // One traversal variant's pass sequence (instantiated in rtg_wave_a.hip / rtg_wave_b.hip).
 template <bool STATS, int FEAT>
@@ -791,15 +788,14 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
     if (!one) sk = SK_ALL;
     // the any-hit packet walk unless RTG_RENDER_EXACT_SHADOW asks for the reference walk
     // (large-leaf scenes: the split any-hit tree cuts their pole fans into small leaves; with
-    // RTG_AHB=ref / exact they keep the cooperative reference walk unless RTG_WIDE_BIGLEAF)
+    // RTG_AHB=ref / exact they keep the cooperative reference walk)
     // large-leaf scenes (production renders): the any-hit walk with their large leaves queued
     // (k_bigleaf_any; RTG_DEFER_ANY=0: the cooperative reference walk)
     const bool defer_any = !STATS && (FEAT & FEAT_BIGLEAF) && W.dq_e && W.shadow_state &&
                            S.anodes && !S.ahb_split && !S.exact_shadow && defer_any_leaves();
-    const bool fast = S.anodes != nullptr && (!(FEAT & FEAT_BIGLEAF) || S.ahb_split || wide_bigleaf() || defer_any) && !S.exact_shadow;
-    // shading fused with the shadow ray: plain shading, the fast any-hit walk (RTG_NO_FUSED_SHADE=1
-    // keeps the queue: experiments)
-    const bool fused = scene_sk == 0 && fast && !(FEAT & FEAT_BIGLEAF) && nshadow > 0 && !no_fused_shade();
+    const bool fast = S.anodes != nullptr && (!(FEAT & FEAT_BIGLEAF) || S.ahb_split || defer_any) && !S.exact_shadow;
+    // shading fused with the shadow ray: plain shading, the fast any-hit walk
+    const bool fused = scene_sk == 0 && fast && !(FEAT & FEAT_BIGLEAF) && nshadow > 0;
     *layout = fused ? (frame_kernel() && !(FEAT == 0 && S.ordered) ? LAYOUT_WAVE_FRAME : LAYOUT_WAVE_FUSED)
                     : (one ? LAYOUT_WAVE_ONE : LAYOUT_WAVE);
     const int s_end = P.sample_begin + P.sample_count;
@@ -835,7 +831,9 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
                 hipLaunchKernelGGL((k_bigleaf<FEAT>), dim3(2048), dim3(256), 0, st, S, W);
                 hipLaunchKernelGGL((k_hitfix<FEAT>), dim3(nb), dim3(256), 0, st, S, C, Pp, s, W,
                                    defer_diag() ? cnt : nullptr);
-                hipLaunchKernelGGL((k_refwalk<FEAT>), dim3(refwalk_blocks()), dim3(256), 0, st, S, C, Pp, s, W);
+                // (one unsettled pixel's reference walk per wave, grid-stride: C4 has ~2 000 per
+                // sample; 256 or 2 048 blocks per sample measured the same, profiles/r05g_c4_refwalk_ab.txt)
+                hipLaunchKernelGGL((k_refwalk<FEAT>), dim3(256 * Pp.slabs), dim3(256), 0, st, S, C, Pp, s, W);
                 deferred = true;
             }
         }

@@ -41,19 +41,6 @@ __global__ __launch_bounds__(256) void k_accum(const DevCamera C, const RenderPa
                   O.ldr);
 }
 
-// RTG_WIDE_BIGLEAF=1: shadow rays of large-leaf scenes also take the any-hit wide walk
-// (experiment; by default they take the cooperative reference walk)
-bool wide_bigleaf() { return std::getenv("RTG_WIDE_BIGLEAF") != nullptr; }
-
-// k_refwalk's grid (one unsettled pixel's reference walk per wave, grid-stride): 256 blocks,
-// 1 024 waves.  RTG_REFWALK_BLOCKS (A/B): 2 048 blocks, a wave for each of C4's ~2 000
-// pixels per pass, measured the same (C4 k_primary stage 0.895 ms either way,
-// profiles/r05g_c4_refwalk_ab.txt)
-int refwalk_blocks() {
-    const char* v = std::getenv("RTG_REFWALK_BLOCKS");
-    const int n = v ? std::atoi(v) : 256;
-    return n > 0 ? n : 256;
-}
 
 // RTG_DEFER_DIAG=1: k_hitfix counts pending / checked-out pixels of production renders into
 // extend_wide_visits / extend_fallbacks (tools/diag_defer.py); otherwise an uncounted render
@@ -87,10 +74,6 @@ bool frame_kernel() {
     return !e || std::strcmp(e, "0") != 0;
 }
 
-bool no_fused_shade() {
-    static const bool v = std::getenv("RTG_NO_FUSED_SHADE") != nullptr;
-    return v;
-}
 
 template <bool STATS>
 static hipError_t wave_shade_t(int sk, bool one, const DevScene& S, const DevCamera& C, const RenderParams& P,

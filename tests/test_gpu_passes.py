@@ -84,28 +84,27 @@ def test_sample_passes_equal_one_sample_passes(name, in_tmp, monkeypatch):
 
 @pytest.mark.parametrize("name,flags", [("c3_small", 0), ("c5_dragon", rtgpu.RTG_RENDER_TREE)])
 def test_sample_passes_accumulate_ranges(name, flags, in_tmp):
-    """RTG_RENDER_ACCUM_ONLY over sample ranges (how samples split across devices): samples
-    [0, 2) then [2, spp) into one accumulation buffer equal the spp samples in one-sample passes."""
+    """RTG_RENDER_ACCUM_ONLY over a sample range (how samples split across devices: each device
+    writes its range's weighted sum, rtg_resolve_accum adds them): ranges [0, 2) and [2, spp) in
+    multi-sample passes equal the same ranges in one-sample passes."""
     torch = pytest.importorskip("torch")
     xml, f0 = _case(name, in_tmp)
     flags |= f0
     hs = rtgpu.HostScene(xml)
     ds = rtgpu.DeviceScene(hs, 0)
     c = hs.camera(0)
-    H, W = c["height"], c["width"]
+    H, W, spp = c["height"], c["width"], c["spp"]
 
-    def acc(ranges, extra):
+    def acc(b, n, extra):
         a = torch.zeros((H, W, 4), dtype=torch.float32, device="cuda:0")
-        for b, n in ranges:
-            ds.render_device(0, 0, 0, accum_ptr=a.data_ptr(), flags=flags | extra | rtgpu.RTG_RENDER_ACCUM_ONLY,
-                             seed=8, sample_begin=b, sample_count=n)
-            torch.cuda.synchronize()
+        ds.render_device(0, 0, 0, accum_ptr=a.data_ptr(), flags=flags | extra | rtgpu.RTG_RENDER_ACCUM_ONLY,
+                         seed=8, sample_begin=b, sample_count=n)
+        torch.cuda.synchronize()
         return a.cpu().numpy()
 
-    spp = c["spp"]
-    ref = acc([(k, 1) for k in range(spp)], ONE)
-    got = acc([(0, 2), (2, spp - 2)], 0)
-    assert np.array_equal(ref.view(np.uint32), got.view(np.uint32))
+    for b, n in ((0, 2), (2, spp - 2)):
+        one, multi = acc(b, n, ONE), acc(b, n, 0)
+        assert np.array_equal(one.view(np.uint32), multi.view(np.uint32)), (b, n)
 
 
 def test_timed_samples_reports_the_last_pass(in_tmp, monkeypatch):
