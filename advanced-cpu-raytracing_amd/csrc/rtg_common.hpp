@@ -2476,7 +2476,7 @@ DEV int shadow_state_defer(const DevScene& S, const WaveBufs& W, size_t q, float
     }
     return res > 0 ? SS_OCC : 0;
 }
-template <bool STATS, int FEAT, bool FAST>
+template <bool STATS, int FEAT, bool FAST, bool QN = false>
 DEV bool shadow_occluded(const DevScene& S, const WaveBufs& W, size_t q, float4 o, float4 d, Cnt<STATS>& cn) {
     Ray r;
     r.o = mk(o.x, o.y, o.z);
@@ -2491,12 +2491,13 @@ DEV bool shadow_occluded(const DevScene& S, const WaveBufs& W, size_t q, float4 
         }
     } else {
         Hit h;
-        res = trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
+        res = trace<true, STATS, FEAT, false, false, QN>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
     }
     return res > 0;
 }
 
-template <bool STATS, int FEAT, bool FAST, bool DEFER = false>
+// QN (the ray trees' shadow rays, !FAST): the reference walk on S.nodes64 (walk_bvh_q)
+template <bool STATS, int FEAT, bool FAST, bool DEFER = false, bool QN = false>
 __global__ __launch_bounds__(256, FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(FEAT)) void k_shadow(
     const DevScene S, const WaveBufs W, DevCounters* counters) {
     const int k = blockIdx.y * 256 + threadIdx.x;
@@ -2507,7 +2508,7 @@ __global__ __launch_bounds__(256, FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(
             const int st = shadow_state_defer<STATS, FEAT>(S, W, q, W.q_o[q], W.q_d[q], cn);
             W.shadow_state[q] = st;
             if (st == SS_OCC) W.occ[W.q_slot[q]] = 1;
-        } else if (shadow_occluded<STATS, FEAT, FAST>(S, W, q, W.q_o[q], W.q_d[q], cn)) {
+        } else if (shadow_occluded<STATS, FEAT, FAST, QN>(S, W, q, W.q_o[q], W.q_d[q], cn)) {
             W.occ[W.q_slot[q]] = 1;
         }
     }

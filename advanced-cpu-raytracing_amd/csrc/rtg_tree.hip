@@ -605,7 +605,11 @@ static void level_launches(TreeState& T, const DevScene& S, const DevCamera& C, 
         W.num_slots = ns;
         W.hit_obj = L.obj;              // the hits the shadow rays leave (their origin leaf)
         W.hit_face = L.face;
-        hipLaunchKernelGGL((k_shadow<STATS, FEAT, false>), dim3(blocks, ns), dim3(256), 0, st, S, W, cnt);
+        if (S.nodes64 && !(FEAT & FEAT_BIGLEAF))
+            hipLaunchKernelGGL((k_shadow<STATS, FEAT, false, false, true>), dim3(blocks, ns), dim3(256), 0, st, S, W,
+                               cnt);
+        else
+            hipLaunchKernelGGL((k_shadow<STATS, FEAT, false>), dim3(blocks, ns), dim3(256), 0, st, S, W, cnt);
     }
     hipLaunchKernelGGL(k_tree_scan, dim3(1), dim3(1024), 0, st, T.G.c_count, blocks, T.offs, next_n, cap_next,
                        T.d_counts ? T.d_counts + kMaxLevels : nullptr);
