@@ -440,22 +440,22 @@ static bool anyhit_trees(const rtg_scene_desc* d, const std::vector<float4>& nd,
 
 // The 64-B node records of the per-lane walk walk_bvh_q (rtg_common.hpp): per node its own
 // 32-B record, then for an inner node its children's boxes quantised conservatively relative to
-// its own box -- per axis the largest lo code and the smallest hi code whose decoded bound
-// (lo + q * (hi - lo) * 2^-16 in float, exactly as the device decodes it; q = 0 / 65535 the box's
-// own bound) still contains the child's -- packed lo | hi << 16, the right child's index (skip of
+// its own box -- per axis the largest codes whose decoded bounds (lo + q * (hi - lo) * 2^-16 and
+// hi - q * (hi - lo) * 2^-16 in float, exactly as the device decodes them; q = 0: the box's own
+// bound) still contain the child's -- packed lo | hi << 16, the right child's index (skip of
 // the left child) and a validity bit per child (0: no usable code -- non-finite or tiny boxes, a
 // child outside its parent -- the child is then always fetched).
-static float qdec_lo(float lo, float s, uint32_t q) { return q == 0 ? lo : lo + (float)q * s; }
-static float qdec_hi(float lo, float hi, float s, uint32_t q) { return q == 0xFFFFu ? hi : lo + (float)q * s; }
+static float qdec_lo(float lo, float s, uint32_t q) { return lo + (float)q * s; }
+static float qdec_hi(float hi, float s, uint32_t q) { return hi - (float)q * s; }
 static bool quantise_axis(float lo, float hi, float clo, float chi, uint32_t& out) {
     const float s = (hi - lo) * 0x1p-16f;
     if (!std::isfinite(lo) || !std::isfinite(hi) || !std::isfinite(clo) || !std::isfinite(chi)) return false;
     if (!(s >= FLT_MIN) || clo < lo || chi > hi || clo > chi) return false;
-    double ql = std::floor(((double)clo - lo) / s), qh = std::ceil(((double)chi - lo) / s);
+    const double ql = std::floor(((double)clo - lo) / s), qh = std::floor(((double)hi - chi) / s);
     uint32_t a = (uint32_t)std::min(65535.0, std::max(0.0, ql)), b = (uint32_t)std::min(65535.0, std::max(0.0, qh));
     while (a > 0 && qdec_lo(lo, s, a) > clo) --a;
-    while (b < 0xFFFFu && qdec_hi(lo, hi, s, b) < chi) ++b;
-    if (qdec_lo(lo, s, a) > clo || qdec_hi(lo, hi, s, b) < chi) return false;
+    while (b > 0 && qdec_hi(hi, s, b) < chi) --b;
+    if (qdec_lo(lo, s, a) > clo || qdec_hi(hi, s, b) < chi) return false;
     out = a | (b << 16);
     return true;
 }

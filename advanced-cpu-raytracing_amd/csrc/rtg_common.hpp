@@ -634,14 +634,13 @@ DEV bool slab_cons(float lx, float ly, float lz, float hx, float hy, float hz, c
 // than the exact test, and the slab test is monotone in the box) is decided there, without
 // fetching its record: the reference's decision and its count, not its dependent fetch.  A right
 // child reached after its left sibling's subtree is tested on its own record as before.
-DEV float q_lo(float lo, float s, uint32_t q) { return q == 0 ? lo : lo + (float)q * s; }
-DEV float q_hi(float lo, float hi, float s, uint32_t q) { return q == 0xFFFFu ? hi : lo + (float)q * s; }
+// (lo codes count up from the node's lo, hi codes down from its hi: code 0 is the bound itself)
 DEV bool q_box_cons(float4 a, float4 b, int qx, int qy, int qz, const SlabRay& sr, float minTc) {
     const float sx = (a.w - a.x) * 0x1p-16f, sy = (b.x - a.y) * 0x1p-16f, sz = (b.y - a.z) * 0x1p-16f;
     const uint32_t ux = (uint32_t)qx, uy = (uint32_t)qy, uz = (uint32_t)qz;
     float tn;
-    return slab_cons(q_lo(a.x, sx, ux & 0xFFFFu), q_lo(a.y, sy, uy & 0xFFFFu), q_lo(a.z, sz, uz & 0xFFFFu),
-                     q_hi(a.x, a.w, sx, ux >> 16), q_hi(a.y, b.x, sy, uy >> 16), q_hi(a.z, b.y, sz, uz >> 16), sr,
+    return slab_cons(a.x + (float)(ux & 0xFFFFu) * sx, a.y + (float)(uy & 0xFFFFu) * sy, a.z + (float)(uz & 0xFFFFu) * sz,
+                     a.w - (float)(ux >> 16) * sx, b.x - (float)(uy >> 16) * sy, b.y - (float)(uz >> 16) * sz, sr,
                      minTc, tn);
 }
 template <bool ANY, bool STATS>
@@ -651,9 +650,14 @@ DEV bool walk_bvh_q(const DevScene& S, int i, const int end, const Ray& r, float
     const RayRcp q = ray_rcp(r);
     const SlabRay sr = slab_ray(r, q);
     while (i < end) {
+        // the whole 64-B record at once (one cache line): the child boxes' load must not wait
+        // for the node's own test -- a second dependent fetch per inner node is what this walk
+        // is there to remove
         const float4* R = S.nodes64 + 4 * (size_t)i;
         const float4 a = R[0];
         const float4 b = R[1];
+        const int4 cl = reinterpret_cast<const int4*>(R)[2];      // left box, right child's index
+        const int4 cr = reinterpret_cast<const int4*>(R)[3];      // right box, validity bits
         c.template node<ANY>();
         const int skip = __float_as_int(b.z);
         if (!box_hit_fast<true>(a.x, a.y, a.z, a.w, b.x, b.y, r, q, minT)) {
@@ -681,8 +685,6 @@ DEV bool walk_bvh_q(const DevScene& S, int i, const int end, const Ray& r, float
             i = skip;
             continue;
         }
-        const int4 cl = reinterpret_cast<const int4*>(R)[2];      // left box, right child's index
-        const int4 cr = reinterpret_cast<const int4*>(R)[3];      // right box, validity bits
         if (q.fast && (cr.w & 1)) {
             const float minTc = minT * (1.0f + 0x1p-21f);
             if (!q_box_cons(a, b, cl.x, cl.y, cl.z, sr, minTc)) {
