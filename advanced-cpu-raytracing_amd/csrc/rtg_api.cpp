@@ -1,7 +1,6 @@
 // C-ABI implementation (include/rtgpu.h): scene ingest, device upload, render.
 #include <hip/hip_runtime.h>
 
-#include <cfloat>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -126,7 +125,6 @@ struct rtg_scene {
     DevBuf<rtg::DevSpotLight> spot_lights;
     DevBuf<rtg::DevCounters> counters;
     DevBuf<rtg::WNode> anodes;
-    DevBuf<float4> nodes64;
     DevBuf<float4> ahtris;
     DevBuf<int> face_leaf;
     DevBuf<int> guard;                // RTG_GUARD builds: index-violation bits
@@ -438,55 +436,6 @@ static bool anyhit_trees(const rtg_scene_desc* d, const std::vector<float4>& nd,
     return ahbOk;
 }
 
-// The 64-B node records of the per-lane walk walk_bvh_q (rtg_common.hpp): per node its own
-// 32-B record, then for an inner node its children's boxes quantised conservatively relative to
-// its own box -- per axis the largest codes whose decoded bounds (lo + q * (hi - lo) * 2^-16 and
-// hi - q * (hi - lo) * 2^-16 in float, exactly as the device decodes them; q = 0: the box's own
-// bound) still contain the child's -- packed lo | hi << 16, the right child's index (skip of
-// the left child) and a validity bit per child (0: no usable code -- non-finite or tiny boxes, a
-// child outside its parent -- the child is then always fetched).
-static float qdec_lo(float lo, float s, uint32_t q) { return lo + (float)q * s; }
-static float qdec_hi(float hi, float s, uint32_t q) { return hi - (float)q * s; }
-static bool quantise_axis(float lo, float hi, float clo, float chi, uint32_t& out) {
-    const float s = (hi - lo) * 0x1p-16f;
-    if (!std::isfinite(lo) || !std::isfinite(hi) || !std::isfinite(clo) || !std::isfinite(chi)) return false;
-    if (!(s >= FLT_MIN) || clo < lo || chi > hi || clo > chi) return false;
-    const double ql = std::floor(((double)clo - lo) / s), qh = std::floor(((double)hi - chi) / s);
-    uint32_t a = (uint32_t)std::min(65535.0, std::max(0.0, ql)), b = (uint32_t)std::min(65535.0, std::max(0.0, qh));
-    while (a > 0 && qdec_lo(lo, s, a) > clo) --a;
-    while (b > 0 && qdec_hi(hi, s, b) < chi) --b;
-    if (qdec_lo(lo, s, a) > clo || qdec_hi(hi, s, b) < chi) return false;
-    out = a | (b << 16);
-    return true;
-}
-static std::vector<float4> child_records(const std::vector<float4>& nd) {
-    const size_t nn = nd.size() / 2;
-    std::vector<float4> out(4 * nn, make_float4(0.f, 0.f, 0.f, 0.f));
-    auto iv = [](float f) { int v; std::memcpy(&v, &f, 4); return v; };
-    auto fv = [](uint32_t v) { float f; std::memcpy(&f, &v, 4); return f; };
-    for (size_t i = 0; i < nn; ++i) {
-        const float4 a = nd[2 * i], b = nd[2 * i + 1];
-        out[4 * i] = a;
-        out[4 * i + 1] = b;
-        if (iv(b.w) >= 0 || i + 1 >= nn) continue;        // a leaf (or the pad node)
-        const int L = (int)i + 1, R = iv(nd[2 * L + 1].z);
-        if (R <= L || (size_t)R >= nn) continue;
-        const float lo[3] = {a.x, a.y, a.z}, hi[3] = {a.w, b.x, b.y};
-        uint32_t code[2][3] = {};
-        bool ok[2] = {true, true};
-        const int child[2] = {L, R};
-        for (int k = 0; k < 2; ++k) {
-            const float4 ca = nd[2 * child[k]], cb = nd[2 * child[k] + 1];
-            const float clo[3] = {ca.x, ca.y, ca.z}, chi[3] = {ca.w, cb.x, cb.y};
-            for (int ax = 0; ax < 3; ++ax) ok[k] = ok[k] && quantise_axis(lo[ax], hi[ax], clo[ax], chi[ax], code[k][ax]);
-        }
-        out[4 * i + 2] = make_float4(fv(code[0][0]), fv(code[0][1]), fv(code[0][2]), fv((uint32_t)R));
-        out[4 * i + 3] = make_float4(fv(code[1][0]), fv(code[1][1]), fv(code[1][2]),
-                                     fv((ok[0] ? 1u : 0u) | (ok[0] && ok[1] ? 2u : 0u)));
-    }
-    return out;
-}
-
 int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     if (!d || !out) return set_err(RTG_ERR_INVALID, "null argument");
     *out = nullptr;
@@ -627,7 +576,6 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     std::vector<float4> ahtris;
     int ahbMode = rtg::AHB_EXACT;
     std::vector<int> faceLeaf;
-    std::vector<float4> nodes64;
     for (int i = 0; i < d->num_objects; ++i) objs[i].aroot = -1;
     if (!std::getenv("RTG_NO_FAST_SHADOW") && d->num_meshes > 0) {
         std::vector<float4> dn;
@@ -650,9 +598,6 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
                 if (l == rtg::LEAF_EXT) { first = nx[p].x; cnt = nx[p].y; }
                 for (int f = first; f < first + cnt; ++f) faceLeaf[f] = p;
             }
-        // the per-lane walk's records with quantised child boxes (walk_bvh_q; RTG_QNODES=0: none)
-        const char* qn = std::getenv("RTG_QNODES");
-        if (!qn || std::strcmp(qn, "0") != 0) nodes64 = child_records(nd);
 
         // any-hit tree per mesh (anyhit_trees, rtg_ahb.cpp)
         std::vector<float4> ht;
@@ -856,7 +801,6 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     HIP_TRY(sc->anodes.upload(anodes));
     HIP_TRY(sc->ahtris.upload(ahtris));
     HIP_TRY(sc->face_leaf.upload(faceLeaf));
-    HIP_TRY(sc->nodes64.upload(nodes64));
     std::vector<rtg::DevCounters> zero(1);
     std::memset(zero.data(), 0, sizeof(rtg::DevCounters));
     HIP_TRY(sc->counters.upload(zero));
@@ -899,7 +843,6 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     HIP_TRY(hipMemset(sc->guard.p, 0, sizeof(int)));
     S.guard = sc->guard.p;
     S.face_leaf = faceLeaf.empty() ? nullptr : sc->face_leaf.p;
-    S.nodes64 = nodes64.empty() ? nullptr : sc->nodes64.p;
     HIP_TRY(hipStreamCreateWithFlags(&sc->stream, hipStreamNonBlocking));
     HIP_TRY(hipEventCreateWithFlags(&sc->done, hipEventDisableTiming));
     HIP_TRY(hipDeviceSynchronize());
@@ -1128,6 +1071,9 @@ static int ensure_defer(WaveWork& ww, size_t pixels, size_t nq) {
     const size_t cap = std::max<size_t>(2 * pixels, 1024);
     const size_t bytes = 256 + pixels * 8 + cap * 48 + nq * 4;
     HIP_TRY(hipMalloc(&ww.dq, bytes));
+    // the counters start at zero; the kernels after their last readers zero them for the next
+    // pass (k_shade: camera entries / unsettled pixels, k_shadow_fin*: shadow entries)
+    HIP_TRY(hipMemset(ww.dq, 0, 256));
     char* b = (char*)ww.dq;
     ww.W.dq_count = (int*)b;
     ww.W.hit_key = (unsigned long long*)(b + 256);

@@ -624,85 +624,6 @@ DEV bool slab_cons(float lx, float ly, float lz, float hx, float hy, float hz, c
     return (tmax > -1e-30f) & (tmax >= fmaf(tmin, 1.0f - 0x1p-21f, -1e-30f)) & (tmin < minTc);
 }
 
-// The same walk on the 64-B records of S.nodes64 (the ray trees' closest hits, C5): each record
-// is the node's own 32-B record followed by its children's boxes, quantised conservatively
-// relative to its own box (rtg_api.cpp child_records: per axis two 16-bit bounds,
-// lo + q * ext * 2^-16 rounded down / up, q = 0 / 65535 the box's own bound), the right child's
-// index and two validity bits.  The reference tests the left child right after its parent, and
-// the right child right after a failing left child, at the same minT -- so at a passing inner
-// node a child whose quantised box fails the conservative slab test (slab_cons: never stricter
-// than the exact test, and the slab test is monotone in the box) is decided there, without
-// fetching its record: the reference's decision and its count, not its dependent fetch.  A right
-// child reached after its left sibling's subtree is tested on its own record as before.
-// (lo codes count up from the node's lo, hi codes down from its hi: code 0 is the bound itself)
-DEV bool q_box_cons(float4 a, float4 b, int qx, int qy, int qz, const SlabRay& sr, float minTc) {
-    const float sx = (a.w - a.x) * 0x1p-16f, sy = (b.x - a.y) * 0x1p-16f, sz = (b.y - a.z) * 0x1p-16f;
-    const uint32_t ux = (uint32_t)qx, uy = (uint32_t)qy, uz = (uint32_t)qz;
-    float tn;
-    return slab_cons(a.x + (float)(ux & 0xFFFFu) * sx, a.y + (float)(uy & 0xFFFFu) * sy, a.z + (float)(uz & 0xFFFFu) * sz,
-                     a.w - (float)(ux >> 16) * sx, b.x - (float)(uy >> 16) * sy, b.y - (float)(uz >> 16) * sz, sr,
-                     minTc, tn);
-}
-template <bool ANY, bool STATS>
-DEV bool walk_bvh_q(const DevScene& S, int i, const int end, const Ray& r, float& minT, int& hitFace, float limit,
-                    Cnt<STATS>& c) {
-    bool hit = false;
-    const RayRcp q = ray_rcp(r);
-    const SlabRay sr = slab_ray(r, q);
-    while (i < end) {
-        // the whole 64-B record at once (one cache line): the child boxes' load must not wait
-        // for the node's own test -- a second dependent fetch per inner node is what this walk
-        // is there to remove
-        const float4* R = S.nodes64 + 4 * (size_t)i;
-        const float4 a = R[0];
-        const float4 b = R[1];
-        const int4 cl = reinterpret_cast<const int4*>(R)[2];      // left box, right child's index
-        const int4 cr = reinterpret_cast<const int4*>(R)[3];      // right box, validity bits
-        c.template node<ANY>();
-        const int skip = __float_as_int(b.z);
-        if (!box_hit_fast<true>(a.x, a.y, a.z, a.w, b.x, b.y, r, q, minT)) {
-            i = skip;
-            continue;
-        }
-        const int leaf = __float_as_int(b.w);
-        if (leaf >= 0) {
-            int first = leaf >> 8, cnt = leaf & 255;
-            if (leaf == LEAF_EXT) {
-                const int2 e = S.node_ext[i];
-                first = e.x;
-                cnt = e.y;
-            }
-            for (int f = first; f < first + cnt; ++f) {
-                c.template tri<ANY>();
-                float t;
-                if (tri_test_sel(S.tris + 3 * f, r, minT, t)) {
-                    minT = t;
-                    hitFace = f;
-                    hit = true;
-                    if (ANY && t < limit) return true;
-                }
-            }
-            i = skip;
-            continue;
-        }
-        if (q.fast && (cr.w & 1)) {
-            const float minTc = minT * (1.0f + 0x1p-21f);
-            if (!q_box_cons(a, b, cl.x, cl.y, cl.z, sr, minTc)) {
-                c.template node<ANY>();                           // the left child's test: it fails
-                if ((cr.w & 2) && !q_box_cons(a, b, cr.x, cr.y, cr.z, sr, minTc)) {
-                    c.template node<ANY>();                       // the right child's: it fails too
-                    i = skip;
-                } else {
-                    i = cl.w;
-                }
-                continue;
-            }
-        }
-        i = i + 1;
-    }
-    return hit;
-}
-
 // One step's large leaves, tested by the whole wave at once.  Every lane that reached a
 // large leaf in this step (`coop`) posts an event -- its ray, minT and leaf -- to the wave's
 // table in LDS; the (event, face) pairs of all events are dealt over the wave's lanes, and
@@ -1135,9 +1056,7 @@ struct Hit {
 // bbox test fails leaves its offset on the ray origin (instancedMesh.cpp:18-60).
 // FEAT (scene features the caller guarantees absent when the bit is clear) lets the
 // traversal kernels drop whole code paths -- and their registers -- for plain scenes.
-// QN: the per-lane walk on S.nodes64 (walk_bvh_q; the caller checks S.nodes64, scenes without
-// large leaves)
-template <bool ANY, bool STATS, int FEAT = FEAT_ALL, bool PK = false, bool DEFER = false, bool QN = false>
+template <bool ANY, bool STATS, int FEAT = FEAT_ALL, bool PK = false, bool DEFER = false>
 DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit, Hit& h, Cnt<STATS>& c,
                DeferCtx* dc = nullptr) {
     h.t = minT;
@@ -1199,8 +1118,6 @@ DEV bool trace(const DevScene& S, Ray& r, float mbTime, float minT, float limit,
         if constexpr (PK)
             found = walk_bvh_packet<ANY, STATS, RTG_PRIMARY_PACKET == 2, DEFER>(S, ob.node_begin, ob.node_end, lr, t,
                                                                                   face, limit, c, dc, k);
-        else if constexpr (QN && !(FEAT & FEAT_BIGLEAF))
-            found = walk_bvh_q<ANY, STATS>(S, ob.node_begin, ob.node_end, lr, t, face, limit, c);
         else found = walk_bvh<ANY, STATS, (FEAT & FEAT_BIGLEAF) != 0>(S, ob.node_begin, ob.node_end, lr, t, face, limit, c);
         if (found) {
             h.t = t; h.obj = k; h.face = face; h.o = r.o;
@@ -2478,7 +2395,7 @@ DEV int shadow_state_defer(const DevScene& S, const WaveBufs& W, size_t q, float
     }
     return res > 0 ? SS_OCC : 0;
 }
-template <bool STATS, int FEAT, bool FAST, bool QN = false>
+template <bool STATS, int FEAT, bool FAST>
 DEV bool shadow_occluded(const DevScene& S, const WaveBufs& W, size_t q, float4 o, float4 d, Cnt<STATS>& cn) {
     Ray r;
     r.o = mk(o.x, o.y, o.z);
@@ -2493,13 +2410,12 @@ DEV bool shadow_occluded(const DevScene& S, const WaveBufs& W, size_t q, float4 
         }
     } else {
         Hit h;
-        res = trace<true, STATS, FEAT, false, false, QN>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
+        res = trace<true, STATS, FEAT>(S, r, 0.f, o.w, d.w, h, cn) ? 1 : 0;
     }
     return res > 0;
 }
 
-// QN (the ray trees' shadow rays, !FAST): the reference walk on S.nodes64 (walk_bvh_q)
-template <bool STATS, int FEAT, bool FAST, bool DEFER = false, bool QN = false>
+template <bool STATS, int FEAT, bool FAST, bool DEFER = false>
 __global__ __launch_bounds__(256, FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(FEAT)) void k_shadow(
     const DevScene S, const WaveBufs W, DevCounters* counters) {
     const int k = blockIdx.y * 256 + threadIdx.x;
@@ -2510,7 +2426,7 @@ __global__ __launch_bounds__(256, FAST ? RTG_WIDE_WAVES(FEAT) : RTG_TRACE_WAVES(
             const int st = shadow_state_defer<STATS, FEAT>(S, W, q, W.q_o[q], W.q_d[q], cn);
             W.shadow_state[q] = st;
             if (st == SS_OCC) W.occ[W.q_slot[q]] = 1;
-        } else if (shadow_occluded<STATS, FEAT, FAST, QN>(S, W, q, W.q_o[q], W.q_d[q], cn)) {
+        } else if (shadow_occluded<STATS, FEAT, FAST>(S, W, q, W.q_o[q], W.q_d[q], cn)) {
             W.occ[W.q_slot[q]] = 1;
         }
     }

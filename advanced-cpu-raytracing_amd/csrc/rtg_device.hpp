@@ -163,7 +163,6 @@ struct DevScene {
     const WNode* __restrict__ anodes;  // any-hit tree (null: shadow rays take the reference walk)
     const float4* __restrict__ ahtris; // its leaf entries: face record, reference leaf node in [0].w
     const int* __restrict__ face_leaf; // per face: its leaf node
-    const float4* __restrict__ nodes64; // per node 64 B: its record + quantised child boxes (walk_bvh_q); null: none
     int exact_shadow;                  // RTG_RENDER_EXACT_SHADOW: shadow rays take the reference walk
     int ahb_split;                     // the any-hit tree splits large leaves (AHB_SPLIT)
     int ordered;                       // RTG_RENDER_ORDERED (plain mesh scenes with an any-hit tree)

@@ -66,9 +66,9 @@ __global__ __launch_bounds__(256) void k_tree_gen(const DevCamera C, const Rende
 // Closest hit of every ray of the level: the per-lane reference walk (the levels below the
 // camera's are incoherent -- round 5 measured packets on level 0 or on every level, the checked
 // closest-hit walk of the any-hit tree and a persistent refilling walk, all slower:
-// profiles/r05g_c5_tree_walks_ab.txt, r05y_c5_closest_ab.txt, r05z_c5_persistent_ab.txt)
-// QN: the walk on the 64-B records with quantised child boxes (walk_bvh_q, S.nodes64)
-template <bool STATS, int FEAT, bool QN = false>
+// profiles/r05g_c5_tree_walks_ab.txt, r05y_c5_closest_ab.txt, r05z_c5_persistent_ab.txt; round 6,
+// 64-B node records with quantised child boxes: C5 1 780 -> 1 575 Mrays/s, r06h_c5_qnodes_ab.txt)
+template <bool STATS, int FEAT>
 __global__ __launch_bounds__(256, RTG_TRACE_WAVES(FEAT)) void k_tree_trace(const DevScene S, const TreeLevel L,
                                                                            const int level, DevCounters* counters) {
     const int i = blockIdx.x * 256 + threadIdx.x;
@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256, RTG_TRACE_WAVES(FEAT)) void k_tree_trace(const
         if (level == 0) cn.cam();
         else cn.sec();
         Hit h;
-        trace<false, STATS, FEAT, false, false, QN>(S, r, 0.f, INFINITY, INFINITY, h, cn);
+        trace<false, STATS, FEAT>(S, r, 0.f, INFINITY, INFINITY, h, cn);
         L.t[i] = h.t;
         L.obj[i] = h.obj;
         L.face[i] = h.face;
@@ -590,10 +590,7 @@ static void level_launches(TreeState& T, const DevScene& S, const DevCamera& C, 
                            int level, TreeLevel& L, int blocks, int ns, int* next_n, int cap_next, DevCounters* cnt,
                            hipStream_t st) {
     if (level == 0) hipLaunchKernelGGL(k_tree_gen, dim3(blocks), dim3(256), 0, st, C, P, s, L);
-    if (S.nodes64 && !(FEAT & FEAT_BIGLEAF))
-        hipLaunchKernelGGL((k_tree_trace<STATS, FEAT, true>), dim3(blocks), dim3(256), 0, st, S, L, level, cnt);
-    else
-        hipLaunchKernelGGL((k_tree_trace<STATS, FEAT>), dim3(blocks), dim3(256), 0, st, S, L, level, cnt);
+    hipLaunchKernelGGL((k_tree_trace<STATS, FEAT>), dim3(blocks), dim3(256), 0, st, S, L, level, cnt);
     if ((T.sk & ~SK_TEX) == 0)
         hipLaunchKernelGGL((k_tree_shade<STATS, SK_TEX>), dim3(blocks), dim3(256), 0, st, S, C, L, level, P, T.G, cnt);
     else
@@ -605,11 +602,7 @@ static void level_launches(TreeState& T, const DevScene& S, const DevCamera& C, 
         W.num_slots = ns;
         W.hit_obj = L.obj;              // the hits the shadow rays leave (their origin leaf)
         W.hit_face = L.face;
-        if (S.nodes64 && !(FEAT & FEAT_BIGLEAF))
-            hipLaunchKernelGGL((k_shadow<STATS, FEAT, false, false, true>), dim3(blocks, ns), dim3(256), 0, st, S, W,
-                               cnt);
-        else
-            hipLaunchKernelGGL((k_shadow<STATS, FEAT, false>), dim3(blocks, ns), dim3(256), 0, st, S, W, cnt);
+        hipLaunchKernelGGL((k_shadow<STATS, FEAT, false>), dim3(blocks, ns), dim3(256), 0, st, S, W, cnt);
     }
     hipLaunchKernelGGL(k_tree_scan, dim3(1), dim3(1024), 0, st, T.G.c_count, blocks, T.offs, next_n, cap_next,
                        T.d_counts ? T.d_counts + kMaxLevels : nullptr);

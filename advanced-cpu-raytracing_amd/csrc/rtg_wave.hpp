@@ -404,6 +404,12 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
         }
     }
     const int obj = FRAME ? fh.obj : (valid ? W.hit_obj[i] : -1);
+    // the camera walk's deferral counters back to zero for the next pass (k_bigleaf / k_refwalk,
+    // their last readers, ran before this kernel; no memset launch per pass)
+    if (!FRAME && W.dq_e && blockIdx.x == 0 && threadIdx.x == 0) {
+        W.dq_count[0] = 0;
+        W.dq_count[1] = 0;
+    }
     // lanes that need the light loop
     bool lit = false;
     ShadeCtx c;
@@ -722,6 +728,7 @@ __global__ __launch_bounds__(256) void k_shadow_fin_one(const DevScene S, const 
     const int slab = (int)(blockIdx.x / (unsigned)P.slab_tiles);
     const int k = threadIdx.x;
     const size_t q = (size_t)blockIdx.x * 256 + k;
+    if (blockIdx.x == 0 && k == 0) W.dq_count[2] = 0;   // (k_bigleaf_any, its last reader, is done)
     if (k >= W.q_count[blockIdx.x]) return;
     const int st = W.shadow_state[q];
     if (!(st & SS_PENDING)) return;
@@ -743,6 +750,7 @@ template <int FEAT>
 __global__ __launch_bounds__(256) void k_shadow_fin(const DevScene S, const WaveBufs W) {
     const int k = blockIdx.y * 256 + threadIdx.x;
     const size_t q = ((size_t)blockIdx.x * W.num_slots) * 256 + k;
+    if (blockIdx.x == 0 && blockIdx.y == 0 && threadIdx.x == 0) W.dq_count[2] = 0;   // (as k_shadow_fin_one)
     if (k >= W.q_count[blockIdx.x]) return;
     const int st = W.shadow_state[q];
     if (!(st & SS_PENDING)) return;
@@ -824,7 +832,6 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
         // large-leaf scenes: the camera walk defers large leaves (k_bigleaf, k_hitfix; production
         // renders only -- counting renders keep the cooperative walk and the reference's counts)
         bool deferred = false;
-        if (W.dq_e) (void)hipMemsetAsync(W.dq_count, 0, 4 * sizeof(int), st);
         if constexpr (!STATS && (FEAT & FEAT_BIGLEAF) != 0) {
             if (!ordered && !frame && W.dq_e && S.face_leaf && S.num_objects < 4096 && S.num_faces < (1 << 20)) {
                 hipLaunchKernelGGL((k_primary<STATS, FEAT, false, true>), dim3(nb), dim3(256), 0, st, S, C, Pp, s, W, cnt);
@@ -832,7 +839,9 @@ hipError_t launch_wave_t(const DevScene& S, const DevCamera& C, const RenderPara
                 hipLaunchKernelGGL((k_hitfix<FEAT>), dim3(nb), dim3(256), 0, st, S, C, Pp, s, W,
                                    defer_diag() ? cnt : nullptr);
                 // (one unsettled pixel's reference walk per wave, grid-stride: C4 has ~2 000 per
-                // sample; 256 or 2 048 blocks per sample measured the same, profiles/r05g_c4_refwalk_ab.txt)
+                // sample; 256 or 2 048 blocks per sample measured the same, profiles/r05g_c4_refwalk_ab.txt;
+                // round 6: both settled inside k_shade instead -- C3 +0.4 %, C4 -2.4 % (k_shade's
+                // registers), profiles/r06j_shade_settle_ab.txt)
                 hipLaunchKernelGGL((k_refwalk<FEAT>), dim3(256 * Pp.slabs), dim3(256), 0, st, S, C, Pp, s, W);
                 deferred = true;
             }

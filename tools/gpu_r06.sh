@@ -36,6 +36,19 @@ for s in "${steps[@]}"; do
       run bench 600 python bench.py $extra ;;
     prof)
       run prof 300 rocprofv3 --kernel-trace --stats --output-format csv -d $out/prof -o run -- python bench.py --steps 20 --warmup 3 --inflight 1 --no-cpu-baseline --no-sweep --no-extras $extra ;;
+    trace:*)
+      # kernel trace of a configuration's bench run with its frame parts, grouped by grid size
+      c=${s#trace:}
+      run trace_$c 600 rocprofv3 --kernel-trace --output-format csv -d $out/trace_$c -o run -- python bench.py --config $c --steps 20 --warmup 2 --no-cpu-baseline $extra
+      run groups_$c 120 python tools/trace_groups.py $out/trace_$c/run_kernel_trace.csv $out/trace_$c/groups.txt
+      find $out/trace_$c -name "*kernel_trace.csv" -delete ;;
+    ptrace:*)
+      # a configuration's frame and its parts of 8 rendered one at a time (tools/diag_parts_serial.py),
+      # kernel-traced and grouped by grid size
+      c=${s#ptrace:}
+      run ptrace_$c 400 rocprofv3 --kernel-trace --output-format csv -d $PWD/$out/ptrace_$c -o run -- python tools/diag_parts_serial.py $c 8 10
+      run pgroups_$c 120 python tools/trace_groups.py $out/ptrace_$c/run_kernel_trace.csv $out/ptrace_$c/groups.txt
+      find $out/ptrace_$c -name "*kernel_trace.csv" -delete ;;
     pmc|pmc:*)
       # counter passes (one rocprofv3 --pmc run per group) + one kernel-trace pass of the same
       # bench invocation; pmc:<name> puts them under $out/pmc_<name>/ (tools/pmc_kernels.py)
@@ -80,6 +93,25 @@ for s in "${steps[@]}"; do
         else
           run cfg_$c 400 python bench.py --config $c $cpu $extra
         fi
+      done ;;
+    inflight:*)
+      # one configuration at several frames in flight ($INFLIGHT, default 1 2 4)
+      c=${s#inflight:}
+      for f in ${INFLIGHT:-1 2 4}; do
+        run inflight_${c}_$f 600 python bench.py --config $c --inflight $f --steps ${CFG_STEPS:-4} --warmup 1 --no-extras --no-cpu-baseline --no-sweep $extra
+      done ;;
+    abparts)
+      # library A/B ($AB_LIBS, "base" = librtgpu.so) on one configuration ($ABCFG, default c3) with
+      # its parts (bench extras), twice interleaved, then each library's serial parts (diag_parts_serial)
+      for rep in 1 2; do
+        for l in $AB_LIBS; do
+          lib=""; [ $l != base ] && lib=$PWD/advanced-cpu-raytracing_amd/$l
+          run abparts_${l}_$rep 400 env RTGPU_LIB=$lib python bench.py --config ${ABCFG:-c3} --no-cpu-baseline --no-sweep --steps 10 $extra
+        done
+      done
+      for l in $AB_LIBS; do
+        lib=""; [ $l != base ] && lib=$PWD/advanced-cpu-raytracing_amd/$l
+        run abserial_$l 300 env RTGPU_LIB=$lib python tools/diag_parts_serial.py ${ABCFG:-c3} 8 10
       done ;;
     ab)
       run ab 1500 bash tools/gpu_ab_head.sh $tag/ab $AB_LIBS ;;

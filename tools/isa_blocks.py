@@ -62,6 +62,8 @@ def main():
             continue
         c = classify(s)
         cur["n"][c] = cur["n"].get(c, 0) + 1
+        if s.startswith("scratch_"):
+            cur["n"]["scratch"] = cur["n"].get("scratch", 0) + 1
     tot = {}
     for b in blocks:
         n = b["n"]
@@ -69,7 +71,8 @@ def main():
             tot[k] = tot.get(k, 0) + v
         depth = re.findall(r"Depth=(\d)", b["note"])
         print(f"{b['name']:12s} d{max(depth) if depth else 0} " +
-              " ".join(f"{k}={n.get(k, 0)}" for k in ("salu", "valu", "smem", "vmem", "lds", "branch")))
+              " ".join(f"{k}={n.get(k, 0)}" for k in ("salu", "valu", "smem", "vmem", "lds", "branch")) +
+              (f" scratch={n['scratch']}" if n.get("scratch") else ""))
     print("total", tot)
 
 
