@@ -539,7 +539,16 @@ struct TreeState {
     std::vector<size_t> plan;
     std::vector<long long> plan_key;
     int sk = SK_ALL;            // the scene's shading features (k_tree_shade variant)
+    // two-stream planned passes (tree_streams): the odd passes' level buffers and their stream;
+    // fork / join events and one "resolve done" event per stream (sample order of the resolves)
+    TreeState* twin = nullptr;
+    hipStream_t st2 = nullptr;
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_res[2] = {nullptr, nullptr};
     ~TreeState() {
+        delete twin;
+        if (st2) (void)hipStreamDestroy(st2);
+        for (hipEvent_t e : {ev_fork, ev_join, ev_res[0], ev_res[1]})
+            if (e) (void)hipEventDestroy(e);
         auto f = [](void* p) { if (p) (void)hipFree(p); };
         for (auto& lv : levels) {
             TreeLevel& L = lv.L;
@@ -662,10 +671,13 @@ static hipError_t tree_pass_sync(TreeState& T, const DevScene& S, const DevCamer
 // on the device (written by the previous level's scan), blocks past it exit at once.  A level
 // that outgrows its capacity, or children past the planned depth, set the overflow flag; the
 // caller checks it once per render and redoes the render host-driven.
+// wait_res / rec_res (two-stream passes): the resolve phase waits for the previous pass's
+// resolves (the other stream) and marks its own end -- the accumulation stays in sample order.
 template <bool STATS, int FEAT>
 static hipError_t tree_pass_async(TreeState& T, const DevScene& S, const DevCamera& C, const RenderParams& P, int s,
                                   bool first, bool last, float* hdr, unsigned char* l, float4* accum,
-                                  DevCounters* cnt, hipStream_t st, hipEvent_t* ev) {
+                                  DevCounters* cnt, hipStream_t st, hipEvent_t* ev, hipEvent_t wait_res = nullptr,
+                                  hipEvent_t rec_res = nullptr) {
     const int ns = S.num_point + S.num_area + S.num_env + S.num_dir + S.num_spot + S.num_mesh;
     const int D = (int)T.plan.size();
     if (ev) (void)hipEventRecord(ev[0], st);
@@ -686,6 +698,7 @@ static hipError_t tree_pass_async(TreeState& T, const DevScene& S, const DevCame
         }
     }
     if (ev) (void)hipEventRecord(ev[1], st);
+    if (wait_res) (void)hipStreamWaitEvent(st, wait_res, 0);
     for (int lv = D - 1; lv >= 0; --lv) {
         const TreeLevel& L = T.levels[lv].L;
         const TreeLevel& Lc = lv + 1 < D ? T.levels[lv + 1].L : L;
@@ -698,8 +711,20 @@ static hipError_t tree_pass_async(TreeState& T, const DevScene& S, const DevCame
         hipLaunchKernelGGL(k_tree_accum, dim3((npix + 255) / 256), dim3(256), 0, st, C, P, s, (int)first, (int)last,
                            T.levels[0].L, hdr, l, accum);
     }
+    if (rec_res) (void)hipEventRecord(rec_res, st);
     if (ev) (void)hipEventRecord(ev[2], st);
     return hipGetLastError();
+}
+
+// Planned passes on two streams (RTG_TREE_STREAMS, default 2; 1: one stream): pass k runs on the
+// render's stream (even k) or a second one with its own level buffers (odd k), so one pass's
+// level boundaries -- the tails of its trace / shade / shadow grids, the one-block scan -- are
+// filled by the other pass's work.  The resolves wait for the previous pass's resolves, so the
+// accumulation keeps its sample order (the same bits as one stream); a pass with timing events
+// (the render's last) and host-driven passes run on the render's stream after a join.
+static int tree_streams() {
+    const char* e = std::getenv("RTG_TREE_STREAMS");
+    return e && std::strcmp(e, "1") == 0 ? 1 : 2;
 }
 
 // RTG_TREE_SYNC=1: every pass host-driven (one synchronisation per level; A/B)
@@ -718,16 +743,33 @@ static hipError_t tree_run(TreeState& T, const DevScene& S, const DevCamera& C, 
     // sizes): two cameras of a scene at the same size keep apart
     const std::vector<long long> key = {P.row_begin, P.row_end, P.part_index, P.part_count, C.width, C.height,
                                         (long long)(size_t)S.objects, S.max_depth, (long long)camera_hash(C), P.slabs};
-    auto prepare = [&]() -> hipError_t {
+    const bool two = tree_streams() == 2 && !STATS;
+    auto prepare_one = [&](TreeState& U) -> hipError_t {
         // capacities and block segments of the plan; the overflow flag cleared
         hipError_t r;
-        for (size_t lv = 0; lv < T.plan.size(); ++lv) {
-            if (T.levels.size() <= lv) T.levels.emplace_back();
-            if ((r = ensure_level(T.levels[lv], T.plan[lv], ns)) != hipSuccess) return r;
+        for (size_t lv = 0; lv < U.plan.size(); ++lv) {
+            if (U.levels.size() <= lv) U.levels.emplace_back();
+            if ((r = ensure_level(U.levels[lv], U.plan[lv], ns)) != hipSuccess) return r;
         }
-        if ((r = ensure_segs(T, (*std::max_element(T.plan.begin(), T.plan.end()) + 255) / 256, ns)) != hipSuccess)
+        if ((r = ensure_segs(U, (*std::max_element(U.plan.begin(), U.plan.end()) + 255) / 256, ns)) != hipSuccess)
             return r;
-        return hipMemsetAsync(T.d_counts + kMaxLevels, 0, sizeof(int), st);
+        return hipMemsetAsync(U.d_counts + kMaxLevels, 0, sizeof(int), st);
+    };
+    auto prepare = [&]() -> hipError_t {
+        hipError_t r;
+        if ((r = prepare_one(T)) != hipSuccess || !two) return r;
+        if (!T.twin) T.twin = new TreeState();
+        TreeState& U = *T.twin;
+        if (!U.d_counts && (r = hipMalloc(&U.d_counts, (kMaxLevels + 1) * sizeof(int))) != hipSuccess) return r;
+        if (!T.st2) {
+            if ((r = hipStreamCreateWithFlags(&T.st2, hipStreamNonBlocking)) != hipSuccess) return r;
+            for (hipEvent_t* pe : {&T.ev_fork, &T.ev_join, &T.ev_res[0], &T.ev_res[1]})
+                if ((r = hipEventCreateWithFlags(pe, hipEventDisableTiming)) != hipSuccess) return r;
+        }
+        U.sk = T.sk;
+        U.plan = T.plan;
+        U.plan_key = T.plan_key;
+        return prepare_one(U);
     };
     auto make_plan = [&](const std::vector<size_t>& seen) {
         // the level sizes seen, with a margin for sampled (stochastic) trees
@@ -750,6 +792,14 @@ static hipError_t tree_run(TreeState& T, const DevScene& S, const DevCamera& C, 
         bool any_async = false;
         if (planned && (e = prepare()) != hipSuccess) return e;
         std::vector<size_t> seen;
+        int n_async = 0;                 // planned passes issued (their parity picks the stream)
+        bool forked = false, used2 = false;
+        auto join = [&]() {              // the render's stream waits for the second one
+            if (!forked) return;
+            (void)hipEventRecord(T.ev_join, T.st2);
+            (void)hipStreamWaitEvent(st, T.ev_join, 0);
+            forked = false;
+        };
         // passes of P.slabs consecutive samples; a shorter last pass (what is left) runs
         // host-driven: its level sizes are not the plan's
         const int s_end = P.sample_begin + P.sample_count;
@@ -759,9 +809,21 @@ static hipError_t tree_run(TreeState& T, const DevScene& S, const DevCamera& C, 
             const bool first = s == P.sample_begin, last = s + Pp.slabs == s_end;
             hipEvent_t* pev = last ? ev : nullptr;
             if (planned && Pp.slabs == P.slabs) {
-                e = tree_pass_async<STATS, FEAT>(T, S, C, Pp, s, first, last, hdr, l, accum, cnt, st, pev);
+                if (two && !forked && !pev) {  // (before this pass: the next one may overlap it)
+                    (void)hipEventRecord(T.ev_fork, st);
+                    (void)hipStreamWaitEvent(T.st2, T.ev_fork, 0);
+                    forked = used2 = true;
+                }
+                const bool on2 = two && (n_async & 1) && !pev;
+                if (pev) join();         // the timed pass alone on the render's stream
+                hipEvent_t wait = two && n_async > 0 ? T.ev_res[(n_async - 1) & 1] : nullptr;
+                hipEvent_t rec = two ? T.ev_res[n_async & 1] : nullptr;
+                e = tree_pass_async<STATS, FEAT>(on2 ? *T.twin : T, S, C, Pp, s, first, last, hdr, l, accum, cnt,
+                                                 on2 ? T.st2 : st, pev, wait, rec);
                 any_async = true;
+                ++n_async;
             } else if (planned) {
+                join();
                 // (the render's last pass: the planned passes before it are untouched -- buffers
                 // only grow -- and the next render re-prepares the plan)
                 std::vector<size_t> sizes;
@@ -779,16 +841,21 @@ static hipError_t tree_run(TreeState& T, const DevScene& S, const DevCamera& C, 
             }
             if (e != hipSuccess) return e;
         }
+        join();
         if (!any_async) {
             if (!seen.empty()) make_plan(seen);
             return hipSuccess;
         }
-        // one synchronisation per render: did a level outgrow the plan?
+        // one synchronisation per render: did a level outgrow the plan (on either stream's buffers)?
+        T.h_total[0] = 0;
         if ((e = hipMemcpyAsync(T.h_total + 1, T.d_counts + kMaxLevels, sizeof(int), hipMemcpyDeviceToHost, st)) !=
             hipSuccess)
             return e;
+        if (used2 && (e = hipMemcpyAsync(T.h_total, T.twin->d_counts + kMaxLevels, sizeof(int),
+                                         hipMemcpyDeviceToHost, st)) != hipSuccess)
+            return e;
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-        if (T.h_total[1] == 0) return hipSuccess;
+        if (T.h_total[1] == 0 && T.h_total[0] == 0) return hipSuccess;
         T.plan.clear();
     }
     return hipSuccess;
