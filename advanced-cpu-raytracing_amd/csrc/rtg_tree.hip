@@ -531,7 +531,7 @@ struct TreeState {
     TreeSegs G{};
     size_t c_qo = 0, c_qd = 0, c_qs = 0, c_qc = 0, c_o = 0, c_d = 0, c_k = 0, c_m = 0, c_p = 0, c_cc = 0, c_off = 0;
     int* offs = nullptr;
-    int* h_total = nullptr;     // pinned host words: [0] a level's size, [1] the overflow flag
+    int* h_total = nullptr;     // pinned host words: [0] a level's size, [1..4] the streams' overflow flags
     // device-driven levels: per level the ray count (written by the previous level's scan) and
     // the overflow flag; the plan = capacities per level learned from a host-driven pass of
     // the same frame part (plan_key)
@@ -539,14 +539,14 @@ struct TreeState {
     std::vector<size_t> plan;
     std::vector<long long> plan_key;
     int sk = SK_ALL;            // the scene's shading features (k_tree_shade variant)
-    // two-stream planned passes (tree_streams): the odd passes' level buffers and their stream;
-    // fork / join events and one "resolve done" event per stream (sample order of the resolves)
-    TreeState* twin = nullptr;
-    hipStream_t st2 = nullptr;
+    // multi-stream planned passes (tree_streams): the other streams' level buffers and the
+    // streams; fork / join events and two "resolve done" events (sample order of the resolves)
+    std::vector<TreeState*> twins;
+    std::vector<hipStream_t> xst;
     hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_res[2] = {nullptr, nullptr};
     ~TreeState() {
-        delete twin;
-        if (st2) (void)hipStreamDestroy(st2);
+        for (TreeState* t : twins) delete t;
+        for (hipStream_t x : xst) (void)hipStreamDestroy(x);
         for (hipEvent_t e : {ev_fork, ev_join, ev_res[0], ev_res[1]})
             if (e) (void)hipEventDestroy(e);
         auto f = [](void* p) { if (p) (void)hipFree(p); };
@@ -716,15 +716,17 @@ static hipError_t tree_pass_async(TreeState& T, const DevScene& S, const DevCame
     return hipGetLastError();
 }
 
-// Planned passes on two streams (RTG_TREE_STREAMS, default 2; 1: one stream): pass k runs on the
-// render's stream (even k) or a second one with its own level buffers (odd k), so one pass's
-// level boundaries -- the tails of its trace / shade / shadow grids, the one-block scan -- are
-// filled by the other pass's work.  The resolves wait for the previous pass's resolves, so the
-// accumulation keeps its sample order (the same bits as one stream); a pass with timing events
-// (the render's last) and host-driven passes run on the render's stream after a join.
+// Planned passes on several streams (RTG_TREE_STREAMS, default 2, at most 4; 1: one stream):
+// pass k runs on stream k mod N (stream 0 the render's), each with its own level buffers, so one
+// pass's level boundaries -- the tails of its trace / shade / shadow grids, the one-block scan,
+// the small deep levels -- are filled by the others' work (C5: 1 789 -> 2 235 Mrays/s with two,
+// profiles/r06l_c5_two_streams_ab.txt).  The resolves wait for the previous pass's resolves, so
+// the accumulation keeps its sample order (the same bits as one stream); a pass with timing
+// events (the render's last) and host-driven passes run on the render's stream after a join.
 static int tree_streams() {
     const char* e = std::getenv("RTG_TREE_STREAMS");
-    return e && std::strcmp(e, "1") == 0 ? 1 : 2;
+    const int n = e ? std::atoi(e) : 2;
+    return n < 1 ? 1 : n > 4 ? 4 : n;
 }
 
 // RTG_TREE_SYNC=1: every pass host-driven (one synchronisation per level; A/B)
@@ -735,7 +737,7 @@ static hipError_t tree_run(TreeState& T, const DevScene& S, const DevCamera& C, 
                            unsigned char* l, float4* accum, DevCounters* cnt, hipStream_t st, hipEvent_t* ev) {
     hipError_t e;
     if (!T.h_total) {
-        if ((e = hipHostMalloc(&T.h_total, 2 * sizeof(int))) != hipSuccess) return e;
+        if ((e = hipHostMalloc(&T.h_total, 8 * sizeof(int))) != hipSuccess) return e;
         if ((e = hipMalloc(&T.d_counts, (kMaxLevels + 1) * sizeof(int))) != hipSuccess) return e;
     }
     const int ns = S.num_point + S.num_area + S.num_env + S.num_dir + S.num_spot + S.num_mesh;
@@ -743,7 +745,7 @@ static hipError_t tree_run(TreeState& T, const DevScene& S, const DevCamera& C, 
     // sizes): two cameras of a scene at the same size keep apart
     const std::vector<long long> key = {P.row_begin, P.row_end, P.part_index, P.part_count, C.width, C.height,
                                         (long long)(size_t)S.objects, S.max_depth, (long long)camera_hash(C), P.slabs};
-    const bool two = tree_streams() == 2 && !STATS;
+    const int NS = STATS ? 1 : tree_streams();
     auto prepare_one = [&](TreeState& U) -> hipError_t {
         // capacities and block segments of the plan; the overflow flag cleared
         hipError_t r;
@@ -757,19 +759,25 @@ static hipError_t tree_run(TreeState& T, const DevScene& S, const DevCamera& C, 
     };
     auto prepare = [&]() -> hipError_t {
         hipError_t r;
-        if ((r = prepare_one(T)) != hipSuccess || !two) return r;
-        if (!T.twin) T.twin = new TreeState();
-        TreeState& U = *T.twin;
-        if (!U.d_counts && (r = hipMalloc(&U.d_counts, (kMaxLevels + 1) * sizeof(int))) != hipSuccess) return r;
-        if (!T.st2) {
-            if ((r = hipStreamCreateWithFlags(&T.st2, hipStreamNonBlocking)) != hipSuccess) return r;
+        if ((r = prepare_one(T)) != hipSuccess || NS == 1) return r;
+        if (!T.ev_fork)
             for (hipEvent_t* pe : {&T.ev_fork, &T.ev_join, &T.ev_res[0], &T.ev_res[1]})
                 if ((r = hipEventCreateWithFlags(pe, hipEventDisableTiming)) != hipSuccess) return r;
+        while ((int)T.twins.size() < NS - 1) {
+            hipStream_t x;
+            if ((r = hipStreamCreateWithFlags(&x, hipStreamNonBlocking)) != hipSuccess) return r;
+            T.xst.push_back(x);
+            T.twins.push_back(new TreeState());
         }
-        U.sk = T.sk;
-        U.plan = T.plan;
-        U.plan_key = T.plan_key;
-        return prepare_one(U);
+        for (int k = 0; k < NS - 1; ++k) {
+            TreeState& U = *T.twins[k];
+            if (!U.d_counts && (r = hipMalloc(&U.d_counts, (kMaxLevels + 1) * sizeof(int))) != hipSuccess) return r;
+            U.sk = T.sk;
+            U.plan = T.plan;
+            U.plan_key = T.plan_key;
+            if ((r = prepare_one(U)) != hipSuccess) return r;
+        }
+        return hipSuccess;
     };
     auto make_plan = [&](const std::vector<size_t>& seen) {
         // the level sizes seen, with a margin for sampled (stochastic) trees
@@ -794,10 +802,12 @@ static hipError_t tree_run(TreeState& T, const DevScene& S, const DevCamera& C, 
         std::vector<size_t> seen;
         int n_async = 0;                 // planned passes issued (their parity picks the stream)
         bool forked = false, used2 = false;
-        auto join = [&]() {              // the render's stream waits for the second one
+        auto join = [&]() {              // the render's stream waits for the others
             if (!forked) return;
-            (void)hipEventRecord(T.ev_join, T.st2);
-            (void)hipStreamWaitEvent(st, T.ev_join, 0);
+            for (int k = 0; k < NS - 1; ++k) {
+                (void)hipEventRecord(T.ev_join, T.xst[k]);
+                (void)hipStreamWaitEvent(st, T.ev_join, 0);
+            }
             forked = false;
         };
         // passes of P.slabs consecutive samples; a shorter last pass (what is left) runs
@@ -809,17 +819,17 @@ static hipError_t tree_run(TreeState& T, const DevScene& S, const DevCamera& C, 
             const bool first = s == P.sample_begin, last = s + Pp.slabs == s_end;
             hipEvent_t* pev = last ? ev : nullptr;
             if (planned && Pp.slabs == P.slabs) {
-                if (two && !forked && !pev) {  // (before this pass: the next one may overlap it)
+                if (NS > 1 && !forked && !pev) {  // (before this pass: the next ones may overlap it)
                     (void)hipEventRecord(T.ev_fork, st);
-                    (void)hipStreamWaitEvent(T.st2, T.ev_fork, 0);
+                    for (int k = 0; k < NS - 1; ++k) (void)hipStreamWaitEvent(T.xst[k], T.ev_fork, 0);
                     forked = used2 = true;
                 }
-                const bool on2 = two && (n_async & 1) && !pev;
+                const int sx = pev ? 0 : n_async % NS;     // stream (and level buffers) of this pass
                 if (pev) join();         // the timed pass alone on the render's stream
-                hipEvent_t wait = two && n_async > 0 ? T.ev_res[(n_async - 1) & 1] : nullptr;
-                hipEvent_t rec = two ? T.ev_res[n_async & 1] : nullptr;
-                e = tree_pass_async<STATS, FEAT>(on2 ? *T.twin : T, S, C, Pp, s, first, last, hdr, l, accum, cnt,
-                                                 on2 ? T.st2 : st, pev, wait, rec);
+                hipEvent_t wait = NS > 1 && n_async > 0 ? T.ev_res[(n_async - 1) & 1] : nullptr;
+                hipEvent_t rec = NS > 1 ? T.ev_res[n_async & 1] : nullptr;
+                e = tree_pass_async<STATS, FEAT>(sx ? *T.twins[sx - 1] : T, S, C, Pp, s, first, last, hdr, l, accum,
+                                                 cnt, sx ? T.xst[sx - 1] : st, pev, wait, rec);
                 any_async = true;
                 ++n_async;
             } else if (planned) {
@@ -846,16 +856,16 @@ static hipError_t tree_run(TreeState& T, const DevScene& S, const DevCamera& C, 
             if (!seen.empty()) make_plan(seen);
             return hipSuccess;
         }
-        // one synchronisation per render: did a level outgrow the plan (on either stream's buffers)?
-        T.h_total[0] = 0;
-        if ((e = hipMemcpyAsync(T.h_total + 1, T.d_counts + kMaxLevels, sizeof(int), hipMemcpyDeviceToHost, st)) !=
-            hipSuccess)
-            return e;
-        if (used2 && (e = hipMemcpyAsync(T.h_total, T.twin->d_counts + kMaxLevels, sizeof(int),
-                                         hipMemcpyDeviceToHost, st)) != hipSuccess)
-            return e;
+        // one synchronisation per render: did a level outgrow the plan (on any stream's buffers)?
+        const int nf = used2 ? NS : 1;
+        for (int k = 0; k < nf; ++k)
+            if ((e = hipMemcpyAsync(T.h_total + 1 + k, (k ? T.twins[k - 1]->d_counts : T.d_counts) + kMaxLevels,
+                                    sizeof(int), hipMemcpyDeviceToHost, st)) != hipSuccess)
+                return e;
         if ((e = hipStreamSynchronize(st)) != hipSuccess) return e;
-        if (T.h_total[1] == 0 && T.h_total[0] == 0) return hipSuccess;
+        bool overflow = false;
+        for (int k = 0; k < nf; ++k) overflow |= T.h_total[1 + k] != 0;
+        if (!overflow) return hipSuccess;
         T.plan.clear();
     }
     return hipSuccess;

@@ -126,19 +126,19 @@ def test_timed_samples_reports_the_last_pass(in_tmp, monkeypatch):
 
 @pytest.mark.parametrize("name", ["c5_dragon", "cornell_dielectric", "spheres_mirror"])
 def test_tree_passes_on_two_streams(name, in_tmp, monkeypatch):
-    """The ray trees' planned passes alternate between two streams with their own level buffers
-    (rtg_tree.hip tree_streams), the resolves kept in sample order by events: the image of one
-    stream bit for bit -- with multi-sample passes, one-sample passes (many planned passes, both
-    streams in use) and a frame part."""
+    """The ray trees' planned passes rotate over several streams with their own level buffers
+    (rtg_tree.hip tree_streams), the resolves kept in sample order by events: with two or three
+    streams the image of one stream bit for bit -- with multi-sample passes, one-sample passes
+    (many planned passes, every stream in use) and a frame part."""
     xml, flags = _case(name, in_tmp)
     hs = rtgpu.HostScene(xml)
     ds = rtgpu.DeviceScene(hs, 0)
     out = {}
-    for streams in ("1", "2"):
+    for streams in ("1", "2", "3"):
         monkeypatch.setenv("RTG_TREE_STREAMS", streams)
         for extra in (0, ONE):
             ds.render(0, seed=5, flags=flags | extra)                  # makes the plan
             out[streams, extra] = ds.render(0, seed=5, flags=flags | extra)
         out[streams, "part"] = ds.render(0, seed=5, flags=flags | ONE, part=(1, 2))
     for k in (0, ONE, "part"):
-        assert _same(out["1", k], out["2", k]), k
+        assert _same(out["1", k], out["2", k]) and _same(out["1", k], out["3", k]), k

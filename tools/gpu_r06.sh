@@ -30,6 +30,10 @@ for s in "${steps[@]}"; do
     tests)
       run pytest 900 python -u -m pytest tests -v -m gpu -x --timeout 300 --timeout-method thread -s
       run smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
+    tests:*)
+      # one test file (tests/<name>.py)
+      t=${s#tests:}
+      run pytest_$t 600 python -u -m pytest tests/$t.py -v -m gpu -x --timeout 300 --timeout-method thread ;;
     slivers)
       run slivers 600 python -u tools/diag_slivers.py $out/slivers.json ;;
     bench)
