@@ -716,16 +716,16 @@ static hipError_t tree_pass_async(TreeState& T, const DevScene& S, const DevCame
     return hipGetLastError();
 }
 
-// Planned passes on several streams (RTG_TREE_STREAMS, default 2, at most 4; 1: one stream):
+// Planned passes on several streams (RTG_TREE_STREAMS, default 3, at most 4; 1: one stream):
 // pass k runs on stream k mod N (stream 0 the render's), each with its own level buffers, so one
 // pass's level boundaries -- the tails of its trace / shade / shadow grids, the one-block scan,
 // the small deep levels -- are filled by the others' work (C5: 1 789 -> 2 235 Mrays/s with two,
-// profiles/r06l_c5_two_streams_ab.txt).  The resolves wait for the previous pass's resolves, so
+// 2 270 with three, 2 232 with four; profiles/r06l_c5_two_streams_ab.txt, r06m_c5_streams_ab.txt).  The resolves wait for the previous pass's resolves, so
 // the accumulation keeps its sample order (the same bits as one stream); a pass with timing
 // events (the render's last) and host-driven passes run on the render's stream after a join.
 static int tree_streams() {
     const char* e = std::getenv("RTG_TREE_STREAMS");
-    const int n = e ? std::atoi(e) : 2;
+    const int n = e ? std::atoi(e) : 3;
     return n < 1 ? 1 : n > 4 ? 4 : n;
 }
 
