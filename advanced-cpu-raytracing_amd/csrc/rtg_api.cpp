@@ -108,6 +108,7 @@ struct rtg_scene {
     int node_count = 0;               // nodes in use (device-built BVH: <= nodes.n / 2)
     DevBuf<int2> node_ext;
     DevBuf<int> env_images;
+    DevBuf<unsigned long long> env_mix;
     DevBuf<float2> face_uv;
     DevBuf<float4> face_v12;
     DevBuf<rtg::DevMeshLight> mesh_lights;
@@ -797,6 +798,20 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     HIP_TRY(sc->textures.upload(texs)); HIP_TRY(sc->images.upload(imgs)); HIP_TRY(sc->texels.upload(pool));
     HIP_TRY(sc->point_lights.upload(pls)); HIP_TRY(sc->area_lights.upload(als)); HIP_TRY(sc->dir_lights.upload(dls));
     HIP_TRY(sc->spot_lights.upload(sls)); HIP_TRY(sc->env_images.upload(envs));
+    {
+        // env_direction's key-independent inner hashes: mix64(RP_ENV << 32 | e * 16384 + j)
+        auto mix = [](uint64_t z) {
+            z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+            z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+            return z ^ (z >> 31);
+        };
+        std::vector<unsigned long long> em((size_t)d->num_env_lights * rtg::kEnvDraws);
+        for (int e = 0; e < d->num_env_lights; ++e)
+            for (int j = 0; j < rtg::kEnvDraws; ++j)
+                em[(size_t)e * rtg::kEnvDraws + j] =
+                    mix(((uint64_t)rtg::kRpEnv << 32) | (uint32_t)((uint32_t)e * 16384u + (uint32_t)j));
+        HIP_TRY(sc->env_mix.upload(em));
+    }
     HIP_TRY(sc->mesh_lights.upload(mls)); HIP_TRY(sc->light_faces.upload(lfs));
     HIP_TRY(sc->anodes.upload(anodes));
     HIP_TRY(sc->ahtris.upload(ahtris));
@@ -822,7 +837,7 @@ int rtg_scene_create(const rtg_scene_desc* d, int device, rtg_scene** out) {
     S.objects = sc->objects.p; S.group_box = sc->group_box.p; S.materials = sc->materials.p; S.brdfs = sc->brdfs.p;
     S.textures = sc->textures.p; S.images = sc->images.p; S.texels = sc->texels.p;
     S.point_lights = sc->point_lights.p; S.area_lights = sc->area_lights.p; S.dir_lights = sc->dir_lights.p;
-    S.spot_lights = sc->spot_lights.p; S.env_images = sc->env_images.p;
+    S.spot_lights = sc->spot_lights.p; S.env_images = sc->env_images.p; S.env_mix = sc->env_mix.p;
     S.perm = sc->perm.p; S.grad = sc->grad.p;
     S.num_objects = d->num_objects; S.num_point = d->num_point_lights; S.num_area = d->num_area_lights;
     S.num_dir = d->num_dir_lights; S.num_spot = d->num_spot_lights; S.num_env = d->num_env_lights;

@@ -1870,16 +1870,93 @@ DEV f3 env_sample(const DevScene& S, int e, f3 dir) {
 
 // GetDirection (sphericalEnvironmentLight.h:36-61): rejection sampling, returns the
 // un-normalised candidate.  The reference spins forever on a NaN normal; bounded here.
-DEV f3 env_direction(f3 surfaceNormal, uint64_t key, int e) {
+// The draws are rnd(key, RP_ENV, e * 16384 + 3k + c); the inner hash of (purpose, index) does
+// not depend on the key, so it comes from a table (S.env_mix, kEnvDraws per light, built by
+// rtg_scene_create with the same mix64): one 64-bit hash per draw instead of two, the same bits.
+// A wave runs until its last lane accepts (~17 candidates for 64 lanes at acceptance pi/12),
+// and the table index is the loop counter, so the loads are scalar.
+static_assert(RP_ENV == kRpEnv, "env_mix table purpose");
+DEV float rnd_mixed(uint64_t key, uint64_t inner) {
+    const uint64_t h = mix64(key ^ inner);
+    return (float)(h >> 40) * (1.0f / 16777216.0f);
+}
+DEV f3 env_direction(const DevScene& S, f3 surfaceNormal, uint64_t key, int e) {
     f3 n = makeUnit(surfaceNormal);
     f3 cand = mk(0, 0, 0);
+    const unsigned long long* T = S.env_mix + (size_t)e * kEnvDraws;
     for (uint32_t k = 0; k < 4096; ++k) {
-        uint32_t base = (uint32_t)e * 16384u + 3u * k;
-        cand.x = 2.0f * rnd(key, RP_ENV, base) - 1.0f;
-        cand.y = 2.0f * rnd(key, RP_ENV, base + 1) - 1.0f;
-        cand.z = 2.0f * rnd(key, RP_ENV, base + 2) - 1.0f;
+        cand.x = 2.0f * rnd_mixed(key, T[3 * k]) - 1.0f;
+        cand.y = 2.0f * rnd_mixed(key, T[3 * k + 1]) - 1.0f;
+        cand.z = 2.0f * rnd_mixed(key, T[3 * k + 2]) - 1.0f;
         float length = len(cand);
         if (length <= 1.0f && dot(n, cand) > 0.0f) break;
+    }
+    return cand;
+}
+
+// The same search for a whole wave (every lane calls it; `want`: the lane needs a direction).
+// A lane's loop runs until its first accepted candidate (3.8 on average at acceptance pi/12),
+// but the wave's until its last lane's (~17 for 64 lanes); here the lanes still searching get
+// the others' help: with na of them, each gets g = 64 / na lanes testing its candidates
+// k .. k+g-1 at once, and takes the smallest accepted index -- the candidate its own loop
+// returns (the first accepted of 0..4095, else the 4095th), computed by the same operations.
+DEV f3 env_candidate(const unsigned long long* T, uint64_t key, int k) {
+    return mk(2.0f * rnd_mixed(key, T[3 * k]) - 1.0f, 2.0f * rnd_mixed(key, T[3 * k + 1]) - 1.0f,
+              2.0f * rnd_mixed(key, T[3 * k + 2]) - 1.0f);
+}
+// position of the r-th (from 0) set bit of m (r < popcount(m))
+DEV int nth_set_bit(uint64_t m, int r) {
+    int pos = 0;
+#pragma unroll
+    for (int w = 32; w >= 1; w >>= 1) {
+        const uint64_t lo = m & ((1ull << w) - 1ull);
+        const int c = __popcll(lo);
+        const bool up = r >= c;
+        r = up ? r - c : r;
+        m = up ? m >> w : lo;
+        pos = up ? pos + w : pos;
+    }
+    return pos;
+}
+DEV f3 env_direction_wave(const DevScene& S, f3 surfaceNormal, uint64_t key, int e, bool want) {
+    const f3 n = makeUnit(surfaceNormal);
+    const unsigned long long* T = S.env_mix + (size_t)e * kEnvDraws;
+    const int lane = threadIdx.x & 63;
+    int k = 0;
+    bool done = !want;
+    f3 cand = mk(0, 0, 0);
+    for (;;) {
+        const uint64_t act = __ballot(!done);
+        if (!act) break;
+        const int na = __popcll(act);
+        const int g = 64 / na;
+        const int r = lane / g;                            // the searcher this lane helps
+        const bool helper = r < na;
+        const int owner = helper ? nth_set_bit(act, r) : lane;
+        const uint64_t okey = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(key >> 32), owner) << 32) |
+                              (uint32_t)__shfl((int)(uint32_t)key, owner);
+        const f3 on = mk(__shfl(n.x, owner), __shfl(n.y, owner), __shfl(n.z, owner));
+        const int kk = __shfl(k, owner) + (lane - r * g);
+        f3 c = mk(0, 0, 0);
+        bool acc = false;
+        if (helper && kk < 4096) {
+            c = env_candidate(T, okey, kk);
+            acc = len(c) <= 1.0f && dot(on, c) > 0.0f;
+        }
+        const uint64_t am = __ballot(acc);
+        const int rank = __popcll(act & ((1ull << lane) - 1ull));
+        const uint64_t mine = done ? 0ull : (am >> (rank * g)) & (g >= 64 ? ~0ull : (1ull << g) - 1ull);
+        const int src = mine ? rank * g + __ffsll((long long)mine) - 1 : lane;
+        const f3 w = mk(__shfl(c.x, src), __shfl(c.y, src), __shfl(c.z, src));
+        if (!done) {
+            if (mine) {
+                cand = w;
+                done = true;
+            } else if ((k += g) >= 4096) {
+                cand = env_candidate(T, key, 4095);
+                done = true;
+            }
+        }
     }
     return cand;
 }
@@ -2087,7 +2164,7 @@ DEV LightSample light_sample(const DevScene& S, int slot, f3 p, f3 n, uint64_t k
         ls.w_i = w_i;
         ls.E = muls(ld3(L.radiance), L.area * lc / dSqr);
     } else if (XL && (i -= S.num_area) < S.num_env) {                     // no shadow ray (:741-755)
-        f3 sd = env_direction(n, key, i);
+        f3 sd = env_direction(S, n, key, i);
         ls.E = env_sample(S, i, sd);
         ls.w_i = n;
         ls.shadow = false;

@@ -131,6 +131,11 @@ enum : int { SK_TEX = 1, SK_BRDF = 2, SK_XLIGHT = 4, SK_ALL = 7 };
 constexpr int kCoopLeaf = RTG_COOP_LEAF;
 constexpr int kBigLeaf = 8;
 
+// env_direction's table of inner RNG hashes (rtg_common.hpp): three draws per candidate, 4 096
+// candidates per environment light, purpose RP_ENV
+constexpr int kEnvDraws = 3 * 4096;
+constexpr uint32_t kRpEnv = 5;
+
 struct DevScene {
     const float4* __restrict__ nodes;
     const int2* __restrict__ node_ext;
@@ -150,6 +155,7 @@ struct DevScene {
     const DevDirLight* __restrict__ dir_lights;
     const DevSpotLight* __restrict__ spot_lights;
     const int* __restrict__ env_images;
+    const unsigned long long* __restrict__ env_mix;   // per env light kEnvDraws inner RNG hashes (env_direction)
     const DevMeshLight* __restrict__ mesh_lights;
     const DevLightFace* __restrict__ light_faces;
     const int* __restrict__ perm;    // Perlin permutation (512) and gradients (12x3)

@@ -25,6 +25,12 @@ namespace rtg {
 
 enum { BASE_FINAL = 1, BASE_ADD_ZERO = 2 };
 
+// k_shade's environment-light directions searched by the whole wave (env_direction_wave);
+// 0: each lane's own loop (A/B)
+#ifndef RTG_ENV_WAVE
+#define RTG_ENV_WAVE 1
+#endif
+
 // ORD: RTG_RENDER_ORDERED (plain mesh scenes): the checked closest-hit walk on the any-hit tree
 // as wave packets (trace_closest_pk), the reference walk where its check fails
 #ifndef RTG_ORD_WAVES
@@ -597,8 +603,13 @@ __global__ __launch_bounds__(256, MODE >= SH_FUSED ? (FAST ? RTG_WIDE_WAVES(FEAT
     for (int l = 0; l < S.num_area; ++l, ++slot) area_light(l);
     if constexpr ((SK & SK_XLIGHT) != 0) {
         for (int l = 0; l < S.num_env; ++l, ++slot) {
+            // (the wave searches its lanes' directions together; every lane takes part)
+#if RTG_ENV_WAVE
+            const f3 sd = env_direction_wave(S, lit ? n : mk(0, 0, 1), key, l, lit);
+#else
+            const f3 sd = lit ? env_direction(S, n, key, l) : mk(0, 0, 0);
+#endif
             if (lit) {                                               // no shadow ray (:741-755)
-                f3 sd = env_direction(n, key, l);
                 put(shade<false, SK>(S, c, n, w_o, env_sample(S, l, sd)));
                 if (!ONE) W.occ[slot] = 0;
             }
