@@ -1930,6 +1930,16 @@ DEV f3 env_direction_wave(const DevScene& S, f3 surfaceNormal, uint64_t key, int
         if (!act) break;
         const int na = __popcll(act);
         const int g = 64 / na;
+        if (g == 1) {                  // more than 32 searching: each tests its own next candidate
+            if (!done) {
+                const f3 c = env_candidate(T, key, k);
+                if ((len(c) <= 1.0f && dot(n, c) > 0.0f) || ++k >= 4096) {
+                    cand = c;
+                    done = true;
+                }
+            }
+            continue;
+        }
         const int r = lane / g;                            // the searcher this lane helps
         const bool helper = r < na;
         const int owner = helper ? nth_set_bit(act, r) : lane;
