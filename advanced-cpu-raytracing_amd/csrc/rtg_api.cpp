@@ -1112,14 +1112,15 @@ static int pipeline(const rtg_scene* s, const rtg_render_opts* o, const rtg::Dev
 }
 
 // Samples per pass of the wavefront and ray-tree pipelines (RenderParams::slabs): as many as
-// keep a pass at most ~RTG_PASS_RAYS camera rays (default 8 Mi: a 1920x1080 frame of 4 samples,
-// one 3840x2160 sample), spread evenly over the passes.  A pass's launches then stay full when
+// keep a pass at most ~RTG_PASS_RAYS camera rays (default 16 Mi: a 1920x1080 frame of 8 samples,
+// two 3840x2160 samples -- against 8 Mi: C4 3 519 -> 3 563 Mrays/s in flight, 3 203 -> 3 356
+// serial, C5 2 265 -> 2 329; profiles/r06u_pass_rays_ab.txt), spread evenly over the passes.  A pass's launches then stay full when
 // a GPU renders a small part of the frame, and a frame of few passes pays the tail of its
 // slowest waves (C3's pole fans, C5's deepest trees) once per pass, not once per sample.
 // RTG_PASS_RAYS=0: one sample per pass (round 5's passes; the image is the same bit for bit).
 static int pass_slabs(const rtg::RenderParams& P, int width) {
     const char* v = std::getenv("RTG_PASS_RAYS");
-    const long long target = v ? std::atoll(v) : (8ll << 20);
+    const long long target = v ? std::atoll(v) : (16ll << 20);
     const long long px = (long long)P.part_rows * width;
     if (target <= 0 || P.sample_count <= 1 || px <= 0) return 1;
     const long long k = std::max(1ll, std::min<long long>(target / px, P.sample_count));

@@ -1,5 +1,5 @@
 """Multi-sample passes (RenderParams::slabs, rtg_api.cpp pass_slabs): the wavefront and ray-tree
-pipelines carry several consecutive samples of the rendered pixels in one pass (~8 Mi camera
+pipelines carry several consecutive samples of the rendered pixels in one pass (~16 Mi camera
 rays), so a GPU holding 1/N of a frame still launches full grids, and a frame pays the tail of
 its slowest waves once per pass.  Each pixel's colours of a pass are added to its accumulation
 in sample order (accum_samples: renderThreadMain's spp loop, main.cpp:80-121), so the image must
